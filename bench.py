@@ -1,0 +1,304 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident batched CRC32 (ENet checksum path) on MI355X.
+
+Metric (BASELINE.json): device-resident batched CRC32 GiB/s on 64 K x 1200 B
+packets (cfg2) + fraction of the HBM-read roofline.  One STEP = one launch of
+enet_hip_crc32_batch_device over one 75 MiB batch already resident in HBM.
+Steps rotate over ROTATE distinct batches (> 256 MiB in total) so the Infinity
+Cache cannot serve them.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
+
+N > 1: every rank processes its own cfg2-sized partition (independent packet
+shards, no collective on the data path: SURVEY.md §8e) -> "scaling": "weak".
+value = sum of payload bytes over all ranks / max over ranks of the timed span.
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "enet-csharp_amd"))
+
+HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E spec, 8.0 TB/s (MI355X_MICROARCH.md)
+GIB = float(1 << 30)
+METRIC = "device-resident batched CRC32 GiB/s (64K×1200B) + % HBM-read peak"
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--rotate", type=int, default=5, help="distinct resident batches cycled through")
+    ap.add_argument("--lanes", type=int, default=0, help="lanes per packet (0 = library default)")
+    ap.add_argument("--wgs", type=int, default=0, help="workgroups per CU (0 = library default)")
+    ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=3.0, help="wall budget per CPU-baseline leg")
+    return ap.parse_args(argv)
+
+
+# ------------------------------------------------------------------ distributed plumbing
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return ws, rank, local
+
+
+def dist_init(ws: int):
+    if ws <= 1:
+        return None
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    # gloo: only the barrier and the max-over-ranks timing cross ranks (no data-path collective)
+    dist.init_process_group(backend="gloo")
+    return dist
+
+
+def barrier(dist):
+    if dist is not None:
+        dist.barrier()
+
+
+def max_over_ranks(dist, x: float) -> float:
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(dist, x: float) -> float:
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def timed_region(dist, sync, steps: int, step_fn):
+    """barrier + sync | K steps | sync + barrier; returns this rank's seconds."""
+    sync()
+    barrier(dist)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step_fn(i)
+    sync()
+    t1 = time.perf_counter()
+    barrier(dist)
+    return t1 - t0
+
+
+# ------------------------------------------------------------------ the GPU engine
+
+class GpuEngine:
+    """Resident batches + launches through the C-ABI on torch's current stream."""
+
+    def __init__(self, device: int, batches, lanes: int, wgs: int):
+        import torch
+        import enethip
+        if not torch.cuda.is_available():
+            raise SystemExit("bench.py: no GPU visible -- the HIP path has no CPU fallback")
+        torch.cuda.set_device(device)
+        self.torch = torch
+        self.ctx = enethip.Context(device, lanes, wgs)
+        self.stream = torch.cuda.current_stream()
+        self.h = self.stream.cuda_stream
+        self.bufs = []
+        for b in batches:
+            self.bufs.append(dict(
+                payload=torch.from_numpy(b.payload).cuda(),
+                off=torch.from_numpy(b.off.view(np.int64)).cuda(),
+                lens=torch.from_numpy(b.lens.view(np.int32)).cuda(),
+                out=torch.zeros(b.n, dtype=torch.int32, device="cuda"),
+                n=b.n, nbytes=b.payload_bytes))
+        self.sink = torch.zeros(4, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+
+    def step(self, i: int):
+        b = self.bufs[i % len(self.bufs)]
+        self.ctx.crc32_batch_device(b["payload"], b["off"], b["lens"], b["n"], b["out"], self.h)
+
+    def probe(self, i: int):
+        b = self.bufs[i % len(self.bufs)]
+        self.ctx.read_probe_device(b["payload"], (b["payload"].numel() // 16) * 16, self.sink, self.h)
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+    def kernel_ms(self, fn, steps: int) -> tuple[float, float]:
+        """HIP events on the launch stream: (mean per-launch kernel ms, span ms per step)."""
+        torch = self.torch
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * steps)]
+        self.sync()
+        for i in range(steps):
+            ev[2 * i].record(self.stream)
+            fn(i)
+            ev[2 * i + 1].record(self.stream)
+        self.sync()
+        per = [ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(steps)]
+        span = ev[0].elapsed_time(ev[-1]) / steps
+        return float(np.mean(per)), float(span)
+
+    def outputs(self, j: int) -> np.ndarray:
+        return self.bufs[j]["out"].cpu().numpy().view(np.uint32)
+
+
+# ------------------------------------------------------------------ CPU baseline
+
+def cpu_baseline(batch, budget_s: float):
+    """The oracle's C restatement of packet.cs:142-160 (kind "port": the C# reference
+    cannot run here), timed on this host on a bounded sample of the same batch."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    lib = oracle.OracleLib()
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1))
+    res = {}
+    for label, th in (("1thread", 1), ("all", threads)):
+        # sample: the first packets of the batch, sized to ~budget_s of work
+        n = batch.n
+        t0 = time.perf_counter()
+        out = lib.batch(batch.payload, batch.off[: min(n, 4096)], batch.lens[: min(n, 4096)], threads=th)
+        dt = max(time.perf_counter() - t0, 1e-6)
+        rate = float(batch.lens[: min(n, 4096)].astype(np.uint64).sum()) / dt
+        sample_n = int(min(n, max(4096, rate * budget_s / max(1.0, float(batch.lens.mean())))))
+        reps = max(1, int(rate * budget_s / max(1.0, float(batch.lens[:sample_n].astype(np.uint64).sum()))))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            out = lib.batch(batch.payload, batch.off[:sample_n], batch.lens[:sample_n], threads=th)
+        dt = time.perf_counter() - t0
+        nbytes = float(batch.lens[:sample_n].astype(np.uint64).sum()) * reps
+        res[label] = dict(gibps=nbytes / dt / GIB, threads=th, packets=sample_n, reps=reps, seconds=dt)
+        del out
+    return res
+
+
+# ------------------------------------------------------------------ main
+
+def make_batches(cfg: str, rotate: int, rank: int):
+    from enethip import workloads
+    out = []
+    for j in range(rotate):
+        seed = workloads.SEED_PAYLOAD + 7919 * (rank * rotate + j)
+        if cfg == "cfg2":
+            out.append(workloads.fixed(65536, 1200, seed=seed, name="cfg2"))
+        else:
+            out.append(workloads.mixed(262144, 64, 1400, seed=seed, name="cfg3"))
+    return out
+
+
+def load_traffic(cfg: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/), or None."""
+    p = os.path.join(ROOT, "profiles", f"traffic_{cfg}.json")
+    try:
+        return json.load(open(p))
+    except (OSError, ValueError):
+        return None
+
+
+def main(argv=None, engine_factory=None, cpu_factory=None):
+    args = parse(argv)
+    ws, rank, local = dist_env()
+    if ws > 1 and args.gpus != ws:
+        args.gpus = ws
+    dist = dist_init(ws)
+    batches = make_batches(args.config, args.rotate, rank)
+    eng = (engine_factory or GpuEngine)(local, batches, args.lanes, args.wgs)
+
+    # correctness gate (untimed): first resident batch vs the oracle
+    eng.step(0)
+    eng.sync()
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    exp = oracle.OracleLib().batch(batches[0].payload, batches[0].off, batches[0].lens, threads=8)
+    if not (eng.outputs(0) == exp).all():
+        raise SystemExit("bench.py: GPU CRCs differ from the oracle -- refusing to report a number")
+
+    for i in range(args.warmup):
+        eng.step(i)
+    secs = timed_region(dist, eng.sync, args.steps, eng.step)
+    secs_max = max_over_ranks(dist, secs)
+    bytes_rank = float(sum(batches[i % len(batches)].payload_bytes for i in range(args.steps)))
+    bytes_all = sum_over_ranks(dist, bytes_rank)
+    value = bytes_all / secs_max / GIB
+
+    # per-launch kernel duration via HIP events on the launch stream (for the roofline)
+    k_ms, span_ms = eng.kernel_ms(eng.step, min(args.steps, 100))
+    p_ms, _ = eng.kernel_ms(eng.probe, min(args.steps, 100))
+    per_launch = float(batches[0].payload_bytes)
+    probe_bytes = float((batches[0].payload.nbytes // 16) * 16)
+    achieved = per_launch / (k_ms * 1e-3) / 1e9
+    probe = probe_bytes / (p_ms * 1e-3) / 1e9
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = (cpu_factory or cpu_baseline)(batches[0], args.cpu_seconds)
+
+    if rank == 0:
+        traffic = load_traffic(args.config)
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": ws,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(secs_max / args.steps * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (splitmix64 payload, device-resident)",
+            "config": {
+                "workload": ("cfg2: 65536 packets x 1200 B packed" if args.config == "cfg2"
+                             else "cfg3: 262144 packets x U[64,1400] B packed") +
+                            f", {args.rotate} rotating resident batches per GPU",
+                "packets_per_gpu": batches[0].n,
+                "payload_bytes_per_step": int(per_launch),
+                "parallelism": f"{ws} independent shards (no collective)",
+                "lanes_per_packet": args.lanes or "default",
+            },
+            "hbm_read_frac": round(value * GIB / 1e9 / (HBM_PEAK_GBPS * ws), 4),
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": (traffic or {}).get("hbm_bytes_per_launch"),
+                "kernel": "crc32_packets_kernel<0>",
+                "kernel_ms": round(k_ms, 5),
+                "span_ms_per_step": round(span_ms, 5),
+                "read_probe_GBps": round(probe, 1),
+            },
+            "cpu_baseline": None if cpu is None else {
+                "value": round(cpu["all"]["gibps"], 3),
+                "unit": "GiB/s",
+                "cores": cpu["all"]["threads"],
+                "kind": "port",
+                "sample": f"oracle C restatement of packet.cs:142-160, first {cpu['all']['packets']} packets "
+                          f"of the cfg batch x {cpu['all']['reps']} reps; 1 thread: "
+                          f"{cpu['1thread']['gibps']:.3f} GiB/s",
+            },
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

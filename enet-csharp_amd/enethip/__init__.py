@@ -1,0 +1,226 @@
+"""Python host binding of libenethip.so (ctypes over include/enet_hip.h).
+
+This mirrors the reference's checksum surface for Python hosts and the test /
+bench harness:
+
+* ``ENetBuffer`` / ``enet_crc32(buffers)`` -- the callback path
+  (enet-csharp/ENet/c/packet.cs:142-160, include/win32.cs:25-29), CPU, never fails.
+* ``Context`` -- one GPU: batched device-resident checksum, receive verify
+  (c/protocol.cs:1052-1068) and gather-list checksum (c/protocol.cs:1690-1698).
+* ``crc32_batch_multi`` -- independent shards over several GPUs, no collective.
+
+The GPU path has no fallback: if libenethip.so is missing or the HIP runtime
+reports an error, these calls raise ``ENetHipError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Sequence
+
+import numpy as np
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "libenethip.so")
+
+# Every symbol include/enet_hip.h declares (tests check the .so exports them all).
+EXPORTED_SYMBOLS = (
+    "enet_hip_crc32", "enet_hip_crc32_update", "enet_hip_device_count", "enet_hip_context_create",
+    "enet_hip_context_destroy", "enet_hip_error_string", "enet_hip_set_tuning",
+    "enet_hip_crc32_batch_device", "enet_hip_crc32_batch_host", "enet_hip_verify_batch_device",
+    "enet_hip_crc32_gather_device", "enet_hip_crc32_batch_multi", "enet_hip_device_alloc",
+    "enet_hip_device_free", "enet_hip_host_alloc", "enet_hip_host_free", "enet_hip_memcpy_h2d",
+    "enet_hip_memcpy_d2h", "enet_hip_synchronize", "enet_hip_read_probe_device",
+)
+
+
+class ENetHipError(RuntimeError):
+    def __init__(self, what: str, code: int):
+        super().__init__(f"{what} failed: {code} ({error_string(code)})")
+        self.code = code
+
+
+class ENetBuffer(ctypes.Structure):
+    """include/win32.cs:25-29 -- length first."""
+    _fields_ = [("dataLength", ctypes.c_size_t), ("data", ctypes.c_void_p)]
+
+
+_lib = None
+
+
+def load(path: str | None = None) -> ctypes.CDLL:
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise ENetHipError(f"load {p} (run __graft_entry__.build())", -1)
+    L = ctypes.CDLL(p)
+    vp, sz, i32, u32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint32
+    L.enet_hip_crc32.restype = u32
+    L.enet_hip_crc32.argtypes = [vp, sz]
+    L.enet_hip_crc32_update.restype = u32
+    L.enet_hip_crc32_update.argtypes = [u32, vp, sz]
+    L.enet_hip_device_count.restype = i32
+    L.enet_hip_device_count.argtypes = [ctypes.POINTER(i32)]
+    L.enet_hip_context_create.restype = i32
+    L.enet_hip_context_create.argtypes = [i32, ctypes.POINTER(vp)]
+    L.enet_hip_context_destroy.restype = i32
+    L.enet_hip_context_destroy.argtypes = [vp]
+    L.enet_hip_error_string.restype = ctypes.c_char_p
+    L.enet_hip_error_string.argtypes = [i32]
+    L.enet_hip_set_tuning.restype = i32
+    L.enet_hip_set_tuning.argtypes = [vp, i32, i32]
+    L.enet_hip_crc32_batch_device.restype = i32
+    L.enet_hip_crc32_batch_device.argtypes = [vp, vp, vp, vp, sz, vp, vp]
+    L.enet_hip_crc32_batch_host.restype = i32
+    L.enet_hip_crc32_batch_host.argtypes = [vp, vp, sz, vp, vp, sz, vp]
+    L.enet_hip_verify_batch_device.restype = i32
+    L.enet_hip_verify_batch_device.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp, vp, vp]
+    L.enet_hip_crc32_gather_device.restype = i32
+    L.enet_hip_crc32_gather_device.argtypes = [vp, vp, vp, vp, vp, sz, vp, vp]
+    L.enet_hip_crc32_batch_multi.restype = i32
+    L.enet_hip_crc32_batch_multi.argtypes = [vp, i32, vp, sz, vp, vp, sz, vp]
+    L.enet_hip_device_alloc.restype = i32
+    L.enet_hip_device_alloc.argtypes = [vp, sz, ctypes.POINTER(vp)]
+    L.enet_hip_device_free.restype = i32
+    L.enet_hip_device_free.argtypes = [vp, vp]
+    L.enet_hip_host_alloc.restype = i32
+    L.enet_hip_host_alloc.argtypes = [sz, ctypes.POINTER(vp)]
+    L.enet_hip_host_free.restype = i32
+    L.enet_hip_host_free.argtypes = [vp]
+    L.enet_hip_memcpy_h2d.restype = i32
+    L.enet_hip_memcpy_h2d.argtypes = [vp, vp, vp, sz]
+    L.enet_hip_memcpy_d2h.restype = i32
+    L.enet_hip_memcpy_d2h.argtypes = [vp, vp, vp, sz]
+    L.enet_hip_read_probe_device.restype = i32
+    L.enet_hip_read_probe_device.argtypes = [vp, vp, sz, vp, vp]
+    L.enet_hip_synchronize.restype = i32
+    L.enet_hip_synchronize.argtypes = [vp]
+    if path is None:
+        _lib = L
+    return L
+
+
+def error_string(code: int) -> str:
+    try:
+        s = load().enet_hip_error_string(int(code))
+        return s.decode() if s else "?"
+    except Exception:  # noqa: BLE001 - only used to format messages
+        return "?"
+
+
+def _check(what: str, rc: int) -> None:
+    if rc != 0:
+        raise ENetHipError(what, rc)
+
+
+def _ptr(x) -> int:
+    """Raw address of a numpy array, a torch tensor or an int."""
+    if x is None:
+        return 0
+    if isinstance(x, int):
+        return x
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    raise TypeError(type(x))
+
+
+def enet_crc32(buffers: Sequence[bytes]) -> int:
+    """CPU callback path: ENet.enet_crc32 over a gather list (packet.cs:142-160)."""
+    L = load()
+    keep = [np.frombuffer(bytes(b), dtype=np.uint8) for b in buffers]
+    arr = (ENetBuffer * max(1, len(keep)))()
+    for i, b in enumerate(keep):
+        arr[i].dataLength = len(b)
+        arr[i].data = b.ctypes.data if len(b) else None
+    return int(L.enet_hip_crc32(ctypes.cast(arr, ctypes.c_void_p), len(keep)))
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    rc = load().enet_hip_device_count(ctypes.byref(n))
+    return n.value if rc == 0 else 0
+
+
+class Context:
+    """One GPU.  Device pointers may be passed as torch tensors or ints."""
+
+    def __init__(self, device: int = 0, lanes_per_packet: int = 0, workgroups_per_cu: int = 0):
+        self.lib = load()
+        h = ctypes.c_void_p()
+        _check("enet_hip_context_create", self.lib.enet_hip_context_create(int(device), ctypes.byref(h)))
+        self.handle = h
+        self.device = device
+        if lanes_per_packet or workgroups_per_cu:
+            self.set_tuning(lanes_per_packet, workgroups_per_cu)
+
+    def set_tuning(self, lanes_per_packet: int = 0, workgroups_per_cu: int = 0) -> None:
+        _check("enet_hip_set_tuning", self.lib.enet_hip_set_tuning(self.handle, lanes_per_packet, workgroups_per_cu))
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            self.lib.enet_hip_context_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # --- device-resident batch entry points (async on `stream`) ---
+    def crc32_batch_device(self, d_bytes, d_off, d_len, n: int, d_out, stream: int = 0) -> None:
+        _check("enet_hip_crc32_batch_device", self.lib.enet_hip_crc32_batch_device(
+            self.handle, _ptr(d_bytes), _ptr(d_off), _ptr(d_len), int(n), _ptr(d_out), stream or None))
+
+    def verify_batch_device(self, d_bytes, d_off, d_len, d_slot, d_connect, n: int, d_ok, d_computed=None,
+                            stream: int = 0) -> None:
+        _check("enet_hip_verify_batch_device", self.lib.enet_hip_verify_batch_device(
+            self.handle, _ptr(d_bytes), _ptr(d_off), _ptr(d_len), _ptr(d_slot), _ptr(d_connect), int(n),
+            _ptr(d_ok), _ptr(d_computed) or None, stream or None))
+
+    def gather_device(self, d_bytes, d_seg_off, d_seg_len, d_seg_first, n_dgrams: int, d_out,
+                      stream: int = 0) -> None:
+        _check("enet_hip_crc32_gather_device", self.lib.enet_hip_crc32_gather_device(
+            self.handle, _ptr(d_bytes), _ptr(d_seg_off), _ptr(d_seg_len), _ptr(d_seg_first), int(n_dgrams),
+            _ptr(d_out), stream or None))
+
+    def read_probe_device(self, d_bytes, nbytes: int, d_sink, stream: int = 0) -> None:
+        _check("enet_hip_read_probe_device", self.lib.enet_hip_read_probe_device(
+            self.handle, _ptr(d_bytes), int(nbytes), _ptr(d_sink), stream or None))
+
+    def synchronize(self) -> None:
+        _check("enet_hip_synchronize", self.lib.enet_hip_synchronize(self.handle))
+
+    # --- host-memory entry point (synchronous) ---
+    def crc32_batch_host(self, payload: np.ndarray, off: np.ndarray, lens: np.ndarray) -> np.ndarray:
+        payload = np.ascontiguousarray(payload, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        out = np.zeros(len(off), dtype=np.uint32)
+        _check("enet_hip_crc32_batch_host", self.lib.enet_hip_crc32_batch_host(
+            self.handle, _ptr(payload), payload.nbytes, _ptr(off), _ptr(lens), len(off), _ptr(out)))
+        return out
+
+
+def crc32_batch_multi(contexts: Sequence[Context], payload: np.ndarray, off: np.ndarray,
+                      lens: np.ndarray) -> np.ndarray:
+    L = load()
+    payload = np.ascontiguousarray(payload, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    out = np.zeros(len(off), dtype=np.uint32)
+    handles = (ctypes.c_void_p * len(contexts))(*[c.handle.value for c in contexts])
+    _check("enet_hip_crc32_batch_multi", L.enet_hip_crc32_batch_multi(
+        ctypes.cast(handles, ctypes.c_void_p), len(contexts), _ptr(payload), payload.nbytes, _ptr(off),
+        _ptr(lens), len(off), _ptr(out)))
+    return out

@@ -1,0 +1,134 @@
+"""Synthetic batches for the BASELINE.json configs.
+
+Payload bytes are splitmix64 output, 8 little-endian bytes per draw; every
+generator is deterministic in its seed.  These are inputs only -- expected CRCs
+always come from the oracle (oracle/), never from here.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+GOLDEN = np.uint64(0x9E3779B97F4A7C15)
+SEED_PAYLOAD = 0x454E6574   # "ENet"   
+SEED_LENGTHS = 0x4C454E53   # "LENS"   
+CONNECT_ID = 0x1234ABCD     # cfg5 slot value
+
+
+def splitmix64(seed: int, count: int, start: int = 0) -> np.ndarray:
+    """Draws start+1 .. start+count of splitmix64(seed) (vectorised, uint64 wraparound)."""
+    with np.errstate(over="ignore"):
+        i = np.arange(start + 1, start + count + 1, dtype=np.uint64)
+        z = np.uint64(seed) + i * GOLDEN
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def payload_bytes(nbytes: int, seed: int = SEED_PAYLOAD) -> np.ndarray:
+    words = splitmix64(seed, (nbytes + 7) // 8)
+    return words.view(np.uint8)[:nbytes].copy()
+
+
+@dataclass
+class Batch:
+    payload: np.ndarray   # uint8, packed
+    off: np.ndarray       # uint64
+    lens: np.ndarray      # uint32
+    name: str
+
+    @property
+    def n(self) -> int:
+        return len(self.off)
+
+    @property
+    def payload_bytes(self) -> int:
+        return int(self.lens.astype(np.uint64).sum())
+
+
+def fixed(n: int, length: int, seed: int = SEED_PAYLOAD, name: str = "") -> Batch:
+    lens = np.full(n, length, dtype=np.uint32)
+    off = np.arange(n, dtype=np.uint64) * np.uint64(length)
+    return Batch(payload_bytes(n * length, seed), off, lens, name or f"{n}x{length}B")
+
+
+def mixed(n: int, lo: int = 64, hi: int = 1400, seed: int = SEED_PAYLOAD, len_seed: int = SEED_LENGTHS,
+          name: str = "") -> Batch:
+    """Lengths uniform in [lo, hi], packed back to back (arbitrary byte alignment)."""
+    lens = (np.uint64(lo) + splitmix64(len_seed, n) % np.uint64(hi - lo + 1)).astype(np.uint32)
+    off = np.zeros(n, dtype=np.uint64)
+    np.cumsum(lens[:-1], out=off[1:])
+    return Batch(payload_bytes(int(lens.astype(np.uint64).sum()), seed), off, lens,
+                 name or f"{n}x[{lo},{hi}]B")
+
+
+def cfg2() -> Batch:
+    """64 K packets x 1200 B (MTU-sized), packed: the headline config."""
+    return fixed(65536, 1200, name="cfg2: 65536 x 1200 B")
+
+
+def cfg3() -> Batch:
+    """256 K packets, lengths uniform in [64, 1400]."""
+    return mixed(262144, 64, 1400, name="cfg3: 262144 x U[64,1400] B")
+
+
+def cfg4(shard: int = 0, shards: int = 1) -> Batch:
+    """1 M packets x 1200 B; shard i of k = contiguous packet range."""
+    n = 1 << 20
+    lo, hi = n * shard // shards, n * (shard + 1) // shards
+    length = 1200
+    words_lo = lo * length // 8
+    nbytes = (hi - lo) * length
+    words = splitmix64(SEED_PAYLOAD, (nbytes + 7) // 8, start=words_lo)
+    payload = words.view(np.uint8)[:nbytes].copy()
+    lens = np.full(hi - lo, length, dtype=np.uint32)
+    off = np.arange(hi - lo, dtype=np.uint64) * np.uint64(length)
+    return Batch(payload, off, lens, f"cfg4: 1048576 x 1200 B shard {shard}/{shards}")
+
+
+@dataclass
+class GatherBatch:
+    """DGRAMs as gather lists: [8 B header+slot][24 B SendFragment][payload chunk]."""
+    payload: np.ndarray
+    seg_off: np.ndarray    # uint64
+    seg_len: np.ndarray    # uint32
+    seg_first: np.ndarray  # uint32, n_dgrams + 1
+    dgram_bytes: int
+    name: str
+
+    @property
+    def n(self) -> int:
+        return len(self.seg_first) - 1
+
+
+def cfg5(messages: int = 4096, message_bytes: int = 65536, mtu: int = 1392) -> GatherBatch:
+    """Fragmented reliable sends (c/peer.cs:130-132, 161-196): fragment = mtu - 4 - 24 - 4
+    = 1360 B with checksums on; a 64 KiB message -> 48 x 1360 + 256.  Each DGRAM is a
+    3-buffer gather list: [4 B header w/ sentTime][4 B slot = connectID][24 B cmd][chunk]."""
+    frag = mtu - 4 - 24 - 4
+    per_msg = (message_bytes + frag - 1) // frag
+    n = messages * per_msg
+    hdr_bytes = n * 8
+    cmd_bytes = n * 24
+    body_bytes = messages * message_bytes
+    payload = payload_bytes(hdr_bytes + cmd_bytes + body_bytes)
+    hdr = payload[:hdr_bytes].reshape(n, 8)
+    hdr[:, 4:8] = np.frombuffer(np.uint32(CONNECT_ID).tobytes(), dtype=np.uint8)
+    seg_off = np.zeros(3 * n, dtype=np.uint64)
+    seg_len = np.zeros(3 * n, dtype=np.uint32)
+    d = np.arange(n, dtype=np.uint64)
+    msg = d // np.uint64(per_msg)
+    k = d % np.uint64(per_msg)
+    chunk_off = np.uint64(hdr_bytes + cmd_bytes) + msg * np.uint64(message_bytes) + k * np.uint64(frag)
+    chunk_len = np.minimum(np.uint64(frag), np.uint64(message_bytes) - k * np.uint64(frag))
+    seg_off[0::3] = d * np.uint64(8)
+    seg_len[0::3] = 8
+    seg_off[1::3] = np.uint64(hdr_bytes) + d * np.uint64(24)
+    seg_len[1::3] = 24
+    seg_off[2::3] = chunk_off
+    seg_len[2::3] = chunk_len.astype(np.uint32)
+    seg_first = (np.arange(n + 1, dtype=np.uint64) * np.uint64(3)).astype(np.uint32)
+    total = int(seg_len.astype(np.uint64).sum())
+    return GatherBatch(payload, seg_off, seg_len, seg_first, total,
+                       f"cfg5: {messages} x {message_bytes} B -> {n} DGRAMs")

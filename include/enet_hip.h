@@ -1,0 +1,142 @@
+/*
+ * enet_hip.h -- C-ABI of libenethip.so, the MI355X (gfx950) CRC32 checksum engine
+ * for enet-csharp (Molth/enet-csharp, a pure-C# ENet 1.3.18 translation).
+ *
+ * Only plain pointers, sizes and integers cross this boundary (no HIP or torch
+ * types): a C# host binds it with [DllImport("enethip")], a C
+ * or C++ host links it directly, Python uses ctypes.
+ *
+ * Reference interfaces replaced / extended (all paths under
+ * /root/reference/enet-csharp/ENet/):
+ *   ENetBuffer ............... include/win32.cs:25-29  { nuint dataLength; void* data; }
+ *   enet_hip_crc32 ........... c/packet.cs:142-160      ENet.enet_crc32 (default checksum)
+ *                              c/enet.cs:195-196        ENET_API.enet_crc32 facade
+ *                              include/enet.cs:663-666  ENetHost.checksum callback field
+ *   enet_hip_crc32_batch_* ... batched form of the per-DGRAM calls at
+ *                              c/protocol.cs:1690-1698 (send stamp) and :1052-1068 (receive)
+ *   enet_hip_verify_batch_* .. c/protocol.cs:1012-1014, 1052-1068 (slot substitution,
+ *                              CRC over the whole DGRAM, drop on mismatch)
+ *   enet_hip_crc32_gather_* .. c/protocol.cs:1546-1559, 1690-1698 (CRC over the
+ *                              host->buffers gather list, <= ENET_BUFFER_MAXIMUM=65
+ *                              buffers, include/enet.cs:417)
+ *
+ * Return values: the checksum functions return the CRC exactly as the reference
+ * does (ENET_HOST_TO_NET_32(~crc), i.e. the 4 bytes to memcpy into the slot).
+ * Every other function returns 0 on success or a negative number -hipError_t
+ * (e.g. -1 = hipErrorInvalidValue for a bad argument, -2 = out of memory,
+ * -100 = no device); enet_hip_error_string() names it.
+ */
+#ifndef ENET_HIP_H
+#define ENET_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(_WIN32)
+#define ENET_HIP_API __declspec(dllexport)
+#else
+#define ENET_HIP_API __attribute__((visibility("default")))
+#endif
+
+/* include/win32.cs:25-29 -- length FIRST (WSABUF order), also on Linux. */
+typedef struct ENetBuffer {
+    size_t dataLength;
+    void* data;
+} ENetBuffer;
+
+/* Shape of ENetHost.checksum (include/enet.cs:666) for native hosts. */
+typedef uint32_t (*ENetChecksumCallback)(const ENetBuffer* buffers, size_t bufferCount);
+
+/* ---- callback path (CPU, synchronous, never fails, never touches the GPU) ---- */
+
+/* Drop-in for ENet.enet_crc32 (c/packet.cs:142-160): CRC-32 over the
+ * concatenation of the buffers, returned as ENET_HOST_TO_NET_32(~crc). */
+ENET_HIP_API uint32_t enet_hip_crc32(const ENetBuffer* buffers, size_t bufferCount);
+
+/* Register-level continuation: feeds `length` bytes into Sarwate register `reg`
+ * (start with 0xFFFFFFFF; the callback value is bswap32(~reg)). */
+ENET_HIP_API uint32_t enet_hip_crc32_update(uint32_t reg, const void* data, size_t length);
+
+/* ---- device context ---- */
+
+typedef struct enet_hip_context enet_hip_context;
+
+ENET_HIP_API int enet_hip_device_count(int* count);
+ENET_HIP_API int enet_hip_context_create(int device, enet_hip_context** out);
+ENET_HIP_API int enet_hip_context_destroy(enet_hip_context* ctx);
+ENET_HIP_API const char* enet_hip_error_string(int code);
+
+/* Tuning knobs (0 = automatic).  lanes_per_packet: 1,2,4,...,64 lanes share one
+ * packet (a power of two); workgroups_per_cu: resident workgroups per CU the
+ * persistent grid is sized for. */
+ENET_HIP_API int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgroups_per_cu);
+
+/* ---- batched checksum, device-resident ----
+ * Packet i is bytes[offsets[i] .. offsets[i]+lengths[i]).  All pointers are
+ * device pointers on ctx's device; out[i] receives what enet_crc32 would return
+ * for that packet as a single ENetBuffer.  Inputs are read-only; `out` is
+ * caller-allocated.  `stream` is a hipStream_t (NULL = ctx's stream).  Async:
+ * returns after the launch. */
+ENET_HIP_API int enet_hip_crc32_batch_device(enet_hip_context* ctx, const uint8_t* bytes,
+                                             const uint64_t* offsets, const uint32_t* lengths,
+                                             size_t count, uint32_t* out, void* stream);
+
+/* ---- batched checksum from/to host memory ----
+ * bytes[0 .. byteCount) is copied H2D, the batch is checksummed on the GPU and
+ * out[] is copied back; synchronous.  Host buffers allocated with
+ * enet_hip_host_alloc are pinned and give full PCIe rate. */
+ENET_HIP_API int enet_hip_crc32_batch_host(enet_hip_context* ctx, const uint8_t* bytes, size_t byteCount,
+                                           const uint64_t* offsets, const uint32_t* lengths,
+                                           size_t count, uint32_t* out);
+
+/* ---- batched receive verify (c/protocol.cs:1052-1068) ----
+ * For DGRAM i: desired = the 4 bytes at slotOffsets[i] (memcpy, host order);
+ * the slot is (virtually) replaced by connectIds[i] (pass 0 for "no peer"), the
+ * CRC is taken over the whole DGRAM, ok[i] = (crc == desired).  The input bytes
+ * are NOT modified.  computed may be NULL.  Device pointers, async. */
+ENET_HIP_API int enet_hip_verify_batch_device(enet_hip_context* ctx, const uint8_t* bytes,
+                                              const uint64_t* offsets, const uint32_t* lengths,
+                                              const uint32_t* slotOffsets, const uint32_t* connectIds,
+                                              size_t count, uint8_t* ok, uint32_t* computed, void* stream);
+
+/* ---- batched gather-list checksum (send path, c/protocol.cs:1690-1698) ----
+ * DGRAM d is the concatenation of segments segFirst[d] .. segFirst[d+1]-1;
+ * segment s is bytes[segOffsets[s] .. +segLengths[s]).  segFirst has
+ * dgramCount+1 entries.  Device pointers, async. */
+ENET_HIP_API int enet_hip_crc32_gather_device(enet_hip_context* ctx, const uint8_t* bytes,
+                                              const uint64_t* segOffsets, const uint32_t* segLengths,
+                                              const uint32_t* segFirst, size_t dgramCount, uint32_t* out,
+                                              void* stream);
+
+/* ---- multi-GPU: independent contiguous shards, no collective ----
+ * Packets [i*count/k, (i+1)*count/k) go to contexts[i]; each shard's bytes are
+ * copied to its device, checksummed and the CRCs copied back into out[].
+ * Synchronous; one host thread per device. */
+ENET_HIP_API int enet_hip_crc32_batch_multi(enet_hip_context* const* contexts, int contextCount,
+                                            const uint8_t* bytes, size_t byteCount, const uint64_t* offsets,
+                                            const uint32_t* lengths, size_t count, uint32_t* out);
+
+/* ---- diagnostics: HBM read-roofline probe ----
+ * Streams bytes[0 .. byteCount) once with 16-byte coalesced loads (no table
+ * work) and XOR-folds it into *sink (device pointer, 16 bytes); the bench times
+ * it beside the checksum kernel as the "achievable read bandwidth" line. */
+ENET_HIP_API int enet_hip_read_probe_device(enet_hip_context* ctx, const uint8_t* bytes, size_t byteCount,
+                                            uint32_t* sink, void* stream);
+
+/* ---- small memory helpers (so C#/ctypes hosts need no HIP binding) ---- */
+ENET_HIP_API int enet_hip_device_alloc(enet_hip_context* ctx, size_t bytes, void** out);
+ENET_HIP_API int enet_hip_device_free(enet_hip_context* ctx, void* ptr);
+ENET_HIP_API int enet_hip_host_alloc(size_t bytes, void** out); /* pinned */
+ENET_HIP_API int enet_hip_host_free(void* ptr);
+ENET_HIP_API int enet_hip_memcpy_h2d(enet_hip_context* ctx, void* dst, const void* src, size_t bytes);
+ENET_HIP_API int enet_hip_memcpy_d2h(enet_hip_context* ctx, void* dst, const void* src, size_t bytes);
+ENET_HIP_API int enet_hip_synchronize(enet_hip_context* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ENET_HIP_H */

@@ -1,0 +1,135 @@
+"""CPU oracle for the ENet CRC32 path -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module, and only as the checker (or the timed CPU baseline, kind "port").
+The shipped library (enet-csharp_amd/) never imports it.
+
+Two restatements of /root/reference/enet-csharp/ENet/c/packet.cs:142-160:
+  * ``enet_crc32_py``   -- pure Python, byte-serial (packet.cs:151-154), for small
+                           cases and for generating golden vectors;
+  * ``OracleLib``       -- ctypes binding of enet_crc32_oracle.c (same loop in C),
+                           for batch-sized parity checks and the CPU baseline.
+Both use ``crc_table()`` (generated from poly 0xEDB88320); tests pin it against
+the reference's literal table (packet.cs:106-140) stored in
+tests/golden/crc_table_ref.json.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "lib", "liboracle.so")
+
+
+def crc_table() -> list[int]:
+    """Reflected CRC-32 table, poly 0xEDB88320 (what packet.cs:106-140 spells out)."""
+    t = []
+    for n in range(256):
+        c = n
+        for _ in range(8):
+            c = (c >> 1) ^ 0xEDB88320 if c & 1 else c >> 1
+        t.append(c)
+    return t
+
+
+_T = crc_table()
+
+
+def host_to_net_32(v: int) -> int:
+    """include/win32.cs:18 on a little-endian host (ReverseEndianness)."""
+    return int.from_bytes((v & 0xFFFFFFFF).to_bytes(4, "little"), "big")
+
+
+def enet_crc32_py(buffers) -> int:
+    """packet.cs:142-160. ``buffers`` is a sequence of bytes-like (the ENetBuffer list)."""
+    crc = 0xFFFFFFFF                                      # :144
+    for buf in buffers:                                   # :146-157
+        for b in bytes(buf):                              # :151-154
+            crc = (crc >> 8) ^ _T[(crc & 0xFF) ^ b]       # :153
+    return host_to_net_32(~crc & 0xFFFFFFFF)             # :159
+
+
+def build() -> str:
+    """Compile oracle/lib/liboracle.so with gcc (oracle/Makefile)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+class OracleLib:
+    """ctypes view of enet_crc32_oracle.c."""
+
+    def __init__(self, path: str | None = None):
+        path = path or _LIB_PATH
+        if not os.path.exists(path):
+            build()
+        self.lib = ctypes.CDLL(path)
+        L = self.lib
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        L.oracle_enet_crc32.restype = ctypes.c_uint32
+        L.oracle_enet_crc32.argtypes = [vp, sz]
+        L.oracle_crc32_batch.restype = None
+        L.oracle_crc32_batch.argtypes = [vp, vp, vp, sz, vp]
+        L.oracle_crc32_batch_mt.restype = ctypes.c_int
+        L.oracle_crc32_batch_mt.argtypes = [vp, vp, vp, sz, vp, ctypes.c_int]
+        L.oracle_crc32_gather.restype = None
+        L.oracle_crc32_gather.argtypes = [vp, vp, vp, vp, sz, vp]
+        L.oracle_verify_batch.restype = None
+        L.oracle_verify_batch.argtypes = [vp, vp, vp, vp, vp, sz, vp, vp]
+        L.oracle_crc_table.restype = None
+        L.oracle_crc_table.argtypes = [vp]
+
+    @staticmethod
+    def _p(a: np.ndarray):
+        return ctypes.c_void_p(a.ctypes.data)
+
+    def table(self) -> np.ndarray:
+        out = np.zeros(256, dtype=np.uint32)
+        self.lib.oracle_crc_table(self._p(out))
+        return out
+
+    def crc32(self, data: bytes) -> int:
+        buf = np.frombuffer(bytes(data), dtype=np.uint8).copy() if len(data) else np.zeros(1, np.uint8)
+        eb = np.array([len(data), buf.ctypes.data], dtype=np.uint64)   # {dataLength, data}
+        return int(self.lib.oracle_enet_crc32(self._p(eb), 1))
+
+    def batch(self, payload: np.ndarray, off: np.ndarray, lens: np.ndarray, threads: int = 1) -> np.ndarray:
+        payload = np.ascontiguousarray(payload, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        out = np.zeros(len(off), dtype=np.uint32)
+        if threads <= 1:
+            self.lib.oracle_crc32_batch(self._p(payload), self._p(off), self._p(lens), len(off), self._p(out))
+        else:
+            rc = self.lib.oracle_crc32_batch_mt(self._p(payload), self._p(off), self._p(lens), len(off),
+                                                self._p(out), int(threads))
+            if rc != 0:
+                raise RuntimeError("oracle_crc32_batch_mt failed")
+        return out
+
+    def gather(self, payload, seg_off, seg_len, seg_first) -> np.ndarray:
+        payload = np.ascontiguousarray(payload, dtype=np.uint8)
+        seg_off = np.ascontiguousarray(seg_off, dtype=np.uint64)
+        seg_len = np.ascontiguousarray(seg_len, dtype=np.uint32)
+        seg_first = np.ascontiguousarray(seg_first, dtype=np.uint32)
+        n = len(seg_first) - 1
+        out = np.zeros(n, dtype=np.uint32)
+        self.lib.oracle_crc32_gather(self._p(payload), self._p(seg_off), self._p(seg_len),
+                                     self._p(seg_first), n, self._p(out))
+        return out
+
+    def verify(self, payload, off, lens, slot_off, connect_id):
+        payload = np.ascontiguousarray(payload, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        slot_off = np.ascontiguousarray(slot_off, dtype=np.uint32)
+        connect_id = np.ascontiguousarray(connect_id, dtype=np.uint32)
+        n = len(off)
+        ok = np.zeros(n, dtype=np.uint8)
+        comp = np.zeros(n, dtype=np.uint32)
+        self.lib.oracle_verify_batch(self._p(payload), self._p(off), self._p(lens), self._p(slot_off),
+                                     self._p(connect_id), n, self._p(ok), self._p(comp))
+        return ok, comp

@@ -1,0 +1,218 @@
+"""GPU parity: the HIP path (through the C-ABI of libenethip.so) against the oracle.
+
+Bit-exact everywhere (integer/byte work).  Sizes run from the golden vectors up
+to BASELINE.json's full configs; the oracle (C, multithreaded) finishes those in
+about a second, so the full sizes are checked element for element, plus
+size-independent properties (linearity, tuning invariance, determinism)."""
+import numpy as np
+import pytest
+
+import enethip
+from enethip import workloads
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.init()
+    c = enethip.Context(0)
+    yield c
+    c.close()
+
+
+def dev(a: np.ndarray):
+    a = np.ascontiguousarray(a)
+    view = {np.dtype(np.uint64): np.int64, np.dtype(np.uint32): np.int32, np.dtype(np.uint8): np.uint8}[a.dtype]
+    return torch.from_numpy(a.view(view)).cuda()
+
+
+def run_batch(ctx, payload, off, lens, lanes=0, wgs=0):
+    ctx.set_tuning(lanes, wgs)
+    d_p, d_o, d_l = dev(payload if len(payload) else np.zeros(16, np.uint8)), dev(off), dev(lens)
+    out = torch.zeros(len(off), dtype=torch.int32, device="cuda")
+    ctx.crc32_batch_device(d_p, d_o, d_l, len(off), out, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint32)
+
+
+def golden_batch(golden):
+    vecs, blob = golden
+    off, lens, exp = [], [], []
+    parts = []
+    pos = 0
+    for v in vecs:
+        data = b"".join(bytes(blob[o:o + n]) for o, n in v["segments"])
+        parts.append(data)
+        off.append(pos)
+        lens.append(len(data))
+        exp.append(int(v["crc"], 16))
+        pos += len(data)
+    payload = np.frombuffer(b"".join(parts), dtype=np.uint8).copy()
+    return payload, np.array(off, np.uint64), np.array(lens, np.uint32), np.array(exp, np.uint32)
+
+
+@pytest.mark.parametrize("lanes", [1, 2, 4, 8, 16, 64])
+def test_golden_vectors(ctx, golden, lanes):
+    payload, off, lens, exp = golden_batch(golden)
+    got = run_batch(ctx, payload, off, lens, lanes)
+    bad = np.nonzero(got != exp)[0]
+    assert len(bad) == 0, [(int(i), int(lens[i]), hex(got[i]), hex(exp[i])) for i in bad[:10]]
+
+
+@pytest.mark.parametrize("lanes", [1, 4, 32])
+def test_random_unaligned_sparse(ctx, oracle_lib, lanes):
+    rng = np.random.default_rng(100 + lanes)
+    n = 5000
+    lens = rng.integers(0, 5000, size=n).astype(np.uint32)
+    lens[:40] = np.arange(40)                       # every tiny length
+    gaps = rng.integers(0, 37, size=n).astype(np.uint64)
+    off = np.zeros(n, dtype=np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64) + gaps[:-1])
+    off += np.uint64(3)
+    perm = rng.permutation(n)                       # packets in arbitrary order
+    off, lens = off[perm], lens[perm]
+    payload = rng.integers(0, 256, size=int((off + lens).max()) + 5, dtype=np.uint8)
+    got = run_batch(ctx, payload, off, lens, lanes)
+    exp = oracle_lib.batch(payload, off, lens, threads=8)
+    assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
+
+
+def test_cfg2_full(ctx, oracle_lib):
+    b = workloads.cfg2()
+    exp = oracle_lib.batch(b.payload, b.off, b.lens, threads=16)
+    for lanes in (1, 4, 8):
+        assert (run_batch(ctx, b.payload, b.off, b.lens, lanes) == exp).all(), lanes
+
+
+def test_cfg3_full(ctx, oracle_lib):
+    b = workloads.cfg3()
+    exp = oracle_lib.batch(b.payload, b.off, b.lens, threads=16)
+    for lanes in (2, 4):
+        assert (run_batch(ctx, b.payload, b.off, b.lens, lanes) == exp).all(), lanes
+
+
+def test_cfg4_shard_full(ctx, oracle_lib):
+    b = workloads.cfg4(1, 8)
+    exp = oracle_lib.batch(b.payload, b.off, b.lens, threads=16)
+    assert (run_batch(ctx, b.payload, b.off, b.lens) == exp).all()
+
+
+def test_linearity_and_determinism(ctx):
+    # For equal-length packets CRC is affine over GF(2): crc(a^b^c) = crc(a)^crc(b)^crc(c).
+    rng = np.random.default_rng(5)
+    n, L = 3000, 1200
+    a, b_, c = (rng.integers(0, 256, size=n * L, dtype=np.uint8) for _ in range(3))
+    off = np.arange(n, dtype=np.uint64) * np.uint64(L)
+    lens = np.full(n, L, np.uint32)
+    ca, cb, cc = (run_batch(ctx, x, off, lens) for x in (a, b_, c))
+    cx = run_batch(ctx, a ^ b_ ^ c, off, lens)
+    assert (cx == (ca ^ cb ^ cc)).all()
+    assert (run_batch(ctx, a, off, lens, 16, 1) == ca).all()
+
+
+def test_host_entry_point(ctx, oracle_lib):
+    b = workloads.mixed(20000, 1, 4096, seed=9, len_seed=10)
+    ctx.set_tuning(0, 0)
+    got = ctx.crc32_batch_host(b.payload, b.off, b.lens)
+    assert (got == oracle_lib.batch(b.payload, b.off, b.lens, threads=8)).all()
+
+
+def test_multi_context_shards(oracle_lib):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    b = workloads.mixed(30001, 64, 1400, seed=3, len_seed=4)
+    ctxs = [enethip.Context(i % max(1, enethip.device_count())) for i in range(3)]
+    try:
+        got = enethip.crc32_batch_multi(ctxs, b.payload, b.off, b.lens)
+    finally:
+        for c in ctxs:
+            c.close()
+    assert (got == oracle_lib.batch(b.payload, b.off, b.lens, threads=8)).all()
+
+
+def _verify_inputs(rng, n):
+    """DGRAMs as ENet puts them on the wire: [2 or 4 B header][4 B slot][commands]."""
+    lens = rng.integers(6, 1400, size=n).astype(np.uint32)
+    slot = np.where(rng.integers(0, 2, size=n) == 1, 4, 2).astype(np.uint32)
+    lens = np.maximum(lens, slot + 4)
+    conn = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    conn[::5] = 0                                   # "no peer" DGRAMs
+    off = np.zeros(n, dtype=np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    payload = rng.integers(0, 256, size=int(lens.sum()), dtype=np.uint8)
+    for i in range(n):                              # stamp like protocol.cs:1690-1698
+        o, s = int(off[i]), int(slot[i])
+        payload[o + s:o + s + 4] = np.frombuffer(np.uint32(conn[i]).tobytes(), np.uint8)
+    return payload, off, lens, slot, conn
+
+
+def test_verify_batch(ctx, oracle_lib):
+    rng = np.random.default_rng(21)
+    n = 4000
+    payload, off, lens, slot, conn = _verify_inputs(rng, n)
+    # stamp the true checksum (computed over the DGRAM with slot = connectID)
+    stamped = oracle_lib.batch(payload, off, lens, threads=8)
+    for i in range(n):
+        o, s = int(off[i]), int(slot[i])
+        payload[o + s:o + s + 4] = np.frombuffer(np.uint32(stamped[i]).tobytes(), np.uint8)
+    bad = rng.choice(n, size=300, replace=False)
+    for i in bad:                                   # corrupt a byte (or the slot) of some DGRAMs
+        j = int(off[i]) + int(rng.integers(0, int(lens[i])))
+        payload[j] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    exp_ok, exp_comp = oracle_lib.verify(payload, off, lens, slot, conn)
+    assert exp_ok.sum() == n - 300
+    for lanes in (1, 4):
+        ctx.set_tuning(lanes, 0)
+        d_ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        d_comp = torch.zeros(n, dtype=torch.int32, device="cuda")
+        ctx.verify_batch_device(dev(payload), dev(off), dev(lens), dev(slot), dev(conn), n, d_ok, d_comp,
+                                stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert (d_ok.cpu().numpy() == exp_ok).all()
+        assert (d_comp.cpu().numpy().view(np.uint32) == exp_comp).all()
+
+
+def test_verify_golden(ctx, golden):
+    vecs, blob = golden
+    vv = [v for v in vecs if v["kind"] == "verify"]
+    off = np.array([v["segments"][0][0] for v in vv], np.uint64)
+    lens = np.array([v["segments"][0][1] for v in vv], np.uint32)
+    slot = np.array([v["slot_off"] for v in vv], np.uint32)
+    conn = np.array([int(v["connect_id"], 16) for v in vv], np.uint32)
+    d_ok = torch.zeros(len(vv), dtype=torch.uint8, device="cuda")
+    ctx.set_tuning(0, 0)
+    ctx.verify_batch_device(dev(blob), dev(off), dev(lens), dev(slot), dev(conn), len(vv), d_ok)
+    ctx.synchronize()
+    assert d_ok.cpu().numpy().astype(bool).tolist() == [v["expect_ok"] for v in vv]
+
+
+def test_gather_golden_and_cfg5(ctx, golden, oracle_lib):
+    vecs, blob = golden
+    seg_off, seg_len, first, exp = [], [], [0], []
+    for v in vecs:
+        for o, n in v["segments"]:
+            seg_off.append(o)
+            seg_len.append(n)
+        first.append(len(seg_off))
+        exp.append(int(v["crc"], 16))
+    out = torch.zeros(len(exp), dtype=torch.int32, device="cuda")
+    ctx.gather_device(dev(blob), dev(np.array(seg_off, np.uint64)), dev(np.array(seg_len, np.uint32)),
+                      dev(np.array(first, np.uint32)), len(exp), out)
+    ctx.synchronize()
+    assert out.cpu().numpy().view(np.uint32).tolist() == exp
+    g = workloads.cfg5(messages=256)
+    out = torch.zeros(g.n, dtype=torch.int32, device="cuda")
+    ctx.gather_device(dev(g.payload), dev(g.seg_off), dev(g.seg_len), dev(g.seg_first), g.n, out)
+    ctx.synchronize()
+    assert (out.cpu().numpy().view(np.uint32) == oracle_lib.gather(g.payload, g.seg_off, g.seg_len,
+                                                                   g.seg_first)).all()
+
+
+def test_bad_tuning_raises(ctx):
+    with pytest.raises(enethip.ENetHipError):
+        ctx.set_tuning(3, 0)

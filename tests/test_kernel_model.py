@@ -1,0 +1,104 @@
+"""CPU checks of the kernel's algebra and LDS schedule (see tests/kernel_model.py).
+
+These run without a GPU: they prove the lane schedule is conflict-free by
+construction and that the windowing / INIT / carry-combine arithmetic reproduces
+the oracle bit for bit.  The -m gpu tests then check the hardware does the same.
+"""
+import random
+
+import pytest
+
+import kernel_model as km
+import oracle
+
+
+def test_slicing_tables_and_image():
+    # T_t[j] is byte j followed by t zero bytes
+    for t in (0, 1, 7, 31):
+        for j in (0, 1, 0x80, 0xFF):
+            reg = 0
+            reg = (reg >> 8) ^ km.T0[(reg ^ j) & 0xFF]
+            for _ in range(t):
+                reg = (reg >> 8) ^ km.T0[reg & 0xFF]
+            assert km.TS[t][j] == reg
+    assert km.IMG[5 * 64 + 2 * 9 + 1] == km.TS[9][5]
+
+
+def test_lds_bank_conflict_free():
+    """Every lookup instruction: the 32 lanes of each half-wave hit 32 distinct banks
+    (ds_read_b32: bank = (addr/4) mod 32, lane groups 0-31 and 32-63)."""
+    rng = random.Random(1)
+    for _ in range(20):
+        words = [rng.getrandbits(32) for _ in range(8)]
+        per_lane = [km.lookup_addresses(l, words) for l in range(64)]
+        for i in range(32):
+            for g in (range(0, 32), range(32, 64)):
+                banks = {(per_lane[l][i] // 4) % 32 for l in g}
+                assert len(banks) == 32, (i, sorted(banks))
+
+
+def test_each_lane_reads_every_byte_once():
+    rng = random.Random(2)
+    block = bytes(rng.getrandbits(8) for _ in range(32))
+    words = [int.from_bytes(block[4 * q:4 * q + 4], "little") for q in range(8)]
+    for lane in range(64):
+        addrs = km.lookup_addresses(lane, words)
+        used = set()
+        for a in addrs:
+            row, col = a // 256, (a % 256) // 4
+            t = col // 2
+            m = t ^ 31
+            assert block[m] == row      # looked-up row is byte m of the block
+            used.add(m)
+        assert used == set(range(32))
+
+
+def test_fold_block_equals_sarwate():
+    rng = random.Random(3)
+    for lane in (0, 5, 17, 33, 63):
+        for _ in range(5):
+            block = bytes(rng.getrandbits(8) for _ in range(32))
+            reg = rng.getrandbits(32)
+            ref = reg
+            for b in block:
+                ref = (ref >> 8) ^ km.T0[(ref ^ b) & 0xFF]
+            assert km.fold_block(reg, block, lane) == ref
+
+
+def test_init_states():
+    for r in range(32):
+        reg = km.INIT[r]
+        for _ in range(r):
+            reg = (reg >> 8) ^ km.T0[reg & 0xFF]
+        assert reg == 0xFFFFFFFF
+
+
+def test_mulmod_is_zero_advance():
+    rng = random.Random(4)
+    for n in (0, 1, 3, 32, 100, 1200):
+        for _ in range(3):
+            r = rng.getrandbits(32)
+            ref = r
+            for _ in range(n):
+                ref = (ref >> 8) ^ km.T0[ref & 0xFF]
+            assert km.mulmod(r, km.x8n(n)) == ref
+
+
+@pytest.mark.parametrize("lanes", [1, 2, 4, 8, 64])
+def test_packet_model_matches_oracle(lanes):
+    rng = random.Random(10 + lanes)
+    for L in [0, 1, 3, 4, 15, 16, 17, 31, 32, 33, 63, 64, 65, 100, 257, 1200, 1201]:
+        pkt = bytes(rng.getrandbits(8) for _ in range(L))
+        assert km.crc_packet(pkt, lanes) == oracle.enet_crc32_py([pkt]), (L, lanes)
+
+
+def test_verify_model(golden):
+    vecs, blob = golden
+    for v in vecs:
+        if v["kind"] != "verify":
+            continue
+        o, n = v["segments"][0]
+        pkt = bytes(blob[o:o + n])
+        for lanes in (1, 4):
+            ok, _ = km.verify_packet(pkt, v["slot_off"], int(v["connect_id"], 16), lanes)
+            assert ok == v["expect_ok"]
