@@ -1,0 +1,228 @@
+// crc32_device.hpp -- gfx950 device building blocks of the CRC32 kernels
+// (included by crc32_kernels.hip and by the measurement-only tools/microbench.hip).
+// Reference algorithm: /root/reference/enet-csharp/ENet/c/packet.cs:142-160.
+//
+// Slicing-by-32 in LDS, conflict-free.  A 32-byte block b_0..b_31 is folded
+// into the Sarwate register by   reg' = XOR_m T_{31-m}[b_m ^ reg_m]   (reg_m = byte
+// m of reg for m < 4, else 0), T_t[j] = byte j followed by t zero bytes.  The 32
+// tables sit side by side: row j (128 B) holds T_0[j] .. T_31[j] in dword columns
+// 0..31, i.e. in LDS banks 0..31 (ds_read_b32 bank = (addr/4) mod 32, lanes 0-31
+// and 32-63 served as separate groups).  At lookup step i a lane l handles byte
+// m = i ^ (l & 31) -- an XOR Latin square -- so in every ds_read_b32 the 32 lanes
+// of a half-wave read 32 different tables = 32 different banks: no conflicts
+// whatever the data (tests/test_kernel_model.py proves it; measured 2.5-2.9 LDS
+// cycles per wave-instruction on MI355X vs ~6 for random rows).  The per-lane
+// byte order costs one dword permutation per block (two bitop3 rounds + a half
+// swap) and one v_perm_b32 + one shift per lookup to form the LDS address.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "crc32_math.hpp"
+
+namespace enethip {
+
+constexpr int kLdsTableBytes = 256 * 32 * 4;       // 256 rows x 32 tables = 32 KiB
+constexpr int kXnEntries = 65536;                  // x^(8n) for n < 65536 (+ high part)
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// LDS dword addressed by an absolute byte address.  The table is the first thing
+// in every kernel's single dynamic LDS array, so it starts at LDS address 0 and
+// an integer -> address_space(3) cast feeds the computed address straight to
+// ds_read_b32 (a generic `lds + addr` costs one v_add per lookup).
+typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+typedef __attribute__((address_space(3))) const u32x4 lds_u32x4;
+
+struct KernelTables {
+    const uint32_t* image;  // kLdsTableBytes, copied into LDS by every workgroup
+    const uint32_t* xn_lo;  // x^(8n) mod P, n < 65536
+    const uint32_t* xn_hi;  // x^(8*65536*q) mod P, q < 65536
+    const uint32_t* init;   // INIT[r], r < 32
+};
+
+// ------------------------------------------------------------------ device helpers
+
+__device__ __forceinline__ u32x4 ldg16(const uint8_t* p) {
+    u32x4 v;
+    __builtin_memcpy(&v, p, 16);  // global_load_dwordx4 (unaligned access mode on gfx950)
+    return v;
+}
+
+// 16 bytes at A, with bytes in front of the packet start `a` read as zero.
+// Precondition: every byte of [max(A,a), A+16) belongs to the packet.
+__device__ __forceinline__ u32x4 ldg16_head(const uint8_t* A, const uint8_t* a) {
+    if (A >= a) return ldg16(A);
+    if (A + 16 <= a) return u32x4{0u, 0u, 0u, 0u};
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int b = 0; b < 16; ++b)
+        if (A + b >= a) w[b >> 2] |= static_cast<uint32_t>(A[b]) << (8 * (b & 3));
+    return u32x4{w[0], w[1], w[2], w[3]};
+}
+
+// Zero the first n (0..16) bytes of a 16-byte piece.
+__device__ __forceinline__ u32x4 zero_prefix(u32x4 v, uint32_t n) {
+    const uint32_t b = n * 8u;
+    const uint32_t k0 = b >= 32u ? 0u : (0xFFFFFFFFu << b);
+    const uint32_t k1 = b >= 64u ? 0u : (b <= 32u ? 0xFFFFFFFFu : (0xFFFFFFFFu << (b - 32u)));
+    const uint32_t k2 = b >= 96u ? 0u : (b <= 64u ? 0xFFFFFFFFu : (0xFFFFFFFFu << (b - 64u)));
+    const uint32_t k3 = b >= 128u ? 0u : (b <= 96u ? 0xFFFFFFFFu : (0xFFFFFFFFu << (b - 96u)));
+    return u32x4{v.x & k0, v.y & k1, v.z & k2, v.w & k3};
+}
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// Per-lane constants of the conflict-free slicing-by-32 schedule.
+struct LaneSched {
+    uint32_t col[8];  // byte h of col[g]: 8 * table index for step i = 4g + h
+    uint32_t sel[4];  // v_perm selector for steps with i & 3 == h
+    uint32_t m1, m2;  // all-ones when this lane swaps dwords q <-> q^1 / q <-> q^2
+    uint32_t hs;      // all-ones when this lane takes the block's two 16-byte halves swapped
+};
+
+__device__ __forceinline__ LaneSched make_sched(uint32_t lane) {
+    LaneSched s;
+    const uint32_t l5 = lane & 31u;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+        uint32_t r = 0;
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            const uint32_t i = 4u * g + h;
+            const uint32_t t = (i ^ l5) ^ 31u;        // table of byte m = i ^ l5
+            r |= (8u * t) << (8 * h);
+        }
+        s.col[g] = r;
+    }
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+        s.sel[h] = static_cast<uint32_t>(h) | ((4u + (static_cast<uint32_t>(h) ^ (l5 & 3u))) << 8) | 0x0C0C0000u;
+    s.m1 = 0u - ((l5 >> 2) & 1u);
+    s.m2 = 0u - ((l5 >> 3) & 1u);
+    s.hs = 0u - ((l5 >> 4) & 1u);
+    return s;
+}
+
+// One 32-byte block folded into `reg` (== 32 Sarwate steps, packet.cs:153).
+// A, B are the block's halves in LANE order: A = bytes 0-15 and B = 16-31 when
+// s.hs == 0, swapped when s.hs is all-ones (the staged kernel swaps them for free
+// by its LDS read addresses; fold_block below swaps registers).
+__device__ __forceinline__ uint32_t fold_block_lane(uint32_t reg, u32x4 A, u32x4 B, const LaneSched& s) {
+    // state enters byte 0-3 of the ORIGINAL block: A.x if no swap, else B.x
+    const uint32_t a0 = __builtin_amdgcn_bitop3_b32(A.x, reg, s.hs, 0xB4);   // A ^ (reg & ~hs)
+    const uint32_t b0 = __builtin_amdgcn_bitop3_b32(B.x, reg, s.hs, 0x78);   // B ^ (reg & hs)
+    const uint32_t w[8] = {a0, A.y, A.z, A.w, b0, B.y, B.z, B.w};
+    // d[q] = w[q ^ ((lane >> 2) & 3)]: two rounds of bitwise selects (0xD8 = m ? b : a)
+    uint32_t x[8], d[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) x[q] = __builtin_amdgcn_bitop3_b32(w[q], w[q ^ 1], s.m1, 0xD8);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) d[q] = __builtin_amdgcn_bitop3_b32(x[q], x[q ^ 2], s.m2, 0xD8);
+    uint32_t v[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        // v_perm: byte0 = 8t, byte1 = data byte j  ->  (j*256 + 8t) >> 1 = j*128 + 4t
+        const uint32_t addr = __builtin_amdgcn_perm(d[i >> 2], s.col[i >> 2], s.sel[i & 3]) >> 1;
+        v[i] = *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr));
+    }
+    uint32_t acc = xor3(v[0], v[1], v[2]);
+#pragma unroll
+    for (int i = 3; i + 1 < 32; i += 2) acc = xor3(acc, v[i], v[i + 1]);
+    return acc ^ v[31];
+}
+
+// Same, halves given in ORIGINAL order (bytes 0-15, 16-31).
+__device__ __forceinline__ uint32_t fold_block(uint32_t reg, u32x4 h0, u32x4 h1, const LaneSched& s) {
+    u32x4 A, B;
+    A.x = __builtin_amdgcn_bitop3_b32(h0.x, h1.x, s.hs, 0xD8);
+    A.y = __builtin_amdgcn_bitop3_b32(h0.y, h1.y, s.hs, 0xD8);
+    A.z = __builtin_amdgcn_bitop3_b32(h0.z, h1.z, s.hs, 0xD8);
+    A.w = __builtin_amdgcn_bitop3_b32(h0.w, h1.w, s.hs, 0xD8);
+    B.x = __builtin_amdgcn_bitop3_b32(h1.x, h0.x, s.hs, 0xD8);
+    B.y = __builtin_amdgcn_bitop3_b32(h1.y, h0.y, s.hs, 0xD8);
+    B.z = __builtin_amdgcn_bitop3_b32(h1.z, h0.z, s.hs, 0xD8);
+    B.w = __builtin_amdgcn_bitop3_b32(h1.w, h0.w, s.hs, 0xD8);
+    return fold_block_lane(reg, A, B, s);
+}
+
+__device__ __forceinline__ uint32_t mulmod(uint32_t a, uint32_t b) {
+    uint32_t p = 0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        const uint32_t m = static_cast<uint32_t>(static_cast<int32_t>(a << j) >> 31);
+        p = __builtin_amdgcn_bitop3_b32(p, b, m, 0x78);                 // p ^ (b & m)
+        const uint32_t r = static_cast<uint32_t>(static_cast<int32_t>(b << 31) >> 31);
+        b = __builtin_amdgcn_bitop3_b32(b >> 1, kPoly, r, 0x78);         // (b>>1) ^ (P & r)
+    }
+    return p;
+}
+
+__device__ __forceinline__ uint32_t x8n_dev(uint32_t n, const KernelTables& tb) {
+    uint32_t x = tb.xn_lo[n & 0xFFFFu];
+    if (n >> 16) x = mulmod(x, tb.xn_hi[n >> 16]);
+    return x;
+}
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = max(v, static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), m)));
+    return v;
+}
+
+// Register after feeding the segment [sp, sp+len) from `reg`, with every block
+// loaded straight from global memory (the general path: any offsets, lengths and
+// alignments).  The segment is processed as an END-aligned window of nb =
+// ceil(len/32) blocks; the rp = 32*nb - len bytes in front of sp read as zero.
+//
+// Software pipeline over HBM latency: a 4-block register ring.  The loop is
+// wave-uniform (trip count = the wave's maximum block count) and every load is
+// unconditional -- lanes past their range re-load their last block (or, with no
+// block at all, the always-valid `safe` buffer) and keep their register by a
+// select -- so the compiler emits counted s_waitcnt vmcnt(N) instead of a full
+// drain per block (a predicated load makes it wait vmcnt(0) every block).
+__device__ __forceinline__ uint32_t fold_window(uint32_t reg, const uint8_t* sp, uint32_t len,
+                                                const LaneSched& s, const uint8_t* safe) {
+    const uint32_t nb = (len + 31u) >> 5;
+    const uint8_t* W = sp + len - (static_cast<size_t>(nb) << 5);
+    const bool head = nb && ((nb << 5) != len);
+    const uint32_t jb = head ? 1u : 0u;                 // first ring block
+    const uint32_t cnt = nb - jb;                       // ring blocks of this lane
+    const uint32_t trips = wave_max(cnt);
+    // address of ring block k (clamped into this lane's valid range)
+    const uint8_t* base = cnt ? W + 32u * jb : safe;
+    const uint32_t last = cnt ? cnt - 1u : 0u;
+#define ENH_BLK(k) (base + 32u * min(static_cast<uint32_t>(k), last))
+    u32x4 r0a = ldg16(ENH_BLK(0)), r0b = ldg16(ENH_BLK(0) + 16);
+    u32x4 r1a = ldg16(ENH_BLK(1)), r1b = ldg16(ENH_BLK(1) + 16);
+    u32x4 r2a = ldg16(ENH_BLK(2)), r2b = ldg16(ENH_BLK(2) + 16);
+    u32x4 r3a = ldg16(ENH_BLK(3)), r3b = ldg16(ENH_BLK(3) + 16);
+    if (head) {
+        const u32x4 ha = ldg16_head(W, sp), hb = ldg16_head(W + 16, sp);
+        reg = fold_block(reg, ha, hb, s);
+    }
+    for (uint32_t k = 0; k < trips; k += 4) {
+        uint32_t nr;
+        nr = fold_block(reg, r0a, r0b, s);
+        reg = (k + 0 < cnt) ? nr : reg;
+        r0a = ldg16(ENH_BLK(k + 4)); r0b = ldg16(ENH_BLK(k + 4) + 16);
+        __builtin_amdgcn_sched_barrier(0);  // keep the reload here: 4 blocks ahead
+        nr = fold_block(reg, r1a, r1b, s);
+        reg = (k + 1 < cnt) ? nr : reg;
+        r1a = ldg16(ENH_BLK(k + 5)); r1b = ldg16(ENH_BLK(k + 5) + 16);
+        __builtin_amdgcn_sched_barrier(0);
+        nr = fold_block(reg, r2a, r2b, s);
+        reg = (k + 2 < cnt) ? nr : reg;
+        r2a = ldg16(ENH_BLK(k + 6)); r2b = ldg16(ENH_BLK(k + 6) + 16);
+        __builtin_amdgcn_sched_barrier(0);
+        nr = fold_block(reg, r3a, r3b, s);
+        reg = (k + 3 < cnt) ? nr : reg;
+        r3a = ldg16(ENH_BLK(k + 7)); r3b = ldg16(ENH_BLK(k + 7) + 16);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#undef ENH_BLK
+    return reg;
+}
+
+}  // namespace enethip

@@ -30,159 +30,40 @@
 #include <cstring>
 #include <mutex>
 #include <thread>
+#include <tuple>
 #include <vector>
 
+#include "crc32_device.hpp"
 #include "crc32_math.hpp"
 #include "enet_hip.h"
 
 namespace enethip {
 
-constexpr int kThreads = 512;                      // workgroup size (8 waves)
-constexpr int kLdsImageBytes = 256 * 64 * 4;       // 256 rows x 64 dwords = 64 KiB
-constexpr int kXnEntries = 65536;                  // x^(8n) for n < 65536 (+ high part)
+constexpr int kThreads = 512;                     // direct / gather kernels: 8 waves
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-struct KernelTables {
-    const uint32_t* image;  // kLdsImageBytes, copied into LDS by every workgroup
-    const uint32_t* xn_lo;  // x^(8n) mod P, n < 65536
-    const uint32_t* xn_hi;  // x^(8*65536*q) mod P, q < 65536
-    const uint32_t* init;   // INIT[r], r < 32
+// Staged-kernel geometry: W waves per workgroup (one workgroup per CU), SB
+// 32-byte blocks per lane per stage, NB stage buffers per wave (NB-1 stages in
+// flight while one is folded).  LDS = 32 KiB tables + W * NB * SB * 2 KiB.
+template <int W, int SB, int NB>
+struct StagedGeom {
+    static constexpr int kWaves = W, kSB = SB, kNB = NB;
+    static constexpr int kThreads = 64 * W;
+    static constexpr uint32_t kRun = 32u * SB;                 // bytes per lane per stage
+    static constexpr uint32_t kStage = 64u * kRun;             // bytes per wave per stage
+    static constexpr uint32_t kSlice = kStage * NB;            // LDS per wave
+    static constexpr int kLds = kLdsTableBytes + W * static_cast<int>(kSlice);
+    static constexpr int kDma = static_cast<int>(kStage / 1024u);       // DMA instructions per stage
+    static constexpr uint32_t kPieces = kRun / 16u;                     // 16-byte pieces per run
+    static constexpr uint32_t kRunsPerDma = 1024u / kRun;
+    static_assert(kLds <= 160 * 1024, "LDS budget");
 };
 
-// ------------------------------------------------------------------ device helpers
-
-__device__ __forceinline__ u32x4 ldg16(const uint8_t* p) {
-    u32x4 v;
-    __builtin_memcpy(&v, p, 16);  // global_load_dwordx4 (unaligned access mode on gfx950)
-    return v;
-}
-
-// 16 bytes at A, with bytes in front of the packet start `a` read as zero.
-// Precondition: every byte of [max(A,a), A+16) belongs to the packet.
-__device__ __forceinline__ u32x4 ldg16_head(const uint8_t* A, const uint8_t* a) {
-    if (A >= a) return ldg16(A);
-    if (A + 16 <= a) return u32x4{0u, 0u, 0u, 0u};
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int b = 0; b < 16; ++b)
-        if (A + b >= a) w[b >> 2] |= static_cast<uint32_t>(A[b]) << (8 * (b & 3));
-    return u32x4{w[0], w[1], w[2], w[3]};
-}
-
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-
-// Per-lane constants of the conflict-free slicing-by-32 schedule.
-struct LaneSched {
-    uint32_t col[8];  // byte h of col[g]: LDS column byte offset for step i = 4g + h
-    uint32_t sel[4];  // v_perm selector for steps with i & 3 == h
-    bool swap1, swap2;
-};
-
-__device__ __forceinline__ LaneSched make_sched(uint32_t lane) {
-    LaneSched s;
-    const uint32_t v = lane & 15u, c = (lane >> 4) & 1u;
-#pragma unroll
-    for (int g = 0; g < 8; ++g) {
-        uint32_t r = 0;
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-            const uint32_t i = 4u * g + h;
-            const uint32_t t = (i ^ v) ^ 31u;        // table of byte m = i ^ v
-            r |= (8u * t + 4u * c) << (8 * h);       // dword column 2t + c
-        }
-        s.col[g] = r;
-    }
-#pragma unroll
-    for (int h = 0; h < 4; ++h)
-        s.sel[h] = static_cast<uint32_t>(h) | ((4u + (static_cast<uint32_t>(h) ^ (v & 3u))) << 8) | 0x0C0C0000u;
-    s.swap1 = (v >> 2) & 1u;
-    s.swap2 = (v >> 3) & 1u;
-    return s;
-}
-
-// One 32-byte block folded into register `reg` (== 32 Sarwate steps, packet.cs:153).
-__device__ __forceinline__ uint32_t fold_block(uint32_t reg, u32x4 h0, u32x4 h1, const uint8_t* lds,
-                                               const LaneSched& s) {
-    uint32_t w[8] = {h0.x ^ reg, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-    uint32_t x[8], d[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) x[q] = s.swap1 ? w[q ^ 1] : w[q];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) d[q] = s.swap2 ? x[q ^ 2] : x[q];
-    uint32_t v[32];
-#pragma unroll
-    for (int i = 0; i < 32; ++i) {
-        const uint32_t addr = __builtin_amdgcn_perm(d[i >> 2], s.col[i >> 2], s.sel[i & 3]);
-        v[i] = *reinterpret_cast<const uint32_t*>(lds + addr);
-    }
-    uint32_t acc = xor3(v[0], v[1], v[2]);
-#pragma unroll
-    for (int i = 3; i + 1 < 32; i += 2) acc = xor3(acc, v[i], v[i + 1]);
-    return acc ^ v[31];
-}
-
-__device__ __forceinline__ uint32_t mulmod(uint32_t a, uint32_t b) {
-    uint32_t p = 0;
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-        const uint32_t m = static_cast<uint32_t>(static_cast<int32_t>(a << j) >> 31);
-        p = __builtin_amdgcn_bitop3_b32(p, b, m, 0x78);                 // p ^ (b & m)
-        const uint32_t r = static_cast<uint32_t>(static_cast<int32_t>(b << 31) >> 31);
-        b = __builtin_amdgcn_bitop3_b32(b >> 1, kPoly, r, 0x78);         // (b>>1) ^ (P & r)
-    }
-    return p;
-}
-
-__device__ __forceinline__ uint32_t x8n_dev(uint32_t n, const KernelTables& tb) {
-    uint32_t x = tb.xn_lo[n & 0xFFFFu];
-    if (n >> 16) x = mulmod(x, tb.xn_hi[n >> 16]);
-    return x;
-}
-
-// Register after feeding blocks [j0, j1) of the end-aligned window of packet
-// bytes [a, a+L), starting from `reg`.  nb = ceil(L/32), rp = 32*nb - L.
-// 4-deep register prefetch ring (software pipeline over HBM latency).
-__device__ __forceinline__ uint32_t fold_window(uint32_t reg, const uint8_t* a, uint32_t L, uint32_t nb,
-                                                uint32_t j0, uint32_t j1, const uint8_t* lds,
-                                                const LaneSched& s) {
-    const uint8_t* W = a + L - (static_cast<size_t>(nb) << 5);
-    uint32_t j = j0;
-    const bool head = (j == 0) && (j < j1) && ((nb << 5) != L);
-    if (head) j = 1;
-    u32x4 r0a = {}, r0b = {}, r1a = {}, r1b = {}, r2a = {}, r2b = {}, r3a = {}, r3b = {};
-    if (j + 0 < j1) { r0a = ldg16(W + 32 * (j + 0)); r0b = ldg16(W + 32 * (j + 0) + 16); }
-    if (j + 1 < j1) { r1a = ldg16(W + 32 * (j + 1)); r1b = ldg16(W + 32 * (j + 1) + 16); }
-    if (j + 2 < j1) { r2a = ldg16(W + 32 * (j + 2)); r2b = ldg16(W + 32 * (j + 2) + 16); }
-    if (j + 3 < j1) { r3a = ldg16(W + 32 * (j + 3)); r3b = ldg16(W + 32 * (j + 3) + 16); }
-    if (head) {
-        const u32x4 ha = ldg16_head(W, a), hb = ldg16_head(W + 16, a);
-        reg = fold_block(reg, ha, hb, lds, s);
-    }
-    while (j < j1) {
-        reg = fold_block(reg, r0a, r0b, lds, s);
-        if (j + 4 < j1) { r0a = ldg16(W + 32 * (j + 4)); r0b = ldg16(W + 32 * (j + 4) + 16); }
-        if (++j >= j1) break;
-        reg = fold_block(reg, r1a, r1b, lds, s);
-        if (j + 4 < j1) { r1a = ldg16(W + 32 * (j + 4)); r1b = ldg16(W + 32 * (j + 4) + 16); }
-        if (++j >= j1) break;
-        reg = fold_block(reg, r2a, r2b, lds, s);
-        if (j + 4 < j1) { r2a = ldg16(W + 32 * (j + 4)); r2b = ldg16(W + 32 * (j + 4) + 16); }
-        if (++j >= j1) break;
-        reg = fold_block(reg, r3a, r3b, lds, s);
-        if (j + 4 < j1) { r3a = ldg16(W + 32 * (j + 4)); r3b = ldg16(W + 32 * (j + 4) + 16); }
-        ++j;
-    }
-    return reg;
-}
-
-__device__ __forceinline__ void fill_lds(uint8_t* lds, const uint32_t* image) {
+template <int NT>
+__device__ __forceinline__ void fill_table(uint8_t* lds, const uint32_t* image) {
     const u32x4* src = reinterpret_cast<const u32x4*>(image);
     u32x4* dst = reinterpret_cast<u32x4*>(lds);
-#pragma unroll 4
-    for (int i = threadIdx.x; i < kLdsImageBytes / 16; i += kThreads) dst[i] = src[i];
+#pragma unroll
+    for (int i = threadIdx.x; i < kLdsTableBytes / 16; i += NT) dst[i] = src[i];
     __syncthreads();
 }
 
@@ -199,60 +80,224 @@ struct PacketArgs {
     uint8_t* ok;
 };
 
-// MODE 0: out[p] = enet_crc32(packet p).  MODE 1: receive verify.
-template <int MODE>
-__global__ void __launch_bounds__(kThreads) crc32_packets_kernel(PacketArgs pa, KernelTables tb) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    fill_lds(lds, tb.image);
-    const uint32_t lane = threadIdx.x & 63u;
-    const LaneSched s = make_sched(lane);
+// One lane's share of one packet: packet pk = [a, a+L) is cut into P = 2^lg
+// segments at 128-byte-aligned ABSOLUTE addresses (nearest to the even split),
+// so no cache line is shared by two lanes' segments (shared lines were fetched
+// twice, microseconds apart: 1.57x HBM over-fetch measured).  Lane k folds its
+// segment [sp, sp+len) as an END-aligned window of nb 32-byte blocks with rp
+// zero bytes in front; its partial register is later advanced by `after` bytes.
+struct Task {
+    const uint8_t* a;   // packet start
+    const uint8_t* sp;  // segment start
+    uint64_t pk;
+    uint32_t L, len, nb, rp, after, k;
+    bool active;
+};
+
+__device__ __forceinline__ Task make_task(const PacketArgs& pa, uint64_t t, uint64_t total) {
+    Task tk;
     const uint32_t P = 1u << pa.lg;
+    tk.active = t < total;
+    tk.pk = t >> pa.lg;
+    tk.k = static_cast<uint32_t>(t) & (P - 1u);
+    tk.L = 0;
+    tk.a = pa.bytes;
+    if (tk.active) {
+        tk.L = pa.len[tk.pk];
+        tk.a = pa.bytes + pa.off[tk.pk];
+    }
+    const uint64_t A = reinterpret_cast<uint64_t>(tk.a), E = A + tk.L;
+    auto cut = [&](uint32_t k) -> uint64_t {
+        if (k == 0) return A;
+        if (k >= P) return E;
+        const uint64_t r = (A + ((static_cast<uint64_t>(tk.L) * k) >> pa.lg) + 64u) & ~static_cast<uint64_t>(127);
+        return min(max(r, A), E);
+    };
+    const uint64_t s0 = cut(tk.k), s1 = cut(tk.k + 1);
+    tk.sp = reinterpret_cast<const uint8_t*>(s0);
+    tk.len = static_cast<uint32_t>(s1 - s0);
+    tk.nb = (tk.len + 31u) >> 5;
+    tk.rp = (tk.nb << 5) - tk.len;
+    tk.after = static_cast<uint32_t>(E - s1);
+    return tk;
+}
+
+// Carry-combine the P partial registers of each packet and write the result.
+template <int MODE>
+__device__ __forceinline__ void finish_task(const PacketArgs& pa, const Task& tk, uint32_t reg,
+                                            const KernelTables& tb) {
+    if (tk.after) reg = mulmod(reg, x8n_dev(tk.after, tb));    // reg(A||B) = reg(A) x^(8|B|) ^ reg(B)
+    for (uint32_t m = 1; m < (1u << pa.lg); m <<= 1) reg ^= __shfl_xor(reg, static_cast<int>(m));
+    if (!tk.active || tk.k != 0) return;
+    if (MODE == 0) {
+        pa.out[tk.pk] = finalize(reg);                            // packet.cs:159
+    } else {
+        // protocol.cs:1052-1068: desired = slot; slot := connectID; crc over the
+        // DGRAM; keep iff equal.  By linearity the substitution adds
+        // (slot ^ connectID) fed at byte offset so, followed by L-so zero bytes.
+        const uint32_t so = pa.slot_off[tk.pk];
+        uint32_t comp = 0;
+        uint8_t okv = 0;
+        if (so <= tk.L && tk.L - so >= 4u) {
+            uint32_t desired;
+            __builtin_memcpy(&desired, tk.a + so, 4);
+            const uint32_t delta = desired ^ pa.connect[tk.pk];
+            const uint32_t fixed = reg ^ mulmod(delta, x8n_dev(tk.L - so, tb));
+            comp = finalize(fixed);
+            okv = (comp == desired) ? 1 : 0;
+        }
+        pa.ok[tk.pk] = okv;
+        if (pa.out) pa.out[tk.pk] = comp;
+    }
+}
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
+    const uint32_t lo = __shfl(static_cast<uint32_t>(v), static_cast<int>(src));
+    const uint32_t hi = __shfl(static_cast<uint32_t>(v >> 32), static_cast<int>(src));
+    return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+// Staged fold of this lane's segment window, all lanes of the wave cooperating
+// on the loads.  Precondition (checked by the caller for the whole wave): every
+// lane's window start Wp = sp + len - 32*nb is 16-byte aligned.
+//
+// A stage = SB blocks of every lane (64 * 32 * SB bytes), NB-buffered in the
+// wave's own LDS slice, NB-1 stages in flight while one is folded.  Lane c's run
+// sits at buf + kRun*c, its 16-byte piece p in slot p ^ swz(c) with
+// swz(c) = ((c >> log2(16/R)) & (R-1)) ^ ((c >> 4) & 1), R = pieces per run,
+// which keeps every 16-lane ds_read_b128 group of gfx950 on 16 distinct slots
+// (the (c >> 4) term undoes the lane's half swap).  A stage arrives by kDma
+// LDS-DMA instructions (global_load_lds_dwordx4), each fetching kRunsPerDma
+// whole runs with kPieces lanes per run.  Only the issuing wave reads its slice,
+// so its own s_waitcnt vmcnt orders DMA and ds_read (no barrier).
+template <class G>
+__device__ __forceinline__ uint32_t run_swz(uint32_t c) {
+    constexpr uint32_t R = G::kPieces;
+    constexpr uint32_t sh = R == 2 ? 3u : R == 4 ? 2u : R == 8 ? 1u : 0u;
+    return ((c >> sh) & (R - 1u)) ^ ((c >> 4) & 1u);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_stages(uint32_t n) {
+    // s_waitcnt needs an immediate: n stages of N DMA instructions may stay in flight
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * N) : "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * N) : "memory"); break;
+    }
+}
+
+template <class G, int ABL>  // ABL (diagnostics only): 0 = real, 1 = no table lookups, 2 = no DMA
+__device__ __forceinline__ uint32_t fold_staged(uint32_t reg, const Task& tk, const LaneSched& s,
+                                                uint32_t slice, const uint8_t* safe) {
+    static_assert(G::kNB <= 4, "wait_vmcnt_stages covers up to 3 stages in flight");
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t cnt = tk.nb;
+    const bool head = cnt && tk.rp;
+    const uint64_t src0 = cnt ? reinterpret_cast<uint64_t>(tk.sp + tk.len) - 32ull * tk.nb
+                              : reinterpret_cast<uint64_t>(safe);
+    // last block | (block 0 half 0 lies wholly in front of the segment) << 31
+    const uint32_t meta = (cnt ? cnt - 1u : 0u) | ((head && tk.rp >= 16u) ? 0x80000000u : 0u);
+    uint64_t dsrc[G::kDma];
+    uint32_t dlast[G::kDma], dpiece[G::kDma];
+#pragma unroll
+    for (int i = 0; i < G::kDma; ++i) {
+        const uint32_t c = G::kRunsPerDma * i + lane / G::kPieces;
+        dsrc[i] = shfl64(src0, c);
+        dlast[i] = __shfl(meta, static_cast<int>(c));
+        dpiece[i] = (lane % G::kPieces) ^ run_swz<G>(c);
+    }
+    const uint32_t trips = wave_max(cnt);
+    const uint32_t stages = (trips + G::kSB - 1) / G::kSB;
+    const uint32_t swz = run_swz<G>(lane);
+    const uint32_t hsb = s.hs & 1u;
+
+    auto issue = [&](uint32_t st) {
+        const uint32_t buf = slice + (st % G::kNB) * G::kStage;
+#pragma unroll
+        for (int i = 0; i < G::kDma; ++i) {
+            const uint32_t last = dlast[i] & 0x7FFFFFFFu;
+            const uint32_t kk = min(G::kSB * st + (dpiece[i] >> 1), last);
+            uint64_t g = dsrc[i] + 32ull * kk + 16ull * (dpiece[i] & 1u);
+            if (kk == 0 && (dpiece[i] & 1u) == 0 && (dlast[i] >> 31)) g += 16;   // stay inside the buffer
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g),
+                                             reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                                 static_cast<uintptr_t>(buf + 1024u * i)),
+                                             16, 0, 0);
+        }
+    };
+
+    if (ABL != 2)
+        for (uint32_t p = 0; p + 1 < G::kNB && p < stages; ++p) issue(p);
+    for (uint32_t st = 0; st < stages; ++st) {
+        if (st + G::kNB - 1 < stages) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // WAR on the buffer being refilled
+            if (ABL != 2) issue(st + G::kNB - 1);
+        }
+        const uint32_t ahead = min(stages - 1u, st + G::kNB - 1u) - st;   // stages issued after st
+        wait_vmcnt_stages<G::kDma>(ABL == 2 ? 0u : ahead);
+        const uint32_t base = slice + (st % G::kNB) * G::kStage + G::kRun * lane;
+#pragma unroll
+        for (int b = 0; b < G::kSB; ++b) {
+            const uint32_t blk = G::kSB * st + b;
+            if (blk >= trips) break;
+            u32x4 A = *reinterpret_cast<lds_u32x4*>(static_cast<uintptr_t>(base + 16u * ((2u * b + hsb) ^ swz)));
+            u32x4 B = *reinterpret_cast<lds_u32x4*>(static_cast<uintptr_t>(base + 16u * ((2u * b + (hsb ^ 1u)) ^ swz)));
+            if (head && blk == 0) {                                   // bytes in front of the segment are zero
+                const uint32_t z0 = min(tk.rp, 16u), z1 = tk.rp > 16u ? tk.rp - 16u : 0u;
+                A = zero_prefix(A, hsb ? z1 : z0);
+                B = zero_prefix(B, hsb ? z0 : z1);
+            }
+            const uint32_t nr = ABL == 1 ? xor3(reg ^ A.x ^ A.y, A.z ^ A.w ^ B.x, B.y ^ B.z ^ B.w)
+                                         : fold_block_lane(reg, A, B, s);
+            reg = blk < cnt ? nr : reg;
+        }
+    }
+    return reg;
+}
+
+// MODE 0: out[p] = enet_crc32(packet p).  MODE 1: receive verify.
+// Persistent: one workgroup of G::kWaves waves per CU; each wave takes 64
+// consecutive tasks at a time.
+template <int MODE, class G, int ABL = 0>
+__global__ void __launch_bounds__(G::kThreads) crc32_staged_kernel(PacketArgs pa, KernelTables tb) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    fill_table<G::kThreads>(lds, tb.image);
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const LaneSched s = make_sched(lane);
+    const uint32_t slice = kLdsTableBytes + wave * G::kSlice;
+    const uint64_t total = pa.n << pa.lg;
+    const uint64_t waves_total = static_cast<uint64_t>(gridDim.x) * G::kWaves;
+    const uint8_t* safe = reinterpret_cast<const uint8_t*>(tb.xn_lo);
+    for (uint64_t wv = static_cast<uint64_t>(blockIdx.x) * G::kWaves + wave; wv * 64 < total; wv += waves_total) {
+        const Task tk = make_task(pa, wv * 64 + lane, total);
+        uint32_t reg = (tk.k == 0) ? tb.init[tk.rp] : 0u;
+        const bool aligned = (tk.len == 0) || ((reinterpret_cast<uintptr_t>(tk.sp + tk.len) & 15u) == 0);
+        if (__all(aligned))
+            reg = fold_staged<G, ABL>(reg, tk, s, slice, safe);
+        else
+            reg = fold_window(reg, tk.sp, tk.len, s, safe);
+        finish_task<MODE>(pa, tk, reg, tb);
+    }
+}
+
+// General direct-load kernel (every block loaded straight into VGPRs); kept as
+// the comparison point and selectable through enet_hip_set_tuning's path knob.
+template <int MODE>
+__global__ void __launch_bounds__(kThreads) crc32_direct_kernel(PacketArgs pa, KernelTables tb) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    fill_table<kThreads>(lds, tb.image);
+    const LaneSched s = make_sched(threadIdx.x & 63u);
     const uint64_t total = pa.n << pa.lg;
     const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
+    const uint8_t* safe = reinterpret_cast<const uint8_t*>(tb.xn_lo);
     for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * kThreads + (threadIdx.x & ~63u); base < total;
          base += stride) {
-        const uint64_t t = base + lane;
-        const bool active = t < total;
-        const uint64_t pk = t >> pa.lg;
-        const uint32_t k = static_cast<uint32_t>(t) & (P - 1u);
-        uint32_t L = 0;
-        const uint8_t* a = pa.bytes;
-        if (active) {
-            L = pa.len[pk];
-            a = pa.bytes + pa.off[pk];
-        }
-        const uint32_t nb = (L + 31u) >> 5;
-        const uint32_t rp = (nb << 5) - L;
-        const uint32_t per = nb >> pa.lg, rem = nb & (P - 1u);
-        const uint32_t j0 = k * per + min(k, rem);
-        const uint32_t j1 = j0 + per + (k < rem ? 1u : 0u);
-        uint32_t reg = (k == 0) ? tb.init[rp] : 0u;
-        reg = fold_window(reg, a, L, nb, j0, j1, lds, s);
-        const uint32_t after = nb - j1;
-        if (after) reg = mulmod(reg, x8n_dev(after << 5, tb));
-        for (uint32_t m = 1; m < P; m <<= 1) reg ^= __shfl_xor(reg, static_cast<int>(m));
-        if (active && k == 0) {
-            if (MODE == 0) {
-                pa.out[pk] = finalize(reg);
-            } else {
-                // protocol.cs:1052-1068: desired = slot; slot := connectID; crc over the
-                // DGRAM; keep iff equal.  By linearity the substitution adds
-                // (slot ^ connectID) fed at byte offset so, followed by L-so zero bytes.
-                const uint32_t so = pa.slot_off[pk];
-                uint32_t comp = 0;
-                uint8_t okv = 0;
-                if (so <= L && L - so >= 4u) {
-                    uint32_t desired;
-                    __builtin_memcpy(&desired, a + so, 4);
-                    const uint32_t delta = desired ^ pa.connect[pk];
-                    const uint32_t fixed = reg ^ mulmod(delta, x8n_dev(L - so, tb));
-                    comp = finalize(fixed);
-                    okv = (comp == desired) ? 1 : 0;
-                }
-                pa.ok[pk] = okv;
-                if (pa.out) pa.out[pk] = comp;
-            }
-        }
+        const Task tk = make_task(pa, base + (threadIdx.x & 63u), total);
+        uint32_t reg = (tk.k == 0) ? tb.init[tk.rp] : 0u;
+        reg = fold_window(reg, tk.sp, tk.len, s, safe);
+        finish_task<MODE>(pa, tk, reg, tb);
     }
 }
 
@@ -268,7 +313,7 @@ struct GatherArgs {
 // One lane per DGRAM; segments folded in order and joined by the carry-combine.
 __global__ void __launch_bounds__(kThreads) crc32_gather_kernel(GatherArgs ga, KernelTables tb) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    fill_lds(lds, tb.image);
+    fill_table<kThreads>(lds, tb.image);
     const LaneSched s = make_sched(threadIdx.x & 63u);
     const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
     for (uint64_t d = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; d < ga.n; d += stride) {
@@ -282,10 +327,10 @@ __global__ void __launch_bounds__(kThreads) crc32_gather_kernel(GatherArgs ga, K
             const uint32_t nb = (L + 31u) >> 5;
             const uint32_t rp = (nb << 5) - L;
             if (first) {
-                reg = fold_window(tb.init[rp], a, L, nb, 0, nb, lds, s);
+                reg = fold_window(tb.init[rp], a, L, s, reinterpret_cast<const uint8_t*>(tb.xn_lo));
                 first = false;
             } else {
-                const uint32_t part = fold_window(0u, a, L, nb, 0, nb, lds, s);
+                const uint32_t part = fold_window(0u, a, L, s, reinterpret_cast<const uint8_t*>(tb.xn_lo));
                 reg = mulmod(reg, x8n_dev(L, tb)) ^ part;
             }
         }
@@ -323,7 +368,9 @@ struct enet_hip_context {
     uint32_t* d_xn = nullptr;    // lo[65536] | hi[65536]
     uint32_t* d_init = nullptr;  // 32
     int lanes_per_packet = 0;    // 0 = auto
-    int wgs_per_cu = 0;          // 0 = auto
+    int wgs_per_cu = 0;          // 0 = auto (direct / gather kernels)
+    int path = 0;                // 0 = staged (auto), 1 = direct
+    int ablation = 0;            // diagnostics: 1 = no lookups, 2 = no DMA (wrong CRCs by design)
     // staging for the host-memory entry points
     std::mutex mu;
     uint8_t* d_bytes = nullptr;
@@ -344,15 +391,15 @@ int herr(hipError_t e) { return e == hipSuccess ? 0 : -static_cast<int>(e); }
 
 struct HostTables {
     std::vector<uint32_t> image, xn, init;
-    HostTables() : image(kLdsImageBytes / 4), xn(2 * kXnEntries), init(32) {
+    HostTables() : image(kLdsTableBytes / 4), xn(2 * kXnEntries), init(32) {
         // slicing tables T_t[j] = byte j followed by t zero bytes (t < 32)
         static uint32_t T[32][256];
         for (uint32_t j = 0; j < 256; ++j) T[0][j] = crc_table_entry(j);
         for (int t = 1; t < 32; ++t)
             for (uint32_t j = 0; j < 256; ++j) T[t][j] = (T[t - 1][j] >> 8) ^ T[0][T[t - 1][j] & 0xFFu];
+        // LDS image: row j (128 B) = T_0[j] .. T_31[j] (crc32_device.hpp)
         for (uint32_t j = 0; j < 256; ++j)
-            for (uint32_t t = 0; t < 32; ++t)
-                for (uint32_t c = 0; c < 2; ++c) image[j * 64 + 2 * t + c] = T[t][j];
+            for (uint32_t t = 0; t < 32; ++t) image[j * 32 + t] = T[t][j];
         // x^(8n) for n < 65536: one zero-byte step per n
         xn[0] = kOneReflected;
         for (int n = 1; n < kXnEntries; ++n) xn[n] = sarwate_step(xn[n - 1], 0);
@@ -388,14 +435,80 @@ unsigned grid_for(const enet_hip_context* ctx, uint64_t tasks) {
     return static_cast<unsigned>(std::max<uint64_t>(1, std::min(need, cap)));
 }
 
+// Staged geometries (waves per CU, blocks per stage, buffers).  kStagedDefault is
+// what path 0 runs; the others are reachable through enet_hip_set_kernel_path
+// (2 + index) for tuning sweeps.
+template <class G>
+struct StagedVariant {
+    static void launch(int mode, int abl, unsigned grid, hipStream_t st, const PacketArgs& pa,
+                       const KernelTables& tb) {
+        if (mode == 1)
+            hipLaunchKernelGGL((crc32_staged_kernel<1, G>), dim3(grid), dim3(G::kThreads), G::kLds, st, pa, tb);
+        else if (abl == 1)
+            hipLaunchKernelGGL((crc32_staged_kernel<0, G, 1>), dim3(grid), dim3(G::kThreads), G::kLds, st, pa, tb);
+        else if (abl == 2)
+            hipLaunchKernelGGL((crc32_staged_kernel<0, G, 2>), dim3(grid), dim3(G::kThreads), G::kLds, st, pa, tb);
+        else
+            hipLaunchKernelGGL((crc32_staged_kernel<0, G, 0>), dim3(grid), dim3(G::kThreads), G::kLds, st, pa, tb);
+    }
+    static int setup() {
+        const void* fns[] = {reinterpret_cast<const void*>(crc32_staged_kernel<0, G, 0>),
+                             reinterpret_cast<const void*>(crc32_staged_kernel<0, G, 1>),
+                             reinterpret_cast<const void*>(crc32_staged_kernel<0, G, 2>),
+                             reinterpret_cast<const void*>(crc32_staged_kernel<1, G, 0>)};
+        for (const void* f : fns) {
+            const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, G::kLds);
+            if (e != hipSuccess) return herr(e);
+        }
+        return 0;
+    }
+};
+
+using StagedGeoms = std::tuple<StagedGeom<16, 2, 2>, StagedGeom<8, 2, 4>, StagedGeom<8, 4, 2>,
+                               StagedGeom<16, 1, 4>, StagedGeom<10, 2, 3>, StagedGeom<5, 4, 3>>;
+constexpr int kNumStagedGeoms = std::tuple_size<StagedGeoms>::value;
+constexpr int kStagedDefault = 0;
+
+template <size_t I = 0>
+void launch_staged(int geom, int mode, int abl, int num_cus, uint64_t tasks, hipStream_t st,
+                   const PacketArgs& pa, const KernelTables& tb) {
+    if constexpr (I < std::tuple_size<StagedGeoms>::value) {
+        using G = std::tuple_element_t<I, StagedGeoms>;
+        if (geom == static_cast<int>(I)) {
+            const uint64_t waves = (tasks + 63) / 64;
+            const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(
+                1, std::min<uint64_t>((waves + G::kWaves - 1) / G::kWaves, static_cast<uint64_t>(num_cus))));
+            StagedVariant<G>::launch(mode, abl, grid, st, pa, tb);
+        } else {
+            launch_staged<I + 1>(geom, mode, abl, num_cus, tasks, st, pa, tb);
+        }
+    }
+}
+
+template <size_t I = 0>
+int setup_staged() {
+    if constexpr (I < std::tuple_size<StagedGeoms>::value) {
+        const int rc = StagedVariant<std::tuple_element_t<I, StagedGeoms>>::setup();
+        return rc ? rc : setup_staged<I + 1>();
+    }
+    return 0;
+}
+
 int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStream_t st) {
     if (pa.n == 0) return 0;
     const uint64_t tasks = pa.n << pa.lg;
-    const unsigned grid = grid_for(ctx, tasks);
-    if (mode == 0)
-        hipLaunchKernelGGL(crc32_packets_kernel<0>, dim3(grid), dim3(kThreads), kLdsImageBytes, st, pa, tables_of(ctx));
-    else
-        hipLaunchKernelGGL(crc32_packets_kernel<1>, dim3(grid), dim3(kThreads), kLdsImageBytes, st, pa, tables_of(ctx));
+    const KernelTables tb = tables_of(ctx);
+    if (ctx->path != 1) {
+        // persistent: one workgroup per CU (up to 160 KiB LDS each)
+        const int geom = ctx->path == 0 ? kStagedDefault : ctx->path - 2;
+        launch_staged(geom, mode, ctx->ablation, ctx->num_cus, tasks, st, pa, tb);
+    } else {
+        const unsigned grid = grid_for(ctx, tasks);
+        if (mode == 0)
+            hipLaunchKernelGGL(crc32_direct_kernel<0>, dim3(grid), dim3(kThreads), kLdsTableBytes, st, pa, tb);
+        else
+            hipLaunchKernelGGL(crc32_direct_kernel<1>, dim3(grid), dim3(kThreads), kLdsTableBytes, st, pa, tb);
+    }
     return herr(hipGetLastError());
 }
 
@@ -444,18 +557,19 @@ int enet_hip_context_create(int device, enet_hip_context** out) {
     int rc = 0;
     do {
         if ((rc = herr(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)))) break;
-        if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_image), kLdsImageBytes)))) break;
+        if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_image), kLdsTableBytes)))) break;
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_xn), ht.xn.size() * 4)))) break;
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_init), 32 * 4)))) break;
-        if ((rc = herr(hipMemcpy(ctx->d_image, ht.image.data(), kLdsImageBytes, hipMemcpyHostToDevice)))) break;
+        if ((rc = herr(hipMemcpy(ctx->d_image, ht.image.data(), kLdsTableBytes, hipMemcpyHostToDevice)))) break;
         if ((rc = herr(hipMemcpy(ctx->d_xn, ht.xn.data(), ht.xn.size() * 4, hipMemcpyHostToDevice)))) break;
         if ((rc = herr(hipMemcpy(ctx->d_init, ht.init.data(), 32 * 4, hipMemcpyHostToDevice)))) break;
-        if ((rc = herr(hipFuncSetAttribute(reinterpret_cast<const void*>(crc32_packets_kernel<0>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, kLdsImageBytes)))) break;
-        if ((rc = herr(hipFuncSetAttribute(reinterpret_cast<const void*>(crc32_packets_kernel<1>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, kLdsImageBytes)))) break;
+        if ((rc = setup_staged())) break;
+        if ((rc = herr(hipFuncSetAttribute(reinterpret_cast<const void*>(crc32_direct_kernel<0>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTableBytes)))) break;
+        if ((rc = herr(hipFuncSetAttribute(reinterpret_cast<const void*>(crc32_direct_kernel<1>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTableBytes)))) break;
         if ((rc = herr(hipFuncSetAttribute(reinterpret_cast<const void*>(crc32_gather_kernel),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, kLdsImageBytes)))) break;
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTableBytes)))) break;
     } while (0);
     if (rc) {
         enet_hip_context_destroy(ctx);
@@ -486,6 +600,18 @@ int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgro
     if (workgroups_per_cu < 0 || workgroups_per_cu > 8) return -static_cast<int>(hipErrorInvalidValue);
     ctx->lanes_per_packet = lanes_per_packet;
     ctx->wgs_per_cu = workgroups_per_cu;
+    return 0;
+}
+
+int enet_hip_diag_ablation(enet_hip_context* ctx, int mode) {
+    if (!ctx || mode < 0 || mode > 2) return -static_cast<int>(hipErrorInvalidValue);
+    ctx->ablation = mode;
+    return 0;
+}
+
+int enet_hip_set_kernel_path(enet_hip_context* ctx, int path) {
+    if (!ctx || path < 0 || path > 1 + kNumStagedGeoms) return -static_cast<int>(hipErrorInvalidValue);
+    ctx->path = path;
     return 0;
 }
 
@@ -535,7 +661,7 @@ int enet_hip_crc32_gather_device(enet_hip_context* ctx, const uint8_t* bytes, co
     ENH_CHECK(hipSetDevice(ctx->device));
     GatherArgs ga{bytes, segOffsets, segLengths, segFirst, dgramCount, out};
     const unsigned grid = grid_for(ctx, dgramCount);
-    hipLaunchKernelGGL(crc32_gather_kernel, dim3(grid), dim3(kThreads), kLdsImageBytes,
+    hipLaunchKernelGGL(crc32_gather_kernel, dim3(grid), dim3(kThreads), kLdsTableBytes,
                        stream ? static_cast<hipStream_t>(stream) : ctx->stream, ga, tables_of(ctx));
     return herr(hipGetLastError());
 }

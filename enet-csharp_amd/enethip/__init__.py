@@ -30,7 +30,8 @@ EXPORTED_SYMBOLS = (
     "enet_hip_crc32_batch_device", "enet_hip_crc32_batch_host", "enet_hip_verify_batch_device",
     "enet_hip_crc32_gather_device", "enet_hip_crc32_batch_multi", "enet_hip_device_alloc",
     "enet_hip_device_free", "enet_hip_host_alloc", "enet_hip_host_free", "enet_hip_memcpy_h2d",
-    "enet_hip_memcpy_d2h", "enet_hip_synchronize", "enet_hip_read_probe_device",
+    "enet_hip_memcpy_d2h", "enet_hip_synchronize", "enet_hip_read_probe_device", "enet_hip_set_kernel_path",
+    "enet_hip_diag_ablation",
 )
 
 
@@ -71,6 +72,10 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.enet_hip_error_string.argtypes = [i32]
     L.enet_hip_set_tuning.restype = i32
     L.enet_hip_set_tuning.argtypes = [vp, i32, i32]
+    L.enet_hip_diag_ablation.restype = i32
+    L.enet_hip_diag_ablation.argtypes = [vp, i32]
+    L.enet_hip_set_kernel_path.restype = i32
+    L.enet_hip_set_kernel_path.argtypes = [vp, i32]
     L.enet_hip_crc32_batch_device.restype = i32
     L.enet_hip_crc32_batch_device.argtypes = [vp, vp, vp, vp, sz, vp, vp]
     L.enet_hip_crc32_batch_host.restype = i32
@@ -159,6 +164,14 @@ class Context:
 
     def set_tuning(self, lanes_per_packet: int = 0, workgroups_per_cu: int = 0) -> None:
         _check("enet_hip_set_tuning", self.lib.enet_hip_set_tuning(self.handle, lanes_per_packet, workgroups_per_cu))
+
+    def set_kernel_path(self, path: int) -> None:
+        """0 = LDS-staged (default), 1 = direct loads."""
+        _check("enet_hip_set_kernel_path", self.lib.enet_hip_set_kernel_path(self.handle, int(path)))
+
+    def diag_ablation(self, mode: int) -> None:
+        """Diagnostics only: 1 = no lookups, 2 = no DMA (wrong CRCs by design)."""
+        _check("enet_hip_diag_ablation", self.lib.enet_hip_diag_ablation(self.handle, int(mode)))
 
     def close(self) -> None:
         if getattr(self, "handle", None):

@@ -75,6 +75,11 @@ ENET_HIP_API const char* enet_hip_error_string(int code);
  * persistent grid is sized for. */
 ENET_HIP_API int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgroups_per_cu);
 
+/* Kernel path for the packet batch entry points: 0 = LDS-staged (default; waves
+ * whose windows are not 16-byte aligned fall back to direct loads inside the
+ * same launch), 1 = direct loads only. */
+ENET_HIP_API int enet_hip_set_kernel_path(enet_hip_context* ctx, int path);
+
 /* ---- batched checksum, device-resident ----
  * Packet i is bytes[offsets[i] .. offsets[i]+lengths[i]).  All pointers are
  * device pointers on ctx's device; out[i] receives what enet_crc32 would return
@@ -126,6 +131,12 @@ ENET_HIP_API int enet_hip_crc32_batch_multi(enet_hip_context* const* contexts, i
  * it beside the checksum kernel as the "achievable read bandwidth" line. */
 ENET_HIP_API int enet_hip_read_probe_device(enet_hip_context* ctx, const uint8_t* bytes, size_t byteCount,
                                             uint32_t* sink, void* stream);
+
+/* ---- diagnostics: roofline ablation of the staged kernel ----
+ * 0 = normal; 1 = skip the table lookups (memory path alone); 2 = skip the
+ * LDS-DMA (compute path alone).  Modes 1 and 2 produce WRONG checksums by
+ * design and exist only to price the two halves of the kernel (tools/). */
+ENET_HIP_API int enet_hip_diag_ablation(enet_hip_context* ctx, int mode);
 
 /* ---- small memory helpers (so C#/ctypes hosts need no HIP binding) ---- */
 ENET_HIP_API int enet_hip_device_alloc(enet_hip_context* ctx, size_t bytes, void** out);

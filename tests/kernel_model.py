@@ -34,12 +34,11 @@ TS = slicing_tables(32)
 
 
 def lds_image() -> list[int]:
-    """dword j*64 + 2t + c = T_t[j]  (256 rows x 64 dwords = 64 KiB)."""
-    img = [0] * (256 * 64)
+    """dword j*32 + t = T_t[j]  (256 rows x 32 dwords = 32 KiB, crc32_device.hpp)."""
+    img = [0] * (256 * 32)
     for j in range(256):
         for t in range(32):
-            for c in range(2):
-                img[j * 64 + 2 * t + c] = TS[t][j]
+            img[j * 32 + t] = TS[t][j]
     return img
 
 
@@ -66,25 +65,28 @@ def v_perm(s0: int, s1: int, sel: int) -> int:
 
 
 def make_sched(lane: int):
-    v, c = lane & 15, (lane >> 4) & 1
+    l5 = lane & 31
     col = []
     for g in range(8):
         r = 0
         for h in range(4):
             i = 4 * g + h
-            t = (i ^ v) ^ 31
-            r |= (8 * t + 4 * c) << (8 * h)
+            t = (i ^ l5) ^ 31
+            r |= (8 * t) << (8 * h)
         col.append(r)
-    sel = [h | ((4 + (h ^ (v & 3))) << 8) | 0x0C0C0000 for h in range(4)]
-    return col, sel, bool((v >> 2) & 1), bool((v >> 3) & 1)
+    sel = [h | ((4 + (h ^ (l5 & 3))) << 8) | 0x0C0C0000 for h in range(4)]
+    return col, sel, bool((l5 >> 2) & 1), bool((l5 >> 3) & 1), bool((l5 >> 4) & 1)
 
 
 def lookup_addresses(lane: int, words: list[int]) -> list[int]:
-    """LDS byte address of each of the 32 lookups of fold_block (state already XORed)."""
-    col, sel, sw1, sw2 = make_sched(lane)
-    x = [words[q ^ 1] if sw1 else words[q] for q in range(8)]
+    """LDS byte address of each of the 32 lookups of fold_block (words in original
+    order, state already XORed): halves put in lane order, two dword-swap rounds,
+    then v_perm(...) >> 1."""
+    col, sel, sw1, sw2, hs = make_sched(lane)
+    w = (words[4:8] + words[0:4]) if hs else list(words)
+    x = [w[q ^ 1] if sw1 else w[q] for q in range(8)]
     d = [x[q ^ 2] if sw2 else x[q] for q in range(8)]
-    return [v_perm(d[i >> 2], col[i >> 2], sel[i & 3]) for i in range(32)]
+    return [v_perm(d[i >> 2], col[i >> 2], sel[i & 3]) >> 1 for i in range(32)]
 
 
 def fold_block(reg: int, block: bytes, lane: int) -> int:
@@ -92,7 +94,7 @@ def fold_block(reg: int, block: bytes, lane: int) -> int:
     w[0] ^= reg
     acc = 0
     for addr in lookup_addresses(lane, w):
-        assert addr % 4 == 0 and addr < 65536
+        assert addr % 4 == 0 and addr < 32768
         acc ^= IMG[addr // 4]
     return acc
 
@@ -134,21 +136,33 @@ def fold_window(reg: int, pkt: bytes, j0: int, j1: int, lane: int) -> int:
     return reg
 
 
-def crc_packet(pkt: bytes, lanes: int = 1, lane_base: int = 0) -> int:
-    """What one packet's P lanes compute (packets start at lane_base, a multiple of P)."""
+def segment_cuts(addr: int, L: int, lanes: int) -> list[int]:
+    """make_task's cut points: packet [addr, addr+L) split at 128-byte-aligned
+    absolute addresses nearest to the even split (offsets relative to addr)."""
+    cuts = [0]
+    for k in range(1, lanes):
+        r = (addr + (L * k) // lanes + 64) & ~127
+        cuts.append(min(max(r, addr), addr + L) - addr)
+    cuts.append(L)
+    return cuts
+
+
+def crc_packet(pkt: bytes, lanes: int = 1, lane_base: int = 0, addr: int = 0) -> int:
+    """What one packet's P lanes compute: lane k folds segment [cut_k, cut_k+1) as
+    its own end-aligned window (zero-init except lane 0, which starts at
+    INIT[rp]), then the partial registers are advanced and XORed."""
     L = len(pkt)
-    nb = (L + 31) // 32
-    rp = 32 * nb - L
-    per, rem = nb // lanes, nb % lanes
+    cuts = segment_cuts(addr, L, lanes)
     total = 0
     for k in range(lanes):
-        j0 = k * per + min(k, rem)
-        j1 = j0 + per + (1 if k < rem else 0)
+        seg = pkt[cuts[k]:cuts[k + 1]]
+        nb = (len(seg) + 31) // 32
+        rp = 32 * nb - len(seg)
         reg = INIT[rp] if k == 0 else 0
-        reg = fold_window(reg, pkt, j0, j1, lane_base + k)
-        after = nb - j1
+        reg = fold_window(reg, seg, 0, nb, lane_base + k)
+        after = L - cuts[k + 1]
         if after:
-            reg = mulmod(reg, x8n(32 * after))
+            reg = mulmod(reg, x8n(after))
         total ^= reg
     return int.from_bytes((~total & 0xFFFFFFFF).to_bytes(4, "little"), "big")
 
@@ -157,16 +171,15 @@ def verify_packet(pkt: bytes, slot_off: int, connect: int, lanes: int = 1) -> tu
     L = len(pkt)
     if slot_off + 4 > L:
         return False, 0
-    nb = (L + 31) // 32
-    rp = 32 * nb - L
-    per, rem = nb // lanes, nb % lanes
+    cuts = segment_cuts(0, L, lanes)
     total = 0
     for k in range(lanes):
-        j0 = k * per + min(k, rem)
-        j1 = j0 + per + (1 if k < rem else 0)
-        reg = fold_window(INIT[rp] if k == 0 else 0, pkt, j0, j1, k)
-        if nb - j1:
-            reg = mulmod(reg, x8n(32 * (nb - j1)))
+        seg = pkt[cuts[k]:cuts[k + 1]]
+        nb = (len(seg) + 31) // 32
+        rp = 32 * nb - len(seg)
+        reg = fold_window(INIT[rp] if k == 0 else 0, seg, 0, nb, k)
+        if L - cuts[k + 1]:
+            reg = mulmod(reg, x8n(L - cuts[k + 1]))
         total ^= reg
     desired = int.from_bytes(pkt[slot_off:slot_off + 4], "little")
     total ^= mulmod(desired ^ connect, x8n(L - slot_off))

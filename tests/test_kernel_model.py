@@ -21,7 +21,7 @@ def test_slicing_tables_and_image():
             for _ in range(t):
                 reg = (reg >> 8) ^ km.T0[reg & 0xFF]
             assert km.TS[t][j] == reg
-    assert km.IMG[5 * 64 + 2 * 9 + 1] == km.TS[9][5]
+    assert km.IMG[5 * 32 + 9] == km.TS[9][5]
 
 
 def test_lds_bank_conflict_free():
@@ -45,8 +45,7 @@ def test_each_lane_reads_every_byte_once():
         addrs = km.lookup_addresses(lane, words)
         used = set()
         for a in addrs:
-            row, col = a // 256, (a % 256) // 4
-            t = col // 2
+            row, t = a // 128, (a % 128) // 4
             m = t ^ 31
             assert block[m] == row      # looked-up row is byte m of the block
             used.add(m)
@@ -89,7 +88,18 @@ def test_packet_model_matches_oracle(lanes):
     rng = random.Random(10 + lanes)
     for L in [0, 1, 3, 4, 15, 16, 17, 31, 32, 33, 63, 64, 65, 100, 257, 1200, 1201]:
         pkt = bytes(rng.getrandbits(8) for _ in range(L))
-        assert km.crc_packet(pkt, lanes) == oracle.enet_crc32_py([pkt]), (L, lanes)
+        for addr in (0, 16, 1200 * 7, 4093):
+            assert km.crc_packet(pkt, lanes, addr=addr) == oracle.enet_crc32_py([pkt]), (L, lanes, addr)
+
+
+def test_segment_cuts_are_line_aligned():
+    for addr in range(0, 4096, 48):
+        for L in (1200, 1392, 300, 4096):
+            for lanes in (2, 4, 8):
+                cuts = km.segment_cuts(addr, L, lanes)
+                assert cuts == sorted(cuts) and cuts[0] == 0 and cuts[-1] == L
+                for c in cuts[1:-1]:
+                    assert c in (0, L) or (addr + c) % 128 == 0
 
 
 def test_verify_model(golden):
