@@ -4,16 +4,20 @@
 //
 // Slicing-by-32 in LDS, conflict-free.  A 32-byte block b_0..b_31 is folded
 // into the Sarwate register by   reg' = XOR_m T_{31-m}[b_m ^ reg_m]   (reg_m = byte
-// m of reg for m < 4, else 0), T_t[j] = byte j followed by t zero bytes.  The 32
-// tables sit side by side: row j (128 B) holds T_0[j] .. T_31[j] in dword columns
-// 0..31, i.e. in LDS banks 0..31 (ds_read_b32 bank = (addr/4) mod 32, lanes 0-31
-// and 32-63 served as separate groups).  At lookup step i a lane l handles byte
-// m = i ^ (l & 31) -- an XOR Latin square -- so in every ds_read_b32 the 32 lanes
-// of a half-wave read 32 different tables = 32 different banks: no conflicts
-// whatever the data (tests/test_kernel_model.py proves it; measured 2.5-2.9 LDS
-// cycles per wave-instruction on MI355X vs ~6 for random rows).  The per-lane
-// byte order costs one dword permutation per block (two bitop3 rounds + a half
-// swap) and one v_perm_b32 + one shift per lookup to form the LDS address.
+// m of reg for m < 4, else 0), T_t[j] = byte j followed by t zero bytes (the
+// stream kernel uses T'_t = T_{t+32(P-1)}, see crc32_kernels.hip).  Row j of the
+// 64 KiB LDS image is 256 bytes; table t sits in dword column 2t + (t >> 4), so
+// the LDS address of a lookup is  j*256 + 8t + 4(t>>4)  -- byte 1 = the data byte,
+// byte 0 = a per-lane constant: ONE v_perm_b32 forms it (no shift, no add).  At
+// lookup step i lane l handles byte m = i ^ (l & 31) -- an XOR Latin square -- so
+// in every ds_read_b32 the 32 lanes of a half-wave read 32 different tables, whose
+// columns 2t + (t>>4) are 32 different banks (ds_read_b32 bank = (addr/4) mod 32,
+// lanes 0-31 and 32-63 served as separate groups): no conflicts whatever the
+// data (tests/test_kernel_model.py proves it).  The 32 dwords per row no table
+// uses (columns 2c+1 for c < 16, 2c for c >= 16) hold byte-indexed tables:
+// INIT[], CINV[] and the stream kernel's butterfly constants.  The
+// per-lane byte order costs one dword permutation per block (two bitop3 rounds +
+// a half swap).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -22,7 +26,20 @@
 
 namespace enethip {
 
-constexpr int kLdsTableBytes = 256 * 32 * 4;       // 256 rows x 32 tables = 32 KiB
+constexpr int kLdsTableBytes = 256 * 256;         // 256 rows x 256 B = 64 KiB
+constexpr int kImageDwords = kLdsTableBytes / 4;
+constexpr int kCinvEntries = 512;
+
+// Byte offset of slicing table t in a row, and of free column c (the 32 dwords
+// per row no slicing table uses).  A free column is a 256-entry table indexed by
+// the row, i.e. by a byte value: one v_perm + ds_read per lookup.
+__host__ __device__ constexpr uint32_t col_byte(uint32_t t) { return 8u * t + 4u * (t >> 4); }
+__host__ __device__ constexpr uint32_t free_col(uint32_t c) { return 4u * (c < 16u ? 2u * c + 1u : 2u * c); }
+constexpr uint32_t kLevelCol = 0;   // columns 4l + b: butterfly level l (x^(-256 * 2^l)), register byte b
+constexpr uint32_t kInitCol = 16;   // INIT[r], rows 0..31
+constexpr uint32_t kCinvCol = 17;   // CINV[n] = x^(-8n), n < 512: row n & 255 of column 17 + (n >> 8)
+__host__ __device__ constexpr uint32_t init_addr(uint32_t r) { return 256u * r + free_col(kInitCol); }
+__host__ __device__ constexpr uint32_t cinv_addr(uint32_t n) { return 256u * (n & 255u) + free_col(kCinvCol + (n >> 8)); }
 constexpr int kXnEntries = 65536;                  // x^(8n) for n < 65536 (+ high part)
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -34,7 +51,7 @@ typedef __attribute__((address_space(3))) const uint32_t lds_u32;
 typedef __attribute__((address_space(3))) const u32x4 lds_u32x4;
 
 struct KernelTables {
-    const uint32_t* image;  // kLdsTableBytes, copied into LDS by every workgroup
+    const uint32_t* image;  // kLdsTableBytes per image (P = 1, 4, 8, 16), copied into LDS
     const uint32_t* xn_lo;  // x^(8n) mod P, n < 65536
     const uint32_t* xn_hi;  // x^(8*65536*q) mod P, q < 65536
     const uint32_t* init;   // INIT[r], r < 32
@@ -76,7 +93,7 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 
 // Per-lane constants of the conflict-free slicing-by-32 schedule.
 struct LaneSched {
-    uint32_t col[8];  // byte h of col[g]: 8 * table index for step i = 4g + h
+    uint32_t col[8];  // byte h of col[g]: column byte of the table for step i = 4g + h
     uint32_t sel[4];  // v_perm selector for steps with i & 3 == h
     uint32_t m1, m2;  // all-ones when this lane swaps dwords q <-> q^1 / q <-> q^2
     uint32_t hs;      // all-ones when this lane takes the block's two 16-byte halves swapped
@@ -92,7 +109,7 @@ __device__ __forceinline__ LaneSched make_sched(uint32_t lane) {
         for (int h = 0; h < 4; ++h) {
             const uint32_t i = 4u * g + h;
             const uint32_t t = (i ^ l5) ^ 31u;        // table of byte m = i ^ l5
-            r |= (8u * t) << (8 * h);
+            r |= col_byte(t) << (8 * h);
         }
         s.col[g] = r;
     }
@@ -123,8 +140,8 @@ __device__ __forceinline__ uint32_t fold_block_lane(uint32_t reg, u32x4 A, u32x4
     uint32_t v[32];
 #pragma unroll
     for (int i = 0; i < 32; ++i) {
-        // v_perm: byte0 = 8t, byte1 = data byte j  ->  (j*256 + 8t) >> 1 = j*128 + 4t
-        const uint32_t addr = __builtin_amdgcn_perm(d[i >> 2], s.col[i >> 2], s.sel[i & 3]) >> 1;
+        // v_perm: byte0 = column byte of table t, byte1 = data byte j -> j*256 + col
+        const uint32_t addr = __builtin_amdgcn_perm(d[i >> 2], s.col[i >> 2], s.sel[i & 3]);
         v[i] = *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr));
     }
     uint32_t acc = xor3(v[0], v[1], v[2]);

@@ -6,23 +6,15 @@
 // kernels compute the same Sarwate register (packet.cs:153) by a different but
 // algebraically identical route.
 //
-// Work decomposition (one launch, persistent grid):
-//   * a TASK is one lane x one packet segment: packet p is split over P = 2^lg
-//     consecutive lanes (lanes_per_packet); each lane runs its share of the
-//     packet's 32-byte blocks, then the P partial registers are combined with
-//     the GF(2) carry-combine  reg(A||B) = reg(A) (*) x^(8|B|)  ^  reg(B)
-//     and an XOR across the P lanes (__shfl_xor).
-//   * a packet of L bytes is processed as an END-aligned window of nb = ceil(L/32)
-//     blocks; the r' = 32*nb - L bytes in front of the packet are treated as zero
-//     and the register starts at INIT[r'] (the state that r' zero bytes carry to
-//     0xFFFFFFFF, packet.cs:144), so no per-packet tail loop is needed.
-//   * each 32-byte block is folded with slicing-by-32: 32 independent table
-//     lookups T_{31-m}[byte_m ^ state_m] XORed together.  The 32 tables live in
-//     LDS (64 KiB) in a layout where, for every lookup instruction, the 32 lanes
-//     of a half-wave hit 32 different banks (conflict-free; DESIGN.md "LDS table
-//     layout"): lane l handles byte m = i ^ (l & 15) at step i, table t = m ^ 31
-//     sits in bank column 2t + ((l >> 4) & 1) of a 256-byte row indexed by the
-//     byte value, and one v_perm_b32 builds the LDS address from the data byte.
+// Kernels:
+//   * crc32_stream_kernel -- the hot path: persistent, LDS-DMA streamed, strided
+//     lane->block assignment (4/8/16 lanes per packet), any alignment.
+//   * crc32_direct_kernel -- general fallback (any lanes per packet): blocks
+//     loaded into VGPRs, contiguous segments joined by the carry-combine.
+//   * crc32_gather_kernel -- one lane per DGRAM over an ENetBuffer gather list.
+// All fold 32-byte blocks with slicing-by-32 from a conflict-free 64 KiB LDS
+// image (crc32_device.hpp); every identity used is modelled and checked against
+// the oracle on CPU in tests/kernel_model.py.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -40,23 +32,6 @@
 namespace enethip {
 
 constexpr int kThreads = 512;                     // direct / gather kernels: 8 waves
-
-// Staged-kernel geometry: W waves per workgroup (one workgroup per CU), SB
-// 32-byte blocks per lane per stage, NB stage buffers per wave (NB-1 stages in
-// flight while one is folded).  LDS = 32 KiB tables + W * NB * SB * 2 KiB.
-template <int W, int SB, int NB>
-struct StagedGeom {
-    static constexpr int kWaves = W, kSB = SB, kNB = NB;
-    static constexpr int kThreads = 64 * W;
-    static constexpr uint32_t kRun = 32u * SB;                 // bytes per lane per stage
-    static constexpr uint32_t kStage = 64u * kRun;             // bytes per wave per stage
-    static constexpr uint32_t kSlice = kStage * NB;            // LDS per wave
-    static constexpr int kLds = kLdsTableBytes + W * static_cast<int>(kSlice);
-    static constexpr int kDma = static_cast<int>(kStage / 1024u);       // DMA instructions per stage
-    static constexpr uint32_t kPieces = kRun / 16u;                     // 16-byte pieces per run
-    static constexpr uint32_t kRunsPerDma = 1024u / kRun;
-    static_assert(kLds <= 160 * 1024, "LDS budget");
-};
 
 template <int NT>
 __device__ __forceinline__ void fill_table(uint8_t* lds, const uint32_t* image) {
@@ -80,13 +55,521 @@ struct PacketArgs {
     uint8_t* ok;
 };
 
-// One lane's share of one packet: packet pk = [a, a+L) is cut into P = 2^lg
-// segments at 128-byte-aligned ABSOLUTE addresses (nearest to the even split),
-// so no cache line is shared by two lanes' segments (shared lines were fetched
-// twice, microseconds apart: 1.57x HBM over-fetch measured).  Lane k folds its
-// segment [sp, sp+len) as an END-aligned window of nb 32-byte blocks with rp
-// zero bytes in front; its partial register is later advanced by `after` bytes.
+__device__ __forceinline__ uint32_t lds_load(uint32_t addr) { return *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr)); }
+__device__ __forceinline__ u32x4 lds_load16(uint32_t addr) { return *reinterpret_cast<lds_u32x4*>(static_cast<uintptr_t>(addr)); }
+
+// ============================================================ stream kernel
+//
+// One persistent workgroup of W waves per CU.  A wave owns groups g = wv,
+// wv + W*grid, ...; a group is 64 consecutive tasks = 64/P packets, P = 2^lg
+// (4, 8 or 16) lanes per packet.  Per packet (crc32 of bytes [a, a+L)):
+//   * window: NB whole 32-byte blocks ending at the packet end when that is
+//     16-byte aligned (lz = 32*NB - L zero bytes in front, tz = 0), else starting
+//     at the 16-byte granule holding a (lz = a & 15, tz = 32*NB - lz - L zero
+//     bytes behind).  Head and tail bytes are zeroed after loading; a 16-byte
+//     piece wholly outside the packet is never read (memory-safe at page ends);
+//   * lane k folds the window blocks w with (w + r) % P == k, r = (-NB) % P,
+//     using the ADVANCING tables T'_t = T_{t+32(P-1)} of this P: each fold also
+//     skips the P-1 blocks the other lanes own, so the P lanes of a packet walk
+//     it front to back together and one stage of a packet is ONE contiguous
+//     P*SB*32-byte chunk.  The rotation r makes lane k end exactly 32k bytes
+//     past the window end; the block-0 lane (k == r) starts at INIT[lz];
+//   * finish: a log2(P)-level butterfly, lane k ^= adv_{-32m}(lane k+m), each
+//     constant advance = 4 byte-indexed LDS lookups (free image columns); then
+//     x^(-8 tz) for START-aligned windows.
+// No x^(8n) gathers and no alignment precondition.  Verify mode substitutes the
+// slot bytes by connectID inside the block that holds them (protocol.cs:1052-1068)
+// and collects the original bytes as `desired`.  tests/kernel_model.py restates
+// all of it and checks it against the oracle.
+//
+// Memory: everything a wave reads from HBM arrives by LDS-DMA
+// (global_load_lds): its share of the table image, the per-group packet
+// metadata and the packet bytes.  A wave streams its groups through a ring of
+// NB stage buffers (a stage = SB blocks of every lane) with NB-1 stages in flight
+// while one is folded, ACROSS group boundaries: the next group's metadata is
+// fetched one group ahead and its first stages are issued while the current
+// group is still being folded.  The wave's own counted s_waitcnt vmcnt(N) orders
+// DMA and ds_read (N = VMEM operations issued after the awaited one; stores are
+// not counted, which only over-waits).  The loop is unrolled NB times so every
+// ring address is an immediate.
+template <int W, int SB, int NB>
+struct StreamGeom {
+    static constexpr int kWaves = W, kSB = SB, kNB = NB;
+    static constexpr int kThreads = 64 * W;
+    static constexpr uint32_t kRun = 32u * SB;               // bytes per lane per stage
+    static constexpr uint32_t kStage = 64u * kRun;           // bytes per wave per stage
+    static constexpr int kDma = static_cast<int>(kStage / 1024u);
+    static constexpr uint32_t kPieces = kRun / 16u;          // 16-byte pieces per run
+    static constexpr uint32_t kRunsPerDma = 1024u / kRun;
+    static constexpr uint32_t kLsb = SB == 1 ? 0u : SB == 2 ? 1u : 2u;
+    static constexpr uint32_t kMetaAhead = 2;                // metadata fetched this many groups ahead
+    static constexpr uint32_t kMetaSlots = NB + kMetaAhead;
+    static constexpr uint32_t kMetaSlot = 512u;
+    static constexpr uint32_t kWaveLds = NB * kStage + kMetaSlots * kMetaSlot;
+    static constexpr int kLds = kLdsTableBytes + W * static_cast<int>(kWaveLds);
+    static constexpr int kTableRounds = (kImageDwords / 4 + 64 * W - 1) / (64 * W);
+    static_assert(kLds <= 160 * 1024, "LDS budget");
+    static_assert(NB >= 2 && NB <= 4 && (SB == 1 || SB == 2 || SB == 4), "geometry");
+};
+
+// s_waitcnt vmcnt(min(n, 63)): the immediate picked by a balanced scalar
+// branch tree (n is wave-uniform).
+template <int Lo, int Hi>
+__device__ __forceinline__ void wait_vm_tree(uint32_t n) {
+    if constexpr (Lo == Hi) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Lo) : "memory");
+    } else {
+        constexpr int Mid = (Lo + Hi) / 2;
+        if (n <= static_cast<uint32_t>(Mid)) wait_vm_tree<Lo, Mid>(n);
+        else wait_vm_tree<Mid + 1, Hi>(n);
+    }
+}
+__device__ __forceinline__ void wait_vm(uint32_t n) { wait_vm_tree<0, 63>(__builtin_amdgcn_readfirstlane(n)); }
+
+__device__ __forceinline__ void dma16(const void* g, uint32_t lds_addr) {
+    __builtin_amdgcn_global_load_lds(g, reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                            static_cast<uintptr_t>(lds_addr)), 16, 0, 0);
+}
+__device__ __forceinline__ void dma4(const void* g, uint32_t lds_addr) {
+    __builtin_amdgcn_global_load_lds(g, reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                            static_cast<uintptr_t>(lds_addr)), 4, 0, 0);
+}
+
+// XOR-butterfly partner within 32 lanes (ds_swizzle bitmask mode, no LDS access).
+template <int M>
+__device__ __forceinline__ uint32_t swz_xor(uint32_t v) {
+    return static_cast<uint32_t>(__builtin_amdgcn_ds_swizzle(static_cast<int>(v), 0x1F | (M << 10)));
+}
+
+// Lane c's run sits at buf + kRun*c, its 16-byte piece p in slot p ^ swz(c):
+// swz(c) = ((c >> log2(16/R)) & (R-1)) ^ ((c >> 4) & 1), R = pieces per run,
+// keeps every 16-lane ds_read_b128 group on 16 distinct slots (the (c >> 4) term
+// undoes the lane's half swap).
+template <class G>
+__device__ __forceinline__ uint32_t run_swz(uint32_t c) {
+    constexpr uint32_t R = G::kPieces;
+    constexpr uint32_t sh = R == 2 ? 3u : R == 4 ? 2u : R == 8 ? 1u : 0u;
+    return ((c >> sh) & (R - 1u)) ^ ((c >> 4) & 1u);
+}
+
+// Metadata of one group into a meta slot: field f of packet j lands at
+// slot + 4*(f*Gp + j); f = 0 len, 1/2 offset lo/hi, 3 slot offset, 4 connectID.
+template <int MODE>
+__device__ __forceinline__ void issue_meta(const PacketArgs& pa, uint64_t pk0, uint32_t lg, uint32_t nmeta,
+                                           uint32_t slot, uint32_t lane) {
+    const uint32_t gsh = 6u - lg;                     // log2(packets per group)
+    for (uint32_t r = 0; r < nmeta; ++r) {
+        const uint32_t idx = 64u * r + lane;
+        const uint32_t f = idx >> gsh;
+        const uint64_t pk = min(pk0 + (idx & ((1u << gsh) - 1u)), pa.n - 1);
+        const uint32_t* src = pa.len + pk;
+        if (f == 1u || f == 2u) src = reinterpret_cast<const uint32_t*>(pa.off) + 2u * pk + (f - 1u);
+        if (MODE && f == 3u) src = pa.slot_off + pk;
+        if (MODE && f == 4u) src = pa.connect + pk;
+        dma4(src, slot + 256u * r);
+    }
+}
+
+__device__ __forceinline__ uint32_t meta_field(uint32_t slot, uint32_t lg, uint32_t f, uint32_t j) {
+    return lds_load(slot + 4u * ((f << (6u - lg)) + j));
+}
+
+// One packet's window, seen from any lane.
+struct Window {
+    uint64_t ws;        // first window byte (16-byte aligned)
+    uint32_t L, lz, nb, tz, r;
+    bool active;
+};
+
+__device__ __forceinline__ Window packet_window(const PacketArgs& pa, uint32_t slot, uint32_t lg, uint64_t pk0,
+                                                uint32_t j) {
+    Window w;
+    w.active = pk0 + j < pa.n;
+    w.L = w.active ? meta_field(slot, lg, 0, j) : 0u;
+    const uint64_t off = static_cast<uint64_t>(meta_field(slot, lg, 1, j)) |
+                         (static_cast<uint64_t>(meta_field(slot, lg, 2, j)) << 32);
+    const uint64_t a = reinterpret_cast<uint64_t>(pa.bytes) + off, e = a + w.L;
+    if (w.L == 0) {
+        w.lz = w.nb = w.tz = 0;
+        w.ws = a;
+    } else if ((e & 15u) == 0) {                      // END-aligned
+        w.nb = (w.L + 31u) >> 5;
+        w.lz = 32u * w.nb - w.L;
+        w.tz = 0;
+        w.ws = e - 32ull * w.nb;
+    } else {                                          // START-aligned
+        w.lz = static_cast<uint32_t>(a & 15u);
+        w.nb = (w.lz + w.L + 31u) >> 5;
+        w.tz = 32u * w.nb - w.lz - w.L;
+        w.ws = a - w.lz;
+    }
+    w.r = (0u - w.nb) & ((1u << lg) - 1u);
+    return w;
+}
+
+// Producer side of a group: per DMA slot i, the address of this lane's 16-byte
+// piece at the group's next stage, the address used once the piece runs past its
+// last in-range block, how many stages stay in range, and the stage-0 bump that
+// skips a head piece lying wholly in front of the packet.
+template <class G>
+struct Producer {
+    uint64_t cur[G::kDma], lim[G::kDma];
+    uint32_t nval[G::kDma], hfix[G::kDma];
+    uint32_t stages;
+};
+
+template <class G>
+__device__ __forceinline__ void producer_setup(Producer<G>& pr, const PacketArgs& pa, uint32_t slot, uint32_t lg,
+                                               uint64_t pk0, uint32_t lane, const uint8_t* safe) {
+    const uint32_t P = 1u << lg;
+    uint32_t most = 0;
+#pragma unroll
+    for (int i = 0; i < G::kDma; ++i) {
+        const uint32_t c = G::kRunsPerDma * i + lane / G::kPieces;    // run (task lane) of this piece
+        const uint32_t p = (lane % G::kPieces) ^ run_swz<G>(c);        // piece index in the run
+        const uint32_t b = p >> 1, h = p & 1u;
+        const Window w = packet_window(pa, slot, lg, pk0, c >> lg);
+        const uint32_t w0 = ((c - w.r) & (P - 1u)) + P * b;            // block of this piece at stage 0
+        // last block whose h-half holds packet bytes
+        const int32_t lastw = static_cast<int32_t>(w.nb) - ((h && w.tz >= 16u) ? 2 : 1);
+        const bool any = static_cast<int32_t>(w0) <= lastw;
+        pr.nval[i] = any ? ((static_cast<uint32_t>(lastw) - w0) >> (lg + G::kLsb)) + 1u : 0u;
+        pr.hfix[i] = (w0 == 0 && h == 0 && w.lz >= 16u) ? 16u : 0u;
+        pr.cur[i] = w.ws + 32ull * w0 + 16u * h + pr.hfix[i];
+        // in-range piece of the last block: its h-half unless that half is all tail
+        // (or, for a one-block window, all head)
+        uint32_t hl = (h && w.tz < 16u) ? 1u : 0u;
+        if (w.nb == 1 && w.lz >= 16u) hl = 1u;
+        pr.lim[i] = w.nb ? w.ws + 32ull * (w.nb - 1u) + 16u * hl : reinterpret_cast<uint64_t>(safe);
+        most = max(most, pr.nval[i]);
+    }
+    pr.stages = __builtin_amdgcn_readfirstlane(wave_max(most));
+}
+
+// Consumer side: this lane's task of the group.
 struct Task {
+    uint64_t pk;
+    uint32_t k, w0, nb, lz, tz, cnt, reg;
+    uint32_t e0, e1, e2, e3;   // block ordinals needing head/tail/slot fix-ups (~0u = none)
+    bool active;
+    int32_t ps;                // verify: window position of the slot
+    uint32_t connect;
+    bool slot_ok;
+};
+
+template <int MODE>
+__device__ __forceinline__ Task consumer_setup(const PacketArgs& pa, uint32_t slot, uint32_t lg, uint64_t pk0,
+                                               uint32_t lane) {
+    const uint32_t P = 1u << lg;
+    Task t;
+    const uint32_t j = lane >> lg;
+    const Window w = packet_window(pa, slot, lg, pk0, j);
+    t.pk = pk0 + j;
+    t.active = w.active;
+    t.k = lane & (P - 1u);
+    t.w0 = (t.k - w.r) & (P - 1u);
+    t.nb = w.nb;
+    t.lz = w.lz;
+    t.tz = w.tz;
+    t.cnt = t.w0 < w.nb ? ((w.nb - 1u - t.w0) >> lg) + 1u : 0u;
+    t.reg = t.k == w.r ? lds_load(init_addr(w.lz)) : 0u;
+    t.e0 = (w.lz && t.w0 == 0 && w.nb) ? 0u : ~0u;
+    t.e1 = (w.tz && t.cnt && t.w0 + P * (t.cnt - 1u) == w.nb - 1u) ? t.cnt - 1u : ~0u;
+    t.e2 = t.e3 = ~0u;
+    t.ps = -4096;
+    t.connect = 0;
+    t.slot_ok = false;
+    if (MODE) {
+        const uint32_t so = meta_field(slot, lg, 3, j);
+        t.connect = meta_field(slot, lg, 4, j);
+        t.slot_ok = w.L >= 4u && so <= w.L - 4u;
+        if (t.slot_ok) {
+            t.ps = static_cast<int32_t>(w.lz + so);
+            const uint32_t ws_ = static_cast<uint32_t>(t.ps) >> 5, we_ = static_cast<uint32_t>(t.ps + 3) >> 5;
+            if (((ws_ + w.r) & (P - 1u)) == t.k) t.e2 = ws_ >> lg;
+            if (we_ != ws_ && ((we_ + w.r) & (P - 1u)) == t.k) t.e3 = we_ >> lg;
+        }
+    }
+    return t;
+}
+
+// First stage >= from holding a fix-up block of any lane (wave-uniform; ~0u = none).
+template <class G>
+__device__ __forceinline__ uint32_t next_edge_stage(const Task& t, uint32_t from) {
+    uint32_t m = ~0u;
+    const uint32_t e[4] = {t.e0, t.e1, t.e2, t.e3};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t st = e[i] == ~0u ? ~0u : e[i] >> G::kLsb;
+        if (st >= from) m = min(m, st);
+    }
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) m = min(m, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), s)));
+    return __builtin_amdgcn_readfirstlane(m);
+}
+
+// Keep bytes [lo, hi) of dword q (bytes 4q .. 4q+3 of the block).
+__device__ __forceinline__ uint32_t keep_mask(int lo, int hi, int q) {
+    const int a = lo - 4 * q, b = hi - 4 * q;
+    const uint32_t ma = a <= 0 ? 0xFFFFFFFFu : a >= 4 ? 0u : (0xFFFFFFFFu << (8 * a));
+    const uint32_t mb = b >= 4 ? 0xFFFFFFFFu : b <= 0 ? 0u : (0xFFFFFFFFu >> (32 - 8 * b));
+    return ma & mb;
+}
+
+// Head/tail zeroing and (verify) slot substitution of block w, words in LANE
+// order (A, B swapped when hs).
+template <int MODE>
+__device__ __forceinline__ void edge_fix(u32x4& A, u32x4& B, uint32_t hs, const Task& t, uint32_t w,
+                                         uint32_t& desired) {
+    uint32_t v[8];
+    const bool sw = hs != 0;
+    const u32x4 h0 = sw ? B : A, h1 = sw ? A : B;
+    v[0] = h0.x; v[1] = h0.y; v[2] = h0.z; v[3] = h0.w;
+    v[4] = h1.x; v[5] = h1.y; v[6] = h1.z; v[7] = h1.w;
+    const int lo = (w == 0) ? static_cast<int>(t.lz) : 0;
+    const int hi = (w + 1 == t.nb) ? 32 - static_cast<int>(t.tz) : 32;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] &= keep_mask(lo, hi, q);
+    if (MODE) {
+        const int rel = t.ps - 32 * static_cast<int>(w);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int d = rel - 4 * q;
+            if (d > -4 && d < 4) {
+                uint32_t M, C;
+                if (d >= 0) {
+                    M = 0xFFFFFFFFu << (8 * d);
+                    C = t.connect << (8 * d);
+                    desired |= v[q] >> (8 * d);
+                } else {
+                    M = 0xFFFFFFFFu >> (-8 * d);
+                    C = t.connect >> (-8 * d);
+                    desired |= (v[q] & M) << (-8 * d);
+                }
+                v[q] = (v[q] & ~M) | (C & M);
+            }
+        }
+    }
+    const u32x4 n0 = {v[0], v[1], v[2], v[3]}, n1 = {v[4], v[5], v[6], v[7]};
+    A = sw ? n1 : n0;
+    B = sw ? n0 : n1;
+}
+
+// adv by -32*2^lvl bytes: four byte-indexed lookups in free image columns.
+template <int LVL>
+__device__ __forceinline__ uint32_t level_apply(uint32_t v) {
+    uint32_t x[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const uint32_t addr = __builtin_amdgcn_perm(v, free_col(kLevelCol + 4 * LVL + b),
+                                                    0x0C0C0000u | ((4u + b) << 8));
+        x[b] = lds_load(addr);
+    }
+    return xor3(x[0], x[1], x[2]) ^ x[3];
+}
+
+template <int LVL>
+__device__ __forceinline__ void butterfly(uint32_t lg, uint32_t& reg, uint32_t& desired, bool verify) {
+    if constexpr (LVL < 4) {
+        if (LVL < static_cast<int>(lg)) {
+            reg ^= level_apply<LVL>(swz_xor<(1 << LVL)>(reg));
+            if (verify) desired |= swz_xor<(1 << LVL)>(desired);
+            butterfly<LVL + 1>(lg, reg, desired, verify);
+        }
+    }
+}
+
+template <int N, class F>
+__device__ __forceinline__ void unroll_slots(F&& f) {
+    if constexpr (N > 0) {
+        unroll_slots<N - 1>(f);
+        f(std::integral_constant<uint32_t, N - 1>{});
+    }
+}
+
+// ABL (diagnostics only): 0 = real, 1 = no table lookups, 2 = no packet DMA.
+template <int MODE, class G, int ABL = 0>
+__global__ void __launch_bounds__(G::kThreads) crc32_stream_kernel(PacketArgs pa, KernelTables tb) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lg = pa.lg, P = 1u << lg;
+    const uint32_t gsh = 6u - lg;                                       // log2(packets per group)
+    constexpr uint32_t F = MODE ? 5u : 3u;
+    const uint32_t nmeta = (F << gsh) > 64u ? 2u : 1u;                  // F * 64/P <= 80 dwords
+    const uint64_t ngroups = (pa.n + (1u << gsh) - 1u) >> gsh;
+    const uint64_t wv = static_cast<uint64_t>(blockIdx.x) * G::kWaves + wave;
+    const uint64_t wt = static_cast<uint64_t>(gridDim.x) * G::kWaves;
+    const uint32_t J = wv < ngroups ? static_cast<uint32_t>((ngroups - 1u - wv) / wt) + 1u : 0u;
+    const uint32_t ring = kLdsTableBytes + wave * G::kWaveLds;
+    const uint32_t meta = ring + G::kNB * G::kStage;
+    const uint8_t* safe = reinterpret_cast<const uint8_t*>(tb.xn_lo);
+    const uint64_t stepB = 32ull * P * G::kSB;                          // bytes per stage per piece
+    auto group_pk0 = [&](uint32_t j) __attribute__((always_inline)) -> uint64_t { return (wv + static_cast<uint64_t>(j) * wt) << gsh; };
+    auto meta_slot = [&](uint32_t j) __attribute__((always_inline)) -> uint32_t { return meta + (j % G::kMetaSlots) * G::kMetaSlot; };
+
+    uint32_t ops = 0;                    // counted VMEM operations issued by this wave
+    // 1. metadata of the first group, then this wave's share of the table image
+    if (J) {
+        issue_meta<MODE>(pa, group_pk0(0), lg, nmeta, meta_slot(0), lane);
+        ops += nmeta;
+    }
+    const uint32_t m_first = ops;
+    {
+        const uint32_t img = lg == 2 ? 1u : lg == 3 ? 2u : 3u;
+        const uint32_t* src = tb.image + static_cast<size_t>(img) * kImageDwords;
+#pragma unroll
+        for (int r = 0; r < G::kTableRounds; ++r) {
+            const uint32_t piece0 = min((static_cast<uint32_t>(r) * G::kWaves + wave) * 64u,
+                                        static_cast<uint32_t>(kImageDwords / 4 - 64));
+            dma16(src + 4u * (piece0 + lane), 16u * piece0);
+        }
+        ops += G::kTableRounds;
+    }
+    const uint32_t m_table = ops;
+
+    // producer state
+    Producer<G> pr;
+    uint32_t pj = 0, pst = 0;
+    bool pdone = J == 0;
+    // metadata marks of the groups after pj (ops count mod 2^16 after each issue)
+    uint64_t mmarks = 0;
+    uint32_t nmm = 0;
+    auto fetch_meta = [&](uint32_t j) __attribute__((always_inline)) {
+        if (j < J) {
+            issue_meta<MODE>(pa, group_pk0(j), lg, nmeta, meta_slot(j), lane);
+            ops += nmeta;
+        }
+        mmarks |= static_cast<uint64_t>(ops & 0xFFFFu) << (16u * nmm);
+        ++nmm;
+    };
+    // marks: ops count (mod 2^16) right after each in-flight stage, oldest in the
+    // low 16 bits -- one scalar, no indexed array
+    uint64_t marks = 0;
+    uint32_t nfl = 0;
+
+    auto produce = [&](uint32_t slotc) __attribute__((always_inline)) {
+        const uint32_t buf = ring + slotc * G::kStage;
+#pragma unroll
+        for (int i = 0; i < G::kDma; ++i) {
+            const uint64_t g = pst < pr.nval[i] ? pr.cur[i] : pr.lim[i];
+            if (ABL != 2) dma16(reinterpret_cast<const void*>(g), buf + 1024u * i);
+            pr.cur[i] += stepB;
+        }
+        if (pst == 0) {
+#pragma unroll
+            for (int i = 0; i < G::kDma; ++i) pr.cur[i] -= pr.hfix[i];
+        }
+        if (ABL != 2) ops += G::kDma;
+        marks |= static_cast<uint64_t>(ops & 0xFFFFu) << (16u * nfl);
+        ++nfl;
+        if (++pst == pr.stages) {
+            pst = 0;
+            if (++pj < J) {
+                wait_vm((ops - static_cast<uint32_t>(mmarks)) & 0xFFFFu);   // metadata of group pj
+                mmarks >>= 16;
+                --nmm;
+                producer_setup<G>(pr, pa, meta_slot(pj), lg, group_pk0(pj), lane, safe);
+                fetch_meta(pj + G::kMetaAhead);
+            } else {
+                pdone = true;
+            }
+        }
+    };
+
+    if (J) {
+        wait_vm(ops - m_first);
+        producer_setup<G>(pr, pa, meta_slot(0), lg, group_pk0(0), lane, safe);
+#pragma unroll
+        for (uint32_t d = 1; d <= G::kMetaAhead; ++d) fetch_meta(d);
+        unroll_slots<G::kNB - 1>([&](auto sc) __attribute__((always_inline)) {
+            if (!pdone) produce(decltype(sc)::value);
+        });
+    }
+    // 2. the table must be complete (all waves' shares) before any lookup
+    wait_vm(ops - m_table);
+    __builtin_amdgcn_s_barrier();
+    if (!J) return;
+
+    const LaneSched s = make_sched(lane);
+    const uint32_t swz = run_swz<G>(lane);
+    const uint32_t hsb = s.hs & 1u;
+    // LDS address of this lane's half-blocks in ring slot 0 (others: + slot*kStage)
+    uint32_t offA[G::kSB], offB[G::kSB];
+#pragma unroll
+    for (int b = 0; b < G::kSB; ++b) {
+        offA[b] = ring + G::kRun * lane + 16u * ((2u * b + hsb) ^ swz);
+        offB[b] = ring + G::kRun * lane + 16u * ((2u * b + (hsb ^ 1u)) ^ swz);
+    }
+
+    uint32_t cj = 0, cst = 0;
+    Task t = consumer_setup<MODE>(pa, meta_slot(0), lg, group_pk0(0), lane);
+    uint32_t cstages = __builtin_amdgcn_readfirstlane(wave_max((t.cnt + G::kSB - 1u) >> G::kLsb));
+    uint32_t nedge = next_edge_stage<G>(t, 0);
+    uint32_t reg = t.reg, desired = 0;
+    bool done = false;
+
+    auto stage = [&](auto sc) __attribute__((always_inline)) {
+        constexpr uint32_t S = decltype(sc)::value;
+        if (done) return;
+        if (!pdone) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          // WAR on the buffer being refilled
+            produce((S + G::kNB - 1) % G::kNB);
+        }
+        wait_vm((ops - static_cast<uint32_t>(marks)) & 0xFFFFu);        // this stage has landed
+        const bool edges = cst == nedge;
+#pragma unroll
+        for (int b = 0; b < G::kSB; ++b) {
+            const uint32_t jb = G::kSB * cst + b;                       // this lane's block ordinal
+            u32x4 A = lds_load16(offA[b] + S * G::kStage);
+            u32x4 B = lds_load16(offB[b] + S * G::kStage);
+            const bool valid = jb < t.cnt;
+            if (edges) {
+                const bool fix = valid && (jb == t.e0 || jb == t.e1 || (MODE && (jb == t.e2 || jb == t.e3)));
+                if (fix) edge_fix<MODE>(A, B, s.hs, t, t.w0 + P * jb, desired);
+            }
+            const uint32_t nr = ABL == 1 ? xor3(reg ^ A.x ^ A.y, A.z ^ A.w ^ B.x, B.y ^ B.z ^ B.w)
+                                         : fold_block_lane(reg, A, B, s);
+            reg = valid ? nr : reg;
+        }
+        if (edges) nedge = next_edge_stage<G>(t, cst + 1);
+        marks >>= 16;
+        --nfl;
+        if (++cst == cstages) {
+            // finish the group: butterfly over the P lanes, then the tail correction
+            butterfly<0>(lg, reg, desired, MODE != 0);
+            if (t.k == 0 && t.tz) reg = mulmod(reg, lds_load(cinv_addr(t.tz)));
+            if (t.active && t.k == 0) {
+                if (MODE == 0) {
+                    pa.out[t.pk] = finalize(reg);                        // packet.cs:159
+                } else {
+                    const uint32_t comp = t.slot_ok ? finalize(reg) : 0u;
+                    pa.ok[t.pk] = (t.slot_ok && comp == desired) ? 1 : 0;
+                    if (pa.out) pa.out[t.pk] = comp;
+                }
+            }
+            if (++cj == J) {
+                done = true;
+                return;
+            }
+            t = consumer_setup<MODE>(pa, meta_slot(cj), lg, group_pk0(cj), lane);
+            cstages = __builtin_amdgcn_readfirstlane(wave_max((t.cnt + G::kSB - 1u) >> G::kLsb));
+            nedge = next_edge_stage<G>(t, 0);
+            reg = t.reg;
+            desired = 0;
+            cst = 0;
+        }
+    };
+    while (!done) unroll_slots<G::kNB>(stage);
+}
+
+// ============================================================ direct kernel
+//
+// General direct-load path (every block loaded straight into VGPRs, any P):
+// packet split into P CONTIGUOUS segments cut at 128-byte-aligned absolute
+// addresses, each an END-aligned window started at INIT[rp], joined by the
+// carry-combine reg(A||B) = reg(A) x^(8|B|) ^ reg(B).  Runs for lanes-per-packet
+// values the stream kernel does not take, and as the comparison point.
+struct DTask {
     const uint8_t* a;   // packet start
     const uint8_t* sp;  // segment start
     uint64_t pk;
@@ -94,8 +577,8 @@ struct Task {
     bool active;
 };
 
-__device__ __forceinline__ Task make_task(const PacketArgs& pa, uint64_t t, uint64_t total) {
-    Task tk;
+__device__ __forceinline__ DTask make_dtask(const PacketArgs& pa, uint64_t t, uint64_t total) {
+    DTask tk;
     const uint32_t P = 1u << pa.lg;
     tk.active = t < total;
     tk.pk = t >> pa.lg;
@@ -122,10 +605,9 @@ __device__ __forceinline__ Task make_task(const PacketArgs& pa, uint64_t t, uint
     return tk;
 }
 
-// Carry-combine the P partial registers of each packet and write the result.
 template <int MODE>
-__device__ __forceinline__ void finish_task(const PacketArgs& pa, const Task& tk, uint32_t reg,
-                                            const KernelTables& tb) {
+__device__ __forceinline__ void finish_dtask(const PacketArgs& pa, const DTask& tk, uint32_t reg,
+                                             const KernelTables& tb) {
     if (tk.after) reg = mulmod(reg, x8n_dev(tk.after, tb));    // reg(A||B) = reg(A) x^(8|B|) ^ reg(B)
     for (uint32_t m = 1; m < (1u << pa.lg); m <<= 1) reg ^= __shfl_xor(reg, static_cast<int>(m));
     if (!tk.active || tk.k != 0) return;
@@ -151,139 +633,6 @@ __device__ __forceinline__ void finish_task(const PacketArgs& pa, const Task& tk
     }
 }
 
-__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
-    const uint32_t lo = __shfl(static_cast<uint32_t>(v), static_cast<int>(src));
-    const uint32_t hi = __shfl(static_cast<uint32_t>(v >> 32), static_cast<int>(src));
-    return (static_cast<uint64_t>(hi) << 32) | lo;
-}
-
-// Staged fold of this lane's segment window, all lanes of the wave cooperating
-// on the loads.  Precondition (checked by the caller for the whole wave): every
-// lane's window start Wp = sp + len - 32*nb is 16-byte aligned.
-//
-// A stage = SB blocks of every lane (64 * 32 * SB bytes), NB-buffered in the
-// wave's own LDS slice, NB-1 stages in flight while one is folded.  Lane c's run
-// sits at buf + kRun*c, its 16-byte piece p in slot p ^ swz(c) with
-// swz(c) = ((c >> log2(16/R)) & (R-1)) ^ ((c >> 4) & 1), R = pieces per run,
-// which keeps every 16-lane ds_read_b128 group of gfx950 on 16 distinct slots
-// (the (c >> 4) term undoes the lane's half swap).  A stage arrives by kDma
-// LDS-DMA instructions (global_load_lds_dwordx4), each fetching kRunsPerDma
-// whole runs with kPieces lanes per run.  Only the issuing wave reads its slice,
-// so its own s_waitcnt vmcnt orders DMA and ds_read (no barrier).
-template <class G>
-__device__ __forceinline__ uint32_t run_swz(uint32_t c) {
-    constexpr uint32_t R = G::kPieces;
-    constexpr uint32_t sh = R == 2 ? 3u : R == 4 ? 2u : R == 8 ? 1u : 0u;
-    return ((c >> sh) & (R - 1u)) ^ ((c >> 4) & 1u);
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt_stages(uint32_t n) {
-    // s_waitcnt needs an immediate: n stages of N DMA instructions may stay in flight
-    switch (n) {
-        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-        case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); break;
-        case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * N) : "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * N) : "memory"); break;
-    }
-}
-
-template <class G, int ABL>  // ABL (diagnostics only): 0 = real, 1 = no table lookups, 2 = no DMA
-__device__ __forceinline__ uint32_t fold_staged(uint32_t reg, const Task& tk, const LaneSched& s,
-                                                uint32_t slice, const uint8_t* safe) {
-    static_assert(G::kNB <= 4, "wait_vmcnt_stages covers up to 3 stages in flight");
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t cnt = tk.nb;
-    const bool head = cnt && tk.rp;
-    const uint64_t src0 = cnt ? reinterpret_cast<uint64_t>(tk.sp + tk.len) - 32ull * tk.nb
-                              : reinterpret_cast<uint64_t>(safe);
-    // last block | (block 0 half 0 lies wholly in front of the segment) << 31
-    const uint32_t meta = (cnt ? cnt - 1u : 0u) | ((head && tk.rp >= 16u) ? 0x80000000u : 0u);
-    uint64_t dsrc[G::kDma];
-    uint32_t dlast[G::kDma], dpiece[G::kDma];
-#pragma unroll
-    for (int i = 0; i < G::kDma; ++i) {
-        const uint32_t c = G::kRunsPerDma * i + lane / G::kPieces;
-        dsrc[i] = shfl64(src0, c);
-        dlast[i] = __shfl(meta, static_cast<int>(c));
-        dpiece[i] = (lane % G::kPieces) ^ run_swz<G>(c);
-    }
-    const uint32_t trips = wave_max(cnt);
-    const uint32_t stages = (trips + G::kSB - 1) / G::kSB;
-    const uint32_t swz = run_swz<G>(lane);
-    const uint32_t hsb = s.hs & 1u;
-
-    auto issue = [&](uint32_t st) {
-        const uint32_t buf = slice + (st % G::kNB) * G::kStage;
-#pragma unroll
-        for (int i = 0; i < G::kDma; ++i) {
-            const uint32_t last = dlast[i] & 0x7FFFFFFFu;
-            const uint32_t kk = min(G::kSB * st + (dpiece[i] >> 1), last);
-            uint64_t g = dsrc[i] + 32ull * kk + 16ull * (dpiece[i] & 1u);
-            if (kk == 0 && (dpiece[i] & 1u) == 0 && (dlast[i] >> 31)) g += 16;   // stay inside the buffer
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g),
-                                             reinterpret_cast<__attribute__((address_space(3))) void*>(
-                                                 static_cast<uintptr_t>(buf + 1024u * i)),
-                                             16, 0, 0);
-        }
-    };
-
-    if (ABL != 2)
-        for (uint32_t p = 0; p + 1 < G::kNB && p < stages; ++p) issue(p);
-    for (uint32_t st = 0; st < stages; ++st) {
-        if (st + G::kNB - 1 < stages) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // WAR on the buffer being refilled
-            if (ABL != 2) issue(st + G::kNB - 1);
-        }
-        const uint32_t ahead = min(stages - 1u, st + G::kNB - 1u) - st;   // stages issued after st
-        wait_vmcnt_stages<G::kDma>(ABL == 2 ? 0u : ahead);
-        const uint32_t base = slice + (st % G::kNB) * G::kStage + G::kRun * lane;
-#pragma unroll
-        for (int b = 0; b < G::kSB; ++b) {
-            const uint32_t blk = G::kSB * st + b;
-            if (blk >= trips) break;
-            u32x4 A = *reinterpret_cast<lds_u32x4*>(static_cast<uintptr_t>(base + 16u * ((2u * b + hsb) ^ swz)));
-            u32x4 B = *reinterpret_cast<lds_u32x4*>(static_cast<uintptr_t>(base + 16u * ((2u * b + (hsb ^ 1u)) ^ swz)));
-            if (head && blk == 0) {                                   // bytes in front of the segment are zero
-                const uint32_t z0 = min(tk.rp, 16u), z1 = tk.rp > 16u ? tk.rp - 16u : 0u;
-                A = zero_prefix(A, hsb ? z1 : z0);
-                B = zero_prefix(B, hsb ? z0 : z1);
-            }
-            const uint32_t nr = ABL == 1 ? xor3(reg ^ A.x ^ A.y, A.z ^ A.w ^ B.x, B.y ^ B.z ^ B.w)
-                                         : fold_block_lane(reg, A, B, s);
-            reg = blk < cnt ? nr : reg;
-        }
-    }
-    return reg;
-}
-
-// MODE 0: out[p] = enet_crc32(packet p).  MODE 1: receive verify.
-// Persistent: one workgroup of G::kWaves waves per CU; each wave takes 64
-// consecutive tasks at a time.
-template <int MODE, class G, int ABL = 0>
-__global__ void __launch_bounds__(G::kThreads) crc32_staged_kernel(PacketArgs pa, KernelTables tb) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    fill_table<G::kThreads>(lds, tb.image);
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const LaneSched s = make_sched(lane);
-    const uint32_t slice = kLdsTableBytes + wave * G::kSlice;
-    const uint64_t total = pa.n << pa.lg;
-    const uint64_t waves_total = static_cast<uint64_t>(gridDim.x) * G::kWaves;
-    const uint8_t* safe = reinterpret_cast<const uint8_t*>(tb.xn_lo);
-    for (uint64_t wv = static_cast<uint64_t>(blockIdx.x) * G::kWaves + wave; wv * 64 < total; wv += waves_total) {
-        const Task tk = make_task(pa, wv * 64 + lane, total);
-        uint32_t reg = (tk.k == 0) ? tb.init[tk.rp] : 0u;
-        const bool aligned = (tk.len == 0) || ((reinterpret_cast<uintptr_t>(tk.sp + tk.len) & 15u) == 0);
-        if (__all(aligned))
-            reg = fold_staged<G, ABL>(reg, tk, s, slice, safe);
-        else
-            reg = fold_window(reg, tk.sp, tk.len, s, safe);
-        finish_task<MODE>(pa, tk, reg, tb);
-    }
-}
-
-// General direct-load kernel (every block loaded straight into VGPRs); kept as
-// the comparison point and selectable through enet_hip_set_tuning's path knob.
 template <int MODE>
 __global__ void __launch_bounds__(kThreads) crc32_direct_kernel(PacketArgs pa, KernelTables tb) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -294,10 +643,10 @@ __global__ void __launch_bounds__(kThreads) crc32_direct_kernel(PacketArgs pa, K
     const uint8_t* safe = reinterpret_cast<const uint8_t*>(tb.xn_lo);
     for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * kThreads + (threadIdx.x & ~63u); base < total;
          base += stride) {
-        const Task tk = make_task(pa, base + (threadIdx.x & 63u), total);
+        const DTask tk = make_dtask(pa, base + (threadIdx.x & 63u), total);
         uint32_t reg = (tk.k == 0) ? tb.init[tk.rp] : 0u;
         reg = fold_window(reg, tk.sp, tk.len, s, safe);
-        finish_task<MODE>(pa, tk, reg, tb);
+        finish_dtask<MODE>(pa, tk, reg, tb);
     }
 }
 
@@ -369,7 +718,7 @@ struct enet_hip_context {
     uint32_t* d_init = nullptr;  // 32
     int lanes_per_packet = 0;    // 0 = auto
     int wgs_per_cu = 0;          // 0 = auto (direct / gather kernels)
-    int path = 0;                // 0 = staged (auto), 1 = direct
+    int path = 0;                // 0 = stream (default geometry), 1 = direct, 2+k = stream geometry k
     int ablation = 0;            // diagnostics: 1 = no lookups, 2 = no DMA (wrong CRCs by design)
     // staging for the host-memory entry points
     std::mutex mu;
@@ -389,25 +738,57 @@ int herr(hipError_t e) { return e == hipSuccess ? 0 : -static_cast<int>(e); }
         if (e_ != hipSuccess) return herr(e_); \
     } while (0)
 
+// x^-1 mod p = (p(x) + 1) / x in the reflected representation (bit 31-i <-> x^i).
+constexpr uint32_t x_inverse() {
+    uint32_t v = 1u;                                   // x^32 / x = x^31
+    for (int i = 1; i < 32; ++i)
+        if ((kPoly >> (31 - i)) & 1u) v |= 1u << (31 - (i - 1));
+    return v;
+}
+static_assert(gf2_mulmod(x_inverse(), kOneReflected >> 1) == kOneReflected, "x * x^-1 = 1");
+
+constexpr int kImages = 4;                             // P = 1, 4, 8, 16
+constexpr int kImageP[kImages] = {1, 4, 8, 16};
+
 struct HostTables {
     std::vector<uint32_t> image, xn, init;
-    HostTables() : image(kLdsTableBytes / 4), xn(2 * kXnEntries), init(32) {
-        // slicing tables T_t[j] = byte j followed by t zero bytes (t < 32)
-        static uint32_t T[32][256];
-        for (uint32_t j = 0; j < 256; ++j) T[0][j] = crc_table_entry(j);
-        for (int t = 1; t < 32; ++t)
-            for (uint32_t j = 0; j < 256; ++j) T[t][j] = (T[t - 1][j] >> 8) ^ T[0][T[t - 1][j] & 0xFFu];
-        // LDS image: row j (128 B) = T_0[j] .. T_31[j] (crc32_device.hpp)
-        for (uint32_t j = 0; j < 256; ++j)
-            for (uint32_t t = 0; t < 32; ++t) image[j * 32 + t] = T[t][j];
+    HostTables() : image(static_cast<size_t>(kImages) * kImageDwords), xn(2 * kXnEntries), init(32) {
+        init[0] = 0xFFFFFFFFu;
+        for (int r = 1; r < 32; ++r) init[r] = unstep_zero(init[r - 1]);
+        std::vector<uint32_t> cinv(kCinvEntries);
+        uint32_t xinv8 = kOneReflected;
+        for (int i = 0; i < 8; ++i) xinv8 = gf2_mulmod(xinv8, x_inverse());
+        cinv[0] = kOneReflected;
+        for (int i = 1; i < kCinvEntries; ++i) cinv[i] = gf2_mulmod(cinv[i - 1], xinv8);
+        // image of P: dword 64j + 2t + (t>>4) = T_{t+32(P-1)}[j] (byte j followed by
+        // t + 32(P-1) zero bytes); the free dwords hold INIT[] and CINV[]
+        for (int im = 0; im < kImages; ++im) {
+            uint32_t* img = image.data() + static_cast<size_t>(im) * kImageDwords;
+            std::vector<uint32_t> row(256);
+            for (uint32_t j = 0; j < 256; ++j) {
+                uint32_t r = crc_table_entry(j);
+                for (int z = 0; z < 32 * (kImageP[im] - 1); ++z) r = sarwate_step(r, 0);
+                row[j] = r;
+            }
+            for (uint32_t t = 0; t < 32; ++t) {
+                for (uint32_t j = 0; j < 256; ++j) img[(j * 256 + col_byte(t)) / 4] = row[j];
+                for (uint32_t j = 0; j < 256; ++j) row[j] = sarwate_step(row[j], 0);
+            }
+            for (uint32_t lvl = 0; lvl < 4; ++lvl) {
+                const uint32_t c = cinv[32u << lvl];                   // x^(-8 * 32 * 2^lvl)
+                for (uint32_t b = 0; b < 4; ++b)
+                    for (uint32_t v = 0; v < 256; ++v)
+                        img[(256u * v + free_col(kLevelCol + 4 * lvl + b)) / 4] = gf2_mulmod(v << (8 * b), c);
+            }
+            for (uint32_t r = 0; r < 32; ++r) img[init_addr(r) / 4] = init[r];
+            for (uint32_t i = 0; i < static_cast<uint32_t>(kCinvEntries); ++i) img[cinv_addr(i) / 4] = cinv[i];
+        }
         // x^(8n) for n < 65536: one zero-byte step per n
         xn[0] = kOneReflected;
         for (int n = 1; n < kXnEntries; ++n) xn[n] = sarwate_step(xn[n - 1], 0);
         const uint32_t x64k = sarwate_step(xn[kXnEntries - 1], 0);  // x^(8*65536)
         xn[kXnEntries] = kOneReflected;
         for (int q = 1; q < kXnEntries; ++q) xn[kXnEntries + q] = gf2_mulmod(xn[kXnEntries + q - 1], x64k);
-        init[0] = 0xFFFFFFFFu;
-        for (int r = 1; r < 32; ++r) init[r] = unstep_zero(init[r - 1]);
     }
 };
 
@@ -416,7 +797,7 @@ const HostTables& host_tables() {
     return t;
 }
 
-int auto_lanes(const enet_hip_context* ctx) { return ctx->lanes_per_packet > 0 ? ctx->lanes_per_packet : 4; }
+int auto_lanes(const enet_hip_context* ctx) { return ctx->lanes_per_packet > 0 ? ctx->lanes_per_packet : 8; }
 
 int log2i(int v) {
     int l = 0;
@@ -435,27 +816,27 @@ unsigned grid_for(const enet_hip_context* ctx, uint64_t tasks) {
     return static_cast<unsigned>(std::max<uint64_t>(1, std::min(need, cap)));
 }
 
-// Staged geometries (waves per CU, blocks per stage, buffers).  kStagedDefault is
-// what path 0 runs; the others are reachable through enet_hip_set_kernel_path
-// (2 + index) for tuning sweeps.
+// Stream geometries (waves per CU, blocks per stage, stage buffers).
+// kStreamDefault is what path 0 runs; the others are reachable through
+// enet_hip_set_kernel_path (2 + index) for tuning sweeps.
 template <class G>
-struct StagedVariant {
+struct StreamVariant {
     static void launch(int mode, int abl, unsigned grid, hipStream_t st, const PacketArgs& pa,
                        const KernelTables& tb) {
         if (mode == 1)
-            hipLaunchKernelGGL((crc32_staged_kernel<1, G>), dim3(grid), dim3(G::kThreads), G::kLds, st, pa, tb);
+            hipLaunchKernelGGL((crc32_stream_kernel<1, G>), dim3(grid), dim3(G::kThreads), G::kLds, st, pa, tb);
         else if (abl == 1)
-            hipLaunchKernelGGL((crc32_staged_kernel<0, G, 1>), dim3(grid), dim3(G::kThreads), G::kLds, st, pa, tb);
+            hipLaunchKernelGGL((crc32_stream_kernel<0, G, 1>), dim3(grid), dim3(G::kThreads), G::kLds, st, pa, tb);
         else if (abl == 2)
-            hipLaunchKernelGGL((crc32_staged_kernel<0, G, 2>), dim3(grid), dim3(G::kThreads), G::kLds, st, pa, tb);
+            hipLaunchKernelGGL((crc32_stream_kernel<0, G, 2>), dim3(grid), dim3(G::kThreads), G::kLds, st, pa, tb);
         else
-            hipLaunchKernelGGL((crc32_staged_kernel<0, G, 0>), dim3(grid), dim3(G::kThreads), G::kLds, st, pa, tb);
+            hipLaunchKernelGGL((crc32_stream_kernel<0, G, 0>), dim3(grid), dim3(G::kThreads), G::kLds, st, pa, tb);
     }
     static int setup() {
-        const void* fns[] = {reinterpret_cast<const void*>(crc32_staged_kernel<0, G, 0>),
-                             reinterpret_cast<const void*>(crc32_staged_kernel<0, G, 1>),
-                             reinterpret_cast<const void*>(crc32_staged_kernel<0, G, 2>),
-                             reinterpret_cast<const void*>(crc32_staged_kernel<1, G, 0>)};
+        const void* fns[] = {reinterpret_cast<const void*>(crc32_stream_kernel<0, G, 0>),
+                             reinterpret_cast<const void*>(crc32_stream_kernel<0, G, 1>),
+                             reinterpret_cast<const void*>(crc32_stream_kernel<0, G, 2>),
+                             reinterpret_cast<const void*>(crc32_stream_kernel<1, G, 0>)};
         for (const void* f : fns) {
             const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, G::kLds);
             if (e != hipSuccess) return herr(e);
@@ -464,45 +845,45 @@ struct StagedVariant {
     }
 };
 
-using StagedGeoms = std::tuple<StagedGeom<16, 2, 2>, StagedGeom<8, 2, 4>, StagedGeom<8, 4, 2>,
-                               StagedGeom<16, 1, 4>, StagedGeom<10, 2, 3>, StagedGeom<5, 4, 3>>;
-constexpr int kNumStagedGeoms = std::tuple_size<StagedGeoms>::value;
-constexpr int kStagedDefault = 0;
+using StreamGeoms = std::tuple<StreamGeom<16, 1, 2>, StreamGeom<11, 1, 3>, StreamGeom<8, 1, 4>,
+                               StreamGeom<8, 2, 2>, StreamGeom<6, 2, 3>, StreamGeom<10, 1, 3>>;
+constexpr int kNumStreamGeoms = std::tuple_size<StreamGeoms>::value;
+constexpr int kStreamDefault = 0;
 
 template <size_t I = 0>
-void launch_staged(int geom, int mode, int abl, int num_cus, uint64_t tasks, hipStream_t st,
+void launch_stream(int geom, int mode, int abl, int num_cus, uint64_t groups, hipStream_t st,
                    const PacketArgs& pa, const KernelTables& tb) {
-    if constexpr (I < std::tuple_size<StagedGeoms>::value) {
-        using G = std::tuple_element_t<I, StagedGeoms>;
+    if constexpr (I < std::tuple_size<StreamGeoms>::value) {
+        using G = std::tuple_element_t<I, StreamGeoms>;
         if (geom == static_cast<int>(I)) {
-            const uint64_t waves = (tasks + 63) / 64;
             const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(
-                1, std::min<uint64_t>((waves + G::kWaves - 1) / G::kWaves, static_cast<uint64_t>(num_cus))));
-            StagedVariant<G>::launch(mode, abl, grid, st, pa, tb);
+                1, std::min<uint64_t>((groups + G::kWaves - 1) / G::kWaves, static_cast<uint64_t>(num_cus))));
+            StreamVariant<G>::launch(mode, abl, grid, st, pa, tb);
         } else {
-            launch_staged<I + 1>(geom, mode, abl, num_cus, tasks, st, pa, tb);
+            launch_stream<I + 1>(geom, mode, abl, num_cus, groups, st, pa, tb);
         }
     }
 }
 
 template <size_t I = 0>
-int setup_staged() {
-    if constexpr (I < std::tuple_size<StagedGeoms>::value) {
-        const int rc = StagedVariant<std::tuple_element_t<I, StagedGeoms>>::setup();
-        return rc ? rc : setup_staged<I + 1>();
+int setup_stream() {
+    if constexpr (I < std::tuple_size<StreamGeoms>::value) {
+        const int rc = StreamVariant<std::tuple_element_t<I, StreamGeoms>>::setup();
+        return rc ? rc : setup_stream<I + 1>();
     }
     return 0;
 }
 
 int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStream_t st) {
     if (pa.n == 0) return 0;
-    const uint64_t tasks = pa.n << pa.lg;
     const KernelTables tb = tables_of(ctx);
-    if (ctx->path != 1) {
-        // persistent: one workgroup per CU (up to 160 KiB LDS each)
-        const int geom = ctx->path == 0 ? kStagedDefault : ctx->path - 2;
-        launch_staged(geom, mode, ctx->ablation, ctx->num_cus, tasks, st, pa, tb);
+    // the stream kernel takes 4, 8 or 16 lanes per packet; anything else runs direct
+    if (ctx->path != 1 && pa.lg >= 2 && pa.lg <= 4) {
+        const uint64_t groups = (pa.n + (64u >> pa.lg) - 1) >> (6 - pa.lg);
+        const int geom = ctx->path == 0 ? kStreamDefault : ctx->path - 2;
+        launch_stream(geom, mode, ctx->ablation, ctx->num_cus, groups, st, pa, tb);
     } else {
+        const uint64_t tasks = pa.n << pa.lg;
         const unsigned grid = grid_for(ctx, tasks);
         if (mode == 0)
             hipLaunchKernelGGL(crc32_direct_kernel<0>, dim3(grid), dim3(kThreads), kLdsTableBytes, st, pa, tb);
@@ -557,13 +938,13 @@ int enet_hip_context_create(int device, enet_hip_context** out) {
     int rc = 0;
     do {
         if ((rc = herr(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)))) break;
-        if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_image), kLdsTableBytes)))) break;
+        if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_image), ht.image.size() * 4)))) break;
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_xn), ht.xn.size() * 4)))) break;
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_init), 32 * 4)))) break;
-        if ((rc = herr(hipMemcpy(ctx->d_image, ht.image.data(), kLdsTableBytes, hipMemcpyHostToDevice)))) break;
+        if ((rc = herr(hipMemcpy(ctx->d_image, ht.image.data(), ht.image.size() * 4, hipMemcpyHostToDevice)))) break;
         if ((rc = herr(hipMemcpy(ctx->d_xn, ht.xn.data(), ht.xn.size() * 4, hipMemcpyHostToDevice)))) break;
         if ((rc = herr(hipMemcpy(ctx->d_init, ht.init.data(), 32 * 4, hipMemcpyHostToDevice)))) break;
-        if ((rc = setup_staged())) break;
+        if ((rc = setup_stream())) break;
         if ((rc = herr(hipFuncSetAttribute(reinterpret_cast<const void*>(crc32_direct_kernel<0>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTableBytes)))) break;
         if ((rc = herr(hipFuncSetAttribute(reinterpret_cast<const void*>(crc32_direct_kernel<1>),
@@ -610,7 +991,7 @@ int enet_hip_diag_ablation(enet_hip_context* ctx, int mode) {
 }
 
 int enet_hip_set_kernel_path(enet_hip_context* ctx, int path) {
-    if (!ctx || path < 0 || path > 1 + kNumStagedGeoms) return -static_cast<int>(hipErrorInvalidValue);
+    if (!ctx || path < 0 || path > 1 + kNumStreamGeoms) return -static_cast<int>(hipErrorInvalidValue);
     ctx->path = path;
     return 0;
 }

@@ -71,13 +71,13 @@ ENET_HIP_API int enet_hip_context_destroy(enet_hip_context* ctx);
 ENET_HIP_API const char* enet_hip_error_string(int code);
 
 /* Tuning knobs (0 = automatic).  lanes_per_packet: 1,2,4,...,64 lanes share one
- * packet (a power of two); workgroups_per_cu: resident workgroups per CU the
- * persistent grid is sized for. */
+ * packet (a power of two; default 8); workgroups_per_cu: resident workgroups per
+ * CU the direct / gather grids are sized for. */
 ENET_HIP_API int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgroups_per_cu);
 
-/* Kernel path for the packet batch entry points: 0 = LDS-staged (default; waves
- * whose windows are not 16-byte aligned fall back to direct loads inside the
- * same launch), 1 = direct loads only. */
+/* Kernel path for the packet batch entry points: 0 = LDS-DMA stream kernel
+ * (default; needs 4, 8 or 16 lanes per packet, other values run direct),
+ * 1 = direct loads only, 2 + k = stream kernel with tuning geometry k (sweeps). */
 ENET_HIP_API int enet_hip_set_kernel_path(enet_hip_context* ctx, int path);
 
 /* ---- batched checksum, device-resident ----
@@ -132,7 +132,7 @@ ENET_HIP_API int enet_hip_crc32_batch_multi(enet_hip_context* const* contexts, i
 ENET_HIP_API int enet_hip_read_probe_device(enet_hip_context* ctx, const uint8_t* bytes, size_t byteCount,
                                             uint32_t* sink, void* stream);
 
-/* ---- diagnostics: roofline ablation of the staged kernel ----
+/* ---- diagnostics: roofline ablation of the stream kernel ----
  * 0 = normal; 1 = skip the table lookups (memory path alone); 2 = skip the
  * LDS-DMA (compute path alone).  Modes 1 and 2 produce WRONG checksums by
  * design and exist only to price the two halves of the kernel (tools/). */

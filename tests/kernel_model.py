@@ -1,15 +1,28 @@
-"""Host-side model of the gfx950 kernel's arithmetic (test infrastructure).
+"""Host-side model of the gfx950 kernels' arithmetic (test infrastructure).
 
-Restates, in Python integers, exactly what crc32_kernels.hip does per lane --
-LDS image layout, per-lane v_perm selectors and column bytes, the dword swaps,
-slicing-by-32 folding, END-aligned windows with INIT[r'], splitting a packet over
-P lanes and the GF(2) carry-combine -- so the algebra and the bank mapping can be
-checked on CPU against the oracle before any GPU run.  It models the arithmetic,
-not the hardware: parity on the device is established by the -m gpu tests.
+Restates, in Python integers, what crc32_kernels.hip does per lane -- the 64 KiB
+LDS image (slicing tables + INIT/CINV in the free dwords), the per-lane v_perm
+selectors and column bytes, the dword swaps, slicing-by-32 folding, and the two
+ways a packet is spread over P lanes:
+
+  * stream kernel (crc32_stream_kernel): STRIDED blocks.  The packet's window
+    starts at the 16-byte granule holding its first byte; lane k folds window
+    blocks k, k+P, k+2P, ... with the advancing tables T'_t = T_{t+32(P-1)}, so
+    after each block its register has also skipped the P-1 blocks the other
+    lanes own.  Head (lz) and tail (tz) bytes are zeroed, and each lane's
+    overshoot past the data end (32*o_k + tz bytes) is undone by one GF(2)
+    multiply by x^(-8n) (CINV table).
+  * direct kernel (crc32_direct_kernel / gather): CONTIGUOUS segments cut at
+    128-byte-aligned addresses, END-aligned windows started at INIT[rp], and the
+    classic carry-combine reg(A||B) = reg(A) * x^(8|B|) ^ reg(B).
+
+It models the arithmetic, not the hardware: parity on the device is established
+by the -m gpu tests.
 """
 from __future__ import annotations
 
 POLY = 0xEDB88320
+ONE = 0x80000000          # the polynomial "1" in the reflected representation
 
 
 def t0(n: int) -> int:
@@ -22,27 +35,151 @@ def t0(n: int) -> int:
 T0 = [t0(n) for n in range(256)]
 
 
-def slicing_tables(k: int = 32) -> list[list[int]]:
-    T = [T0[:]]
+def zstep(reg: int) -> int:
+    """One zero byte through the Sarwate register."""
+    return (reg >> 8) ^ T0[reg & 0xFF]
+
+
+def slicing_tables(k: int = 32, skip: int = 0) -> list[list[int]]:
+    """T_t[j] = byte j followed by t + skip zero bytes, t < k."""
+    first = []
+    for j in range(256):
+        r = T0[j]
+        for _ in range(skip):
+            r = zstep(r)
+        first.append(r)
+    T = [first]
     for _ in range(1, k):
-        prev = T[-1]
-        T.append([(prev[j] >> 8) ^ T0[prev[j] & 0xFF] for j in range(256)])
+        T.append([zstep(v) for v in T[-1]])
     return T
 
 
 TS = slicing_tables(32)
 
 
-def lds_image() -> list[int]:
-    """dword j*32 + t = T_t[j]  (256 rows x 32 dwords = 32 KiB, crc32_device.hpp)."""
-    img = [0] * (256 * 32)
+# ---------------------------------------------------------------- GF(2) helpers
+def mulmod(a: int, b: int) -> int:
+    p = 0
+    for j in range(32):
+        if (a >> (31 - j)) & 1:
+            p ^= b
+        b = (b >> 1) ^ (POLY if b & 1 else 0)
+    return p
+
+
+def x8n(n: int) -> int:
+    r = ONE
+    for _ in range(n):
+        r = zstep(r)
+    return r
+
+
+def x_inverse() -> int:
+    """x^-1 mod p = (p(x) + 1) / x, reflected (bit 31-i <-> x^i)."""
+    # p(x) + 1 = x^32 + sum of POLY's terms without the constant; divide by x
+    # POLY reflected: bit (31-i) set <-> x^i in p (i < 32); x^0 is bit 31.
+    v = 0
+    for i in range(1, 32):                      # term x^i of p, i >= 1 -> x^(i-1)
+        if (POLY >> (31 - i)) & 1:
+            v |= 1 << (31 - (i - 1))
+    v |= 1 << (31 - 31)                         # x^32 / x = x^31
+    return v
+
+
+XINV = x_inverse()
+assert mulmod(XINV, x8n(0) >> 1) == ONE       # x^-1 * x = 1  (x = ONE >> 1)
+
+
+def cinv_table(n: int = 512) -> list[int]:
+    """CINV[i] = x^(-8i) mod p."""
+    xinv8 = ONE
+    for _ in range(8):
+        xinv8 = mulmod(xinv8, XINV)
+    out = [ONE]
+    for _ in range(1, n):
+        out.append(mulmod(out[-1], xinv8))
+    return out
+
+
+CINV = cinv_table()
+
+
+def unstep_zero(reg_next: int) -> int:
+    top = reg_next >> 24
+    n = next(k for k in range(256) if (T0[k] >> 24) == top)
+    return (((reg_next ^ T0[n]) << 8) & 0xFFFFFFFF) | n
+
+
+INIT = [0xFFFFFFFF]
+for _ in range(31):
+    INIT.append(unstep_zero(INIT[-1]))
+
+
+# ---------------------------------------------------------------- 64 KiB LDS image
+def col_byte(t: int) -> int:
+    """Byte offset of table t inside a 256-byte row: dword 2t + (t >> 4)."""
+    return 8 * t + 4 * (t >> 4)
+
+
+def free_col(c: int) -> int:
+    """Byte offset of free column c (c < 32): the dwords no slicing table uses."""
+    return 4 * (2 * c + 1 if c < 16 else 2 * c)
+
+
+# Free columns are 256-entry tables indexed by the row (a byte value), so a
+# lookup is one v_perm (byte -> address byte 1, column -> byte 0) + ds_read.
+KLEVEL_COL = 0            # columns 0..15: butterfly tables, level l (m = 2^l), byte b -> column 4l + b
+KINIT_COL = 16            # INIT[r], r < 32 (rows 0..31)
+KCINV_COL = 17            # CINV[n], n < 512: rows n & 255 of columns 17 + (n >> 8)
+
+
+def init_addr(r: int) -> int:
+    return 256 * r + free_col(KINIT_COL)
+
+
+def cinv_addr(n: int) -> int:
+    return 256 * (n & 255) + free_col(KCINV_COL + (n >> 8))
+
+
+def level_addr(lvl: int, b: int, v: int) -> int:
+    return 256 * v + free_col(KLEVEL_COL + 4 * lvl + b)
+
+
+def lds_image(P: int = 1) -> list[int]:
+    """dword 64*j + 2t + (t>>4) = T'_t[j] = T_{t + 32(P-1)}[j]; free columns hold
+    the butterfly tables, INIT and CINV."""
+    T = slicing_tables(32, 32 * (P - 1))
+    img = [0] * (256 * 64)
     for j in range(256):
         for t in range(32):
-            img[j * 32 + t] = TS[t][j]
+            img[64 * j + col_byte(t) // 4] = T[t][j]
+    for lvl in range(4):
+        c = CINV[32 << lvl]                       # x^(-8 * 32m), m = 2^lvl
+        for b in range(4):
+            for v in range(256):
+                img[level_addr(lvl, b, v) // 4] = mulmod(v << (8 * b), c)
+    for r in range(32):
+        img[init_addr(r) // 4] = INIT[r]
+    for n in range(512):
+        img[cinv_addr(n) // 4] = CINV[n]
     return img
 
 
-IMG = lds_image()
+_IMG_CACHE: dict[int, list[int]] = {}
+
+
+def image(P: int = 1) -> list[int]:
+    if P not in _IMG_CACHE:
+        _IMG_CACHE[P] = lds_image(P)
+    return _IMG_CACHE[P]
+
+
+def level_apply(img: list[int], lvl: int, v: int) -> int:
+    """adv by -32*2^lvl bytes via four column lookups (the kernel's butterfly step)."""
+    out = 0
+    for b in range(4):
+        out ^= img[level_addr(lvl, b, (v >> (8 * b)) & 0xFF) // 4]
+    return out
 
 
 def v_perm(s0: int, s1: int, sel: int) -> int:
@@ -57,7 +194,7 @@ def v_perm(s0: int, s1: int, sel: int) -> int:
             b = 0x00
         elif sb >= 13:
             b = 0xFF
-        else:  # 8..11: sign replication of bytes 1,3,5,7 (unused by the kernel)
+        else:  # 8..11: sign replication (unused by the kernel)
             src = (data >> (8 * (2 * (sb - 8) + 1) + 7)) & 1
             b = 0xFF if src else 0
         out |= b << (8 * k)
@@ -72,8 +209,9 @@ def make_sched(lane: int):
         for h in range(4):
             i = 4 * g + h
             t = (i ^ l5) ^ 31
-            r |= (8 * t) << (8 * h)
+            r |= col_byte(t) << (8 * h)
         col.append(r)
+    # byte 0 of the address = column byte h of col (S1), byte 1 = data byte (S0)
     sel = [h | ((4 + (h ^ (l5 & 3))) << 8) | 0x0C0C0000 for h in range(4)]
     return col, sel, bool((l5 >> 2) & 1), bool((l5 >> 3) & 1), bool((l5 >> 4) & 1)
 
@@ -81,63 +219,117 @@ def make_sched(lane: int):
 def lookup_addresses(lane: int, words: list[int]) -> list[int]:
     """LDS byte address of each of the 32 lookups of fold_block (words in original
     order, state already XORed): halves put in lane order, two dword-swap rounds,
-    then v_perm(...) >> 1."""
+    then one v_perm per lookup (no shift)."""
     col, sel, sw1, sw2, hs = make_sched(lane)
     w = (words[4:8] + words[0:4]) if hs else list(words)
     x = [w[q ^ 1] if sw1 else w[q] for q in range(8)]
     d = [x[q ^ 2] if sw2 else x[q] for q in range(8)]
-    return [v_perm(d[i >> 2], col[i >> 2], sel[i & 3]) >> 1 for i in range(32)]
+    return [v_perm(d[i >> 2], col[i >> 2], sel[i & 3]) for i in range(32)]
 
 
-def fold_block(reg: int, block: bytes, lane: int) -> int:
+def fold_block(reg: int, block: bytes, lane: int, P: int = 1) -> int:
+    img = image(P)
     w = [int.from_bytes(block[4 * q:4 * q + 4], "little") for q in range(8)]
     w[0] ^= reg
     acc = 0
     for addr in lookup_addresses(lane, w):
-        assert addr % 4 == 0 and addr < 32768
-        acc ^= IMG[addr // 4]
+        assert addr % 4 == 0 and addr < 65536
+        acc ^= img[addr // 4]
     return acc
 
 
-def mulmod(a: int, b: int) -> int:
-    p = 0
-    for j in range(32):
-        if (a >> (31 - j)) & 1:
-            p ^= b
-        b = (b >> 1) ^ (POLY if b & 1 else 0)
-    return p
+def finalize(reg: int) -> int:
+    return int.from_bytes((~reg & 0xFFFFFFFF).to_bytes(4, "little"), "big")
 
 
-def x8n(n: int) -> int:
-    r = 0x80000000
-    for _ in range(n):
-        r = (r >> 8) ^ T0[r & 0xFF]
-    return r
+# ---------------------------------------------------------------- stream kernel
+def stream_window(addr: int, L: int):
+    """(lz, NB, tz).  Packet end 16-byte aligned: END-aligned window (tz = 0, lz <
+    32 leading zero bytes, the first granule may lie wholly in front of the packet
+    and is then not loaded).  Otherwise START-aligned at the packet's 16-byte
+    granule (lz = addr & 15) with tz trailing bytes zeroed."""
+    if L == 0:
+        return 0, 0, 0
+    if (addr + L) % 16 == 0:
+        nb = (L + 31) // 32
+        return 32 * nb - L, nb, 0
+    lz = addr & 15
+    nb = (lz + L + 31) // 32
+    return lz, nb, 32 * nb - lz - L
 
 
-def unstep_zero(reg_next: int) -> int:
-    top = reg_next >> 24
-    n = next(k for k in range(256) if (T0[k] >> 24) == top)
-    return (((reg_next ^ T0[n]) << 8) & 0xFFFFFFFF) | n
+def stream_lane_blocks(k: int, P: int, nb: int) -> list[int]:
+    """Rotated assignment: lane k folds window blocks w with (w + r) % P == k,
+    r = (-nb) % P, so that lane k ends exactly 32k bytes past the window end."""
+    r = (-nb) % P
+    return list(range((k - r) % P, nb, P))
 
 
-INIT = [0xFFFFFFFF]
-for _ in range(31):
-    INIT.append(unstep_zero(INIT[-1]))
-
-
-def fold_window(reg: int, pkt: bytes, j0: int, j1: int, lane: int) -> int:
+def stream_packet(pkt: bytes, P: int, addr: int = 0, lane_base: int = 0,
+                  slot: tuple[int, int] | None = None) -> tuple[int, int]:
+    """What crc32_stream_kernel's P lanes compute for one packet at byte address
+    `addr`.  slot = (slot_offset, connect_id) models the verify mode: the 4 slot
+    bytes are replaced by connect_id inside the lane that folds them and the
+    original bytes are returned as `desired`.  Returns (register, desired)."""
     L = len(pkt)
+    lz, nb, tz = stream_window(addr, L)
+    win = bytes(lz) + pkt + bytes(tz)          # head/tail bytes zeroed by the kernel
+    img = image(P)
+    r = (-nb) % P
+    desired = 0
+    regs = []
+    for k in range(P):
+        lane = lane_base + k
+        reg = INIT[lz] if k == r else 0
+        blocks = stream_lane_blocks(k, P, nb)
+        for w in blocks:
+            blk = bytearray(win[32 * w:32 * w + 32])
+            if slot is not None:
+                so, cid = slot
+                for q in range(4):
+                    pos = lz + so + q - 32 * w
+                    if 0 <= pos < 32:
+                        desired |= blk[pos] << (8 * q)
+                        blk[pos] = (cid >> (8 * q)) & 0xFF
+            reg = fold_block(reg, bytes(blk), lane, P)
+        if blocks:
+            assert blocks[-1] + P - nb == k        # overshoot is exactly k blocks
+        regs.append(reg)
+    m, lvl = 1, 0
+    while m < P:                                   # butterfly: lane k += adv_{-32m}(lane k+m)
+        for k in range(0, P, 2 * m):
+            regs[k] ^= level_apply(img, lvl, regs[k + m])
+        m, lvl = 2 * m, lvl + 1
+    total = regs[0]
+    if tz:
+        total = mulmod(total, CINV[tz])
+    return total, desired
+
+
+def stream_crc(pkt: bytes, P: int, addr: int = 0, lane_base: int = 0) -> int:
+    return finalize(stream_packet(pkt, P, addr, lane_base)[0])
+
+
+def stream_verify(pkt: bytes, slot_off: int, connect: int, P: int, addr: int = 0) -> tuple[bool, int]:
+    if slot_off + 4 > len(pkt):
+        return False, 0
+    reg, desired = stream_packet(pkt, P, addr, 0, (slot_off, connect))
+    comp = finalize(reg)
+    return comp == desired, comp
+
+
+# ---------------------------------------------------------------- direct kernel
+def fold_window(reg: int, seg: bytes, lane: int) -> int:
+    L = len(seg)
     nb = (L + 31) // 32
-    rp = 32 * nb - L
-    win = bytes(rp) + pkt          # bytes in front of the packet read as zero
-    for j in range(j0, j1):
+    win = bytes(32 * nb - L) + seg
+    for j in range(nb):
         reg = fold_block(reg, win[32 * j:32 * j + 32], lane)
     return reg
 
 
 def segment_cuts(addr: int, L: int, lanes: int) -> list[int]:
-    """make_task's cut points: packet [addr, addr+L) split at 128-byte-aligned
+    """Direct kernel's cut points: packet [addr, addr+L) split at 128-byte-aligned
     absolute addresses nearest to the even split (offsets relative to addr)."""
     cuts = [0]
     for k in range(1, lanes):
@@ -148,9 +340,6 @@ def segment_cuts(addr: int, L: int, lanes: int) -> list[int]:
 
 
 def crc_packet(pkt: bytes, lanes: int = 1, lane_base: int = 0, addr: int = 0) -> int:
-    """What one packet's P lanes compute: lane k folds segment [cut_k, cut_k+1) as
-    its own end-aligned window (zero-init except lane 0, which starts at
-    INIT[rp]), then the partial registers are advanced and XORed."""
     L = len(pkt)
     cuts = segment_cuts(addr, L, lanes)
     total = 0
@@ -159,29 +348,9 @@ def crc_packet(pkt: bytes, lanes: int = 1, lane_base: int = 0, addr: int = 0) ->
         nb = (len(seg) + 31) // 32
         rp = 32 * nb - len(seg)
         reg = INIT[rp] if k == 0 else 0
-        reg = fold_window(reg, seg, 0, nb, lane_base + k)
+        reg = fold_window(reg, seg, lane_base + k)
         after = L - cuts[k + 1]
         if after:
             reg = mulmod(reg, x8n(after))
         total ^= reg
-    return int.from_bytes((~total & 0xFFFFFFFF).to_bytes(4, "little"), "big")
-
-
-def verify_packet(pkt: bytes, slot_off: int, connect: int, lanes: int = 1) -> tuple[bool, int]:
-    L = len(pkt)
-    if slot_off + 4 > L:
-        return False, 0
-    cuts = segment_cuts(0, L, lanes)
-    total = 0
-    for k in range(lanes):
-        seg = pkt[cuts[k]:cuts[k + 1]]
-        nb = (len(seg) + 31) // 32
-        rp = 32 * nb - len(seg)
-        reg = fold_window(INIT[rp] if k == 0 else 0, seg, 0, nb, k)
-        if L - cuts[k + 1]:
-            reg = mulmod(reg, x8n(L - cuts[k + 1]))
-        total ^= reg
-    desired = int.from_bytes(pkt[slot_off:slot_off + 4], "little")
-    total ^= mulmod(desired ^ connect, x8n(L - slot_off))
-    comp = int.from_bytes((~total & 0xFFFFFFFF).to_bytes(4, "little"), "big")
-    return comp == desired, comp
+    return finalize(total)

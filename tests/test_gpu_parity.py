@@ -115,6 +115,28 @@ def test_linearity_and_determinism(ctx):
     assert (run_batch(ctx, a, off, lens, 16, 1) == ca).all()
 
 
+N_STREAM_GEOMS = 6
+
+
+@pytest.mark.parametrize("geom", range(N_STREAM_GEOMS))
+def test_stream_geometries(ctx, golden, oracle_lib, geom):
+    """Every stream-kernel geometry (path 2 + k) x 4/8/16 lanes: golden vectors,
+    unaligned mixed sizes (empty packets included) and many groups per wave."""
+    payload, off, lens, exp = golden_batch(golden)
+    b = workloads.mixed(30000, 0, 3000, seed=40 + geom, len_seed=41 + geom)
+    exp_b = oracle_lib.batch(b.payload, b.off, b.lens, threads=16)
+    small = workloads.mixed(200000, 1, 100, seed=7, len_seed=8)
+    exp_s = oracle_lib.batch(small.payload, small.off, small.lens, threads=16)
+    try:
+        ctx.set_kernel_path(2 + geom)
+        for lanes in (4, 8, 16):
+            assert (run_batch(ctx, payload, off, lens, lanes) == exp).all(), ("golden", lanes)
+            assert (run_batch(ctx, b.payload, b.off, b.lens, lanes) == exp_b).all(), ("mixed", lanes)
+        assert (run_batch(ctx, small.payload, small.off, small.lens, 4) == exp_s).all()
+    finally:
+        ctx.set_kernel_path(0)
+
+
 def test_host_entry_point(ctx, oracle_lib):
     b = workloads.mixed(20000, 1, 4096, seed=9, len_seed=10)
     ctx.set_tuning(0, 0)
@@ -166,7 +188,7 @@ def test_verify_batch(ctx, oracle_lib):
         payload[j] ^= np.uint8(1 << int(rng.integers(0, 8)))
     exp_ok, exp_comp = oracle_lib.verify(payload, off, lens, slot, conn)
     assert exp_ok.sum() == n - 300
-    for lanes in (1, 4):
+    for lanes in (1, 4, 8, 16):
         ctx.set_tuning(lanes, 0)
         d_ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
         d_comp = torch.zeros(n, dtype=torch.int32, device="cuda")

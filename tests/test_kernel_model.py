@@ -21,7 +21,36 @@ def test_slicing_tables_and_image():
             for _ in range(t):
                 reg = (reg >> 8) ^ km.T0[reg & 0xFF]
             assert km.TS[t][j] == reg
-    assert km.IMG[5 * 32 + 9] == km.TS[9][5]
+    img = km.image(1)
+    assert img[64 * 5 + km.col_byte(9) // 4] == km.TS[9][5]
+    assert img[64 * 5 + km.col_byte(20) // 4] == km.TS[20][5]
+    # advancing tables: T'_t = T_{t + 32(P-1)}
+    img4 = km.image(4)
+    ref = km.TS[3][7]
+    for _ in range(96):
+        ref = km.zstep(ref)
+    assert img4[64 * 7 + km.col_byte(3) // 4] == ref
+
+
+def test_free_columns_disjoint_from_tables():
+    used = {km.col_byte(t) for t in range(32)}
+    free = {km.free_col(c) for c in range(32)}
+    assert not (used & free) and len(used | free) == 64
+    img = km.image(8)
+    for r in range(32):
+        assert img[km.init_addr(r) // 4] == km.INIT[r]
+    for i in (0, 1, 31, 200, 255, 256, 511):
+        assert img[km.cinv_addr(i) // 4] == km.CINV[i]
+    rng = random.Random(9)
+    for lvl in range(4):
+        for _ in range(20):
+            v = rng.getrandbits(32)
+            assert km.level_apply(img, lvl, v) == km.mulmod(v, km.CINV[32 << lvl])
+
+
+def test_cinv_inverts_x8n():
+    for n in (0, 1, 2, 31, 32, 100, 511):
+        assert km.mulmod(km.CINV[n], km.x8n(n)) == km.ONE
 
 
 def test_lds_bank_conflict_free():
@@ -41,11 +70,12 @@ def test_each_lane_reads_every_byte_once():
     rng = random.Random(2)
     block = bytes(rng.getrandbits(8) for _ in range(32))
     words = [int.from_bytes(block[4 * q:4 * q + 4], "little") for q in range(8)]
+    inv = {km.col_byte(t): t for t in range(32)}
     for lane in range(64):
         addrs = km.lookup_addresses(lane, words)
         used = set()
         for a in addrs:
-            row, t = a // 128, (a % 128) // 4
+            row, t = a // 256, inv[a % 256]
             m = t ^ 31
             assert block[m] == row      # looked-up row is byte m of the block
             used.add(m)
@@ -84,12 +114,21 @@ def test_mulmod_is_zero_advance():
 
 
 @pytest.mark.parametrize("lanes", [1, 2, 4, 8, 64])
-def test_packet_model_matches_oracle(lanes):
+def test_direct_packet_model_matches_oracle(lanes):
     rng = random.Random(10 + lanes)
     for L in [0, 1, 3, 4, 15, 16, 17, 31, 32, 33, 63, 64, 65, 100, 257, 1200, 1201]:
         pkt = bytes(rng.getrandbits(8) for _ in range(L))
         for addr in (0, 16, 1200 * 7, 4093):
             assert km.crc_packet(pkt, lanes, addr=addr) == oracle.enet_crc32_py([pkt]), (L, lanes, addr)
+
+
+@pytest.mark.parametrize("P", [1, 4, 8, 16])
+def test_stream_packet_model_matches_oracle(P):
+    rng = random.Random(100 + P)
+    for L in [0, 1, 3, 4, 15, 16, 17, 31, 32, 33, 63, 64, 65, 100, 257, 511, 512, 1200, 1201]:
+        pkt = bytes(rng.getrandbits(8) for _ in range(L))
+        for addr in (0, 1, 15, 16, 1200 * 7, 4093):
+            assert km.stream_crc(pkt, P, addr) == oracle.enet_crc32_py([pkt]), (L, P, addr)
 
 
 def test_segment_cuts_are_line_aligned():
@@ -104,11 +143,15 @@ def test_segment_cuts_are_line_aligned():
 
 def test_verify_model(golden):
     vecs, blob = golden
+    n = 0
     for v in vecs:
         if v["kind"] != "verify":
             continue
-        o, n = v["segments"][0]
-        pkt = bytes(blob[o:o + n])
-        for lanes in (1, 4):
-            ok, _ = km.verify_packet(pkt, v["slot_off"], int(v["connect_id"], 16), lanes)
-            assert ok == v["expect_ok"]
+        o, ln = v["segments"][0]
+        pkt = bytes(blob[o:o + ln])
+        for P in (4, 8):
+            for addr in (0, 5):
+                ok, _ = km.stream_verify(pkt, v["slot_off"], int(v["connect_id"], 16), P, addr)
+                assert ok == v["expect_ok"]
+        n += 1
+    assert n > 0
