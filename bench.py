@@ -41,9 +41,10 @@ def parse(argv=None):
     ap.add_argument("--rotate", type=int, default=5, help="distinct resident batches cycled through")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per packet (0 = library default)")
     ap.add_argument("--wgs", type=int, default=0, help="workgroups per CU (0 = library default)")
-    ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3"])
+    ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "small"],
+                    help="cfg2 = the metric's workload; cfg3 = mixed lengths; small = harness tests only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=3.0, help="wall budget per CPU-baseline leg")
+    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget per CPU-baseline leg")
     return ap.parse_args(argv)
 
 
@@ -216,6 +217,8 @@ def make_batches(cfg: str, rotate: int, rank: int):
         seed = workloads.SEED_PAYLOAD + 7919 * (rank * rotate + j)
         if cfg == "cfg2":
             out.append(workloads.fixed(65536, 1200, seed=seed, name="cfg2"))
+        elif cfg == "small":
+            out.append(workloads.fixed(2048, 1200, seed=seed, name="small"))
         else:
             out.append(workloads.mixed(262144, 64, 1400, seed=seed, name="cfg3"))
     return out
@@ -289,8 +292,9 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
             "dtype": "u8",
             "data": "synthetic (splitmix64 payload, device-resident)",
             "config": {
-                "workload": ("cfg2: 65536 packets x 1200 B packed" if args.config == "cfg2"
-                             else "cfg3: 262144 packets x U[64,1400] B packed") +
+                "workload": {"cfg2": "cfg2: 65536 packets x 1200 B packed",
+                             "cfg3": "cfg3: 262144 packets x U[64,1400] B packed",
+                             "small": "small: 2048 packets x 1200 B (harness tests)"}[args.config] +
                             f", {args.rotate} rotating resident batches per GPU",
                 "packets_per_gpu": batches[0].n,
                 "payload_bytes_per_step": int(per_launch),
@@ -305,7 +309,7 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": (traffic or {}).get("hbm_bytes_per_launch"),
-                "kernel": "crc32_packets_kernel<0>",
+                "kernel": "crc32_stream_kernel<0, StreamGeom<16,1,2>>",
                 "kernel_ms": round(k_ms, 5),
                 "span_ms_per_step": round(span_ms, 5),
                 "read_probe_GBps": round(probe, 1),

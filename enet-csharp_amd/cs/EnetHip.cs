@@ -1,0 +1,215 @@
+// EnetHip.cs -- C# side of libenethip (the MI355X CRC32 checksum engine) for
+// enet-csharp.  Drop this file into the ENet project (namespace enet) and ship
+// libenethip.so next to the application.  See INTEGRATION.md.
+//
+// Binds include/enet_hip.h.  Reference interfaces (enet-csharp/ENet/):
+//   ENetHost.checksum ........ include/enet.cs:663-666  (delegate* managed<ENetBuffer*, nuint, uint>)
+//   ENet.enet_crc32 .......... c/packet.cs:142-160       (the default checksum)
+//   ENetBuffer ............... include/win32.cs:25-29    ({ nuint dataLength; void* data; }, length first)
+//
+// The callback field holds a *managed* function pointer, so the native export is
+// wrapped by EnetHip.Checksum, which has exactly the reference signature:
+//     host->checksum = &EnetHip.Checksum;
+// The batch API (device-resident or host-memory batches, receive verify, gather
+// lists, multi-GPU shards) returns 0 or -hipError_t; the wrappers below turn a
+// negative code into EnetHipException.  The callback itself never fails and never
+// touches the GPU.
+//
+// No .NET toolchain exists in the build image, so this file is shipped as source
+// and is not compiled by the repository's build; its declarations mirror the
+// C header one to one (tests/test_library_cpu.py checks the header against the
+// exported symbols).
+
+using System;
+using System.Runtime.CompilerServices;
+using System.Runtime.InteropServices;
+using System.Security;
+
+namespace enet
+{
+    public sealed class EnetHipException : Exception
+    {
+        public int Code { get; }
+
+        public EnetHipException(string call, int code)
+            : base($"{call} failed: {code} ({Marshal.PtrToStringAnsi(EnetHipNative.enet_hip_error_string(code))})")
+        {
+            Code = code;
+        }
+    }
+
+    [SuppressUnmanagedCodeSecurity]
+    public static unsafe class EnetHipNative
+    {
+        private const string LIB = "enethip";
+
+        // ---- callback path (CPU) ----
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern uint enet_hip_crc32(ENetBuffer* buffers, nuint bufferCount);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern uint enet_hip_crc32_update(uint reg, void* data, nuint length);
+
+        // ---- context ----
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_device_count(int* count);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_context_create(int device, IntPtr* ctx);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_context_destroy(IntPtr ctx);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern IntPtr enet_hip_error_string(int code);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_set_tuning(IntPtr ctx, int lanesPerPacket, int workgroupsPerCu);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_set_kernel_path(IntPtr ctx, int path);
+
+        // ---- batches ----
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_crc32_batch_device(IntPtr ctx, byte* bytes, ulong* offsets, uint* lengths,
+                                                             nuint count, uint* output, IntPtr stream);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_crc32_batch_host(IntPtr ctx, byte* bytes, nuint byteCount, ulong* offsets,
+                                                           uint* lengths, nuint count, uint* output);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_verify_batch_device(IntPtr ctx, byte* bytes, ulong* offsets, uint* lengths,
+                                                              uint* slotOffsets, uint* connectIds, nuint count,
+                                                              byte* ok, uint* computed, IntPtr stream);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_crc32_gather_device(IntPtr ctx, byte* bytes, ulong* segOffsets,
+                                                              uint* segLengths, uint* segFirst, nuint dgramCount,
+                                                              uint* output, IntPtr stream);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_crc32_batch_multi(IntPtr* contexts, int contextCount, byte* bytes,
+                                                            nuint byteCount, ulong* offsets, uint* lengths,
+                                                            nuint count, uint* output);
+
+        // ---- memory helpers ----
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_device_alloc(IntPtr ctx, nuint bytes, void** output);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_device_free(IntPtr ctx, void* ptr);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_host_alloc(nuint bytes, void** output);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_host_free(void* ptr);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_memcpy_h2d(IntPtr ctx, void* dst, void* src, nuint bytes);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_memcpy_d2h(IntPtr ctx, void* dst, void* src, nuint bytes);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_synchronize(IntPtr ctx);
+    }
+
+    public static unsafe class EnetHip
+    {
+        /// <summary>
+        ///     Drop-in for ENet.enet_crc32 (c/packet.cs:142-160): <c>host->checksum = &amp;EnetHip.Checksum;</c>
+        ///     CPU, synchronous, bit-exact, never fails.
+        /// </summary>
+        [MethodImpl(MethodImplOptions.AggressiveInlining)]
+        public static uint Checksum(ENetBuffer* buffers, nuint bufferCount) => EnetHipNative.enet_hip_crc32(buffers, bufferCount);
+
+        internal static void Check(string call, int rc)
+        {
+            if (rc != 0)
+                throw new EnetHipException(call, rc);
+        }
+    }
+
+    /// <summary>One GPU: owns the library context (tables, stream, staging).</summary>
+    public sealed unsafe class EnetHipContext : IDisposable
+    {
+        public IntPtr Handle { get; private set; }
+
+        public EnetHipContext(int device = 0, int lanesPerPacket = 0)
+        {
+            IntPtr h;
+            EnetHip.Check("enet_hip_context_create", EnetHipNative.enet_hip_context_create(device, &h));
+            Handle = h;
+            if (lanesPerPacket != 0)
+                EnetHip.Check("enet_hip_set_tuning", EnetHipNative.enet_hip_set_tuning(h, lanesPerPacket, 0));
+        }
+
+        /// <summary>
+        ///     CRCs of packets bytes[offsets[i] .. +lengths[i]) from host memory (H2D, kernel, D2H; synchronous).
+        ///     Buffers from <see cref="PinnedBuffer{T}" /> run at full PCIe rate.
+        /// </summary>
+        public void BatchHost(ReadOnlySpan<byte> bytes, ReadOnlySpan<ulong> offsets, ReadOnlySpan<uint> lengths,
+                              Span<uint> output)
+        {
+            if (offsets.Length != lengths.Length || output.Length < offsets.Length)
+                throw new ArgumentException("offsets, lengths and output must have the same length");
+            fixed (byte* b = bytes)
+            fixed (ulong* o = offsets)
+            fixed (uint* l = lengths)
+            fixed (uint* r = output)
+                EnetHip.Check("enet_hip_crc32_batch_host",
+                    EnetHipNative.enet_hip_crc32_batch_host(Handle, b, (nuint)bytes.Length, o, l, (nuint)offsets.Length, r));
+        }
+
+        /// <summary>Device-resident batch (device pointers, async on <paramref name="stream" />).</summary>
+        public void BatchDevice(byte* bytes, ulong* offsets, uint* lengths, nuint count, uint* output, IntPtr stream = default)
+            => EnetHip.Check("enet_hip_crc32_batch_device",
+                EnetHipNative.enet_hip_crc32_batch_device(Handle, bytes, offsets, lengths, count, output, stream));
+
+        /// <summary>Batched receive verify (c/protocol.cs:1052-1068); ok[i] = 1 keeps DGRAM i.</summary>
+        public void VerifyDevice(byte* bytes, ulong* offsets, uint* lengths, uint* slotOffsets, uint* connectIds,
+                                 nuint count, byte* ok, uint* computed = null, IntPtr stream = default)
+            => EnetHip.Check("enet_hip_verify_batch_device",
+                EnetHipNative.enet_hip_verify_batch_device(Handle, bytes, offsets, lengths, slotOffsets, connectIds,
+                    count, ok, computed, stream));
+
+        public void Synchronize() => EnetHip.Check("enet_hip_synchronize", EnetHipNative.enet_hip_synchronize(Handle));
+
+        public void Dispose()
+        {
+            if (Handle != IntPtr.Zero)
+            {
+                EnetHipNative.enet_hip_context_destroy(Handle);
+                Handle = IntPtr.Zero;
+            }
+        }
+    }
+
+    /// <summary>Page-locked host memory for full-rate H2D/D2H.</summary>
+    public sealed unsafe class PinnedBuffer<T> : IDisposable where T : unmanaged
+    {
+        public T* Pointer { get; private set; }
+        public int Length { get; }
+
+        public PinnedBuffer(int length)
+        {
+            void* p;
+            EnetHip.Check("enet_hip_host_alloc", EnetHipNative.enet_hip_host_alloc((nuint)(length * sizeof(T)), &p));
+            Pointer = (T*)p;
+            Length = length;
+        }
+
+        public Span<T> Span => new Span<T>(Pointer, Length);
+
+        public void Dispose()
+        {
+            if (Pointer != null)
+            {
+                EnetHipNative.enet_hip_host_free(Pointer);
+                Pointer = null;
+            }
+        }
+    }
+}

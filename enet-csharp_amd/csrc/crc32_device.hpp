@@ -15,7 +15,7 @@
 // lanes 0-31 and 32-63 served as separate groups): no conflicts whatever the
 // data (tests/test_kernel_model.py proves it).  The 32 dwords per row no table
 // uses (columns 2c+1 for c < 16, 2c for c >= 16) hold byte-indexed tables:
-// INIT[], CINV[] and the stream kernel's butterfly constants.  The
+// INIT[] and CINV[].  The
 // per-lane byte order costs one dword permutation per block (two bitop3 rounds +
 // a half swap).
 #pragma once
@@ -35,7 +35,6 @@ constexpr int kCinvEntries = 512;
 // the row, i.e. by a byte value: one v_perm + ds_read per lookup.
 __host__ __device__ constexpr uint32_t col_byte(uint32_t t) { return 8u * t + 4u * (t >> 4); }
 __host__ __device__ constexpr uint32_t free_col(uint32_t c) { return 4u * (c < 16u ? 2u * c + 1u : 2u * c); }
-constexpr uint32_t kLevelCol = 0;   // columns 4l + b: butterfly level l (x^(-256 * 2^l)), register byte b
 constexpr uint32_t kInitCol = 16;   // INIT[r], rows 0..31
 constexpr uint32_t kCinvCol = 17;   // CINV[n] = x^(-8n), n < 512: row n & 255 of column 17 + (n >> 8)
 __host__ __device__ constexpr uint32_t init_addr(uint32_t r) { return 256u * r + free_col(kInitCol); }
@@ -55,6 +54,7 @@ struct KernelTables {
     const uint32_t* xn_lo;  // x^(8n) mod P, n < 65536
     const uint32_t* xn_hi;  // x^(8*65536*q) mod P, q < 65536
     const uint32_t* init;   // INIT[r], r < 32
+    const uint8_t* zero;    // 256 zero bytes: DMA source of pieces wholly outside a packet
 };
 
 // ------------------------------------------------------------------ device helpers
@@ -186,6 +186,39 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) v = max(v, static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), m)));
     return v;
+}
+
+// Cross-lane moves on the DPP network (VALU, no LDS traffic -- ds_bpermute based
+// shuffles cost LDS cycles and bank-conflict cycles on gfx950).
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), CTRL, 0xF, 0xF, true));
+}
+constexpr int kDppQuadXor1 = 0xB1;       // quad_perm [1,0,3,2]
+constexpr int kDppQuadXor2 = 0x4E;       // quad_perm [2,3,0,1]
+constexpr int kDppRowHalfMirror = 0x141;
+constexpr int kDppRowMirror = 0x140;
+constexpr int kDppRowShl = 0x100;        // + n: lane i reads lane i+n of its row (0 past the row end)
+
+// Wave-uniform max / min of a per-lane value: DPP within each 16-lane row, then
+// four v_readlane and scalar ops.
+__device__ __forceinline__ uint32_t wave_max_u(uint32_t v) {
+    v = max(v, dpp<kDppQuadXor1>(v));
+    v = max(v, dpp<kDppQuadXor2>(v));
+    v = max(v, dpp<kDppRowHalfMirror>(v));
+    v = max(v, dpp<kDppRowMirror>(v));
+    const uint32_t a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
+    const uint32_t c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+    return max(max(a, b), max(c, d));
+}
+__device__ __forceinline__ uint32_t wave_min_u(uint32_t v) {
+    v = min(v, dpp<kDppQuadXor1>(v));
+    v = min(v, dpp<kDppQuadXor2>(v));
+    v = min(v, dpp<kDppRowHalfMirror>(v));
+    v = min(v, dpp<kDppRowMirror>(v));
+    const uint32_t a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
+    const uint32_t c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+    return min(min(a, b), min(c, d));
 }
 
 // Register after feeding the segment [sp, sp+len) from `reg`, with every block

@@ -66,17 +66,17 @@ __device__ __forceinline__ u32x4 lds_load16(uint32_t addr) { return *reinterpret
 //   * window: NB whole 32-byte blocks ending at the packet end when that is
 //     16-byte aligned (lz = 32*NB - L zero bytes in front, tz = 0), else starting
 //     at the 16-byte granule holding a (lz = a & 15, tz = 32*NB - lz - L zero
-//     bytes behind).  Head and tail bytes are zeroed after loading; a 16-byte
-//     piece wholly outside the packet is never read (memory-safe at page ends);
+//     bytes behind).  A 16-byte piece wholly outside the packet is read from a
+//     zero buffer instead (memory-safe at page ends, and no masking); only the
+//     partial head/tail pieces of unaligned packets get byte masks;
 //   * lane k folds the window blocks w with (w + r) % P == k, r = (-NB) % P,
 //     using the ADVANCING tables T'_t = T_{t+32(P-1)} of this P: each fold also
 //     skips the P-1 blocks the other lanes own, so the P lanes of a packet walk
 //     it front to back together and one stage of a packet is ONE contiguous
 //     P*SB*32-byte chunk.  The rotation r makes lane k end exactly 32k bytes
 //     past the window end; the block-0 lane (k == r) starts at INIT[lz];
-//   * finish: a log2(P)-level butterfly, lane k ^= adv_{-32m}(lane k+m), each
-//     constant advance = 4 byte-indexed LDS lookups (free image columns); then
-//     x^(-8 tz) for START-aligned windows.
+//   * finish: lane k multiplies by CINV[32k + tz] = x^(-8(32k + tz)) (a byte-
+//     indexed free column of the image), then the P registers are XORed (DPP).
 // No x^(8n) gathers and no alignment precondition.  Verify mode substitutes the
 // slot bytes by connectID inside the block that holds them (protocol.cs:1052-1068)
 // and collects the original bytes as `desired`.  tests/kernel_model.py restates
@@ -135,11 +135,6 @@ __device__ __forceinline__ void dma4(const void* g, uint32_t lds_addr) {
                                             static_cast<uintptr_t>(lds_addr)), 4, 0, 0);
 }
 
-// XOR-butterfly partner within 32 lanes (ds_swizzle bitmask mode, no LDS access).
-template <int M>
-__device__ __forceinline__ uint32_t swz_xor(uint32_t v) {
-    return static_cast<uint32_t>(__builtin_amdgcn_ds_swizzle(static_cast<int>(v), 0x1F | (M << 10)));
-}
 
 // Lane c's run sits at buf + kRun*c, its 16-byte piece p in slot p ^ swz(c):
 // swz(c) = ((c >> log2(16/R)) & (R-1)) ^ ((c >> 4) & 1), R = pieces per run,
@@ -208,21 +203,23 @@ __device__ __forceinline__ Window packet_window(const PacketArgs& pa, uint32_t s
 }
 
 // Producer side of a group: per DMA slot i, the address of this lane's 16-byte
-// piece at the group's next stage, the address used once the piece runs past its
-// last in-range block, how many stages stay in range, and the stage-0 bump that
-// skips a head piece lying wholly in front of the packet.
+// piece at the group's next stage and how many stages it holds packet bytes;
+// past that, and for a head piece lying wholly in front of the packet, the
+// piece is read from the zero buffer (so whole-piece head/tail zeroing is free).
 template <class G>
 struct Producer {
-    uint64_t cur[G::kDma], lim[G::kDma];
-    uint32_t nval[G::kDma], hfix[G::kDma];
+    uint64_t cur[G::kDma];
+    uint32_t nval[G::kDma];
+    uint32_t head;       // bit i: piece i is a wholly-outside head piece at stage 0
     uint32_t stages;
 };
 
 template <class G>
 __device__ __forceinline__ void producer_setup(Producer<G>& pr, const PacketArgs& pa, uint32_t slot, uint32_t lg,
-                                               uint64_t pk0, uint32_t lane, const uint8_t* safe) {
+                                               uint64_t pk0, uint32_t lane) {
     const uint32_t P = 1u << lg;
     uint32_t most = 0;
+    pr.head = 0;
 #pragma unroll
     for (int i = 0; i < G::kDma; ++i) {
         const uint32_t c = G::kRunsPerDma * i + lane / G::kPieces;    // run (task lane) of this piece
@@ -234,16 +231,11 @@ __device__ __forceinline__ void producer_setup(Producer<G>& pr, const PacketArgs
         const int32_t lastw = static_cast<int32_t>(w.nb) - ((h && w.tz >= 16u) ? 2 : 1);
         const bool any = static_cast<int32_t>(w0) <= lastw;
         pr.nval[i] = any ? ((static_cast<uint32_t>(lastw) - w0) >> (lg + G::kLsb)) + 1u : 0u;
-        pr.hfix[i] = (w0 == 0 && h == 0 && w.lz >= 16u) ? 16u : 0u;
-        pr.cur[i] = w.ws + 32ull * w0 + 16u * h + pr.hfix[i];
-        // in-range piece of the last block: its h-half unless that half is all tail
-        // (or, for a one-block window, all head)
-        uint32_t hl = (h && w.tz < 16u) ? 1u : 0u;
-        if (w.nb == 1 && w.lz >= 16u) hl = 1u;
-        pr.lim[i] = w.nb ? w.ws + 32ull * (w.nb - 1u) + 16u * hl : reinterpret_cast<uint64_t>(safe);
+        if (w0 == 0 && h == 0 && w.lz >= 16u) pr.head |= 1u << i;
+        pr.cur[i] = w.ws + 32ull * w0 + 16u * h;
         most = max(most, pr.nval[i]);
     }
-    pr.stages = __builtin_amdgcn_readfirstlane(wave_max(most));
+    pr.stages = wave_max_u(most);
 }
 
 // Consumer side: this lane's task of the group.
@@ -273,8 +265,9 @@ __device__ __forceinline__ Task consumer_setup(const PacketArgs& pa, uint32_t sl
     t.tz = w.tz;
     t.cnt = t.w0 < w.nb ? ((w.nb - 1u - t.w0) >> lg) + 1u : 0u;
     t.reg = t.k == w.r ? lds_load(init_addr(w.lz)) : 0u;
-    t.e0 = (w.lz && t.w0 == 0 && w.nb) ? 0u : ~0u;
-    t.e1 = (w.tz && t.cnt && t.w0 + P * (t.cnt - 1u) == w.nb - 1u) ? t.cnt - 1u : ~0u;
+    // partial head / tail pieces need byte masks (whole ones come from the zero buffer)
+    t.e0 = ((w.lz & 15u) && t.w0 == 0 && w.nb) ? 0u : ~0u;
+    t.e1 = ((w.tz & 15u) && t.cnt && t.w0 + P * (t.cnt - 1u) == w.nb - 1u) ? t.cnt - 1u : ~0u;
     t.e2 = t.e3 = ~0u;
     t.ps = -4096;
     t.connect = 0;
@@ -303,9 +296,7 @@ __device__ __forceinline__ uint32_t next_edge_stage(const Task& t, uint32_t from
         const uint32_t st = e[i] == ~0u ? ~0u : e[i] >> G::kLsb;
         if (st >= from) m = min(m, st);
     }
-#pragma unroll
-    for (int s = 32; s >= 1; s >>= 1) m = min(m, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), s)));
-    return __builtin_amdgcn_readfirstlane(m);
+    return wave_min_u(m);
 }
 
 // Keep bytes [lo, hi) of dword q (bytes 4q .. 4q+3 of the block).
@@ -355,27 +346,21 @@ __device__ __forceinline__ void edge_fix(u32x4& A, u32x4& B, uint32_t hs, const 
     B = sw ? n0 : n1;
 }
 
-// adv by -32*2^lvl bytes: four byte-indexed lookups in free image columns.
+// XOR of the P registers of each packet into its lane k == 0 (DPP tree inside a
+// 16-lane row: lane k takes lane k + 2^l at level l).
 template <int LVL>
-__device__ __forceinline__ uint32_t level_apply(uint32_t v) {
-    uint32_t x[4];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        const uint32_t addr = __builtin_amdgcn_perm(v, free_col(kLevelCol + 4 * LVL + b),
-                                                    0x0C0C0000u | ((4u + b) << 8));
-        x[b] = lds_load(addr);
+__device__ __forceinline__ uint32_t xor_lanes(uint32_t lg, uint32_t v) {
+    if constexpr (LVL < 4) {
+        if (LVL < static_cast<int>(lg)) return xor_lanes<LVL + 1>(lg, v ^ dpp<kDppRowShl + (1 << LVL)>(v));
     }
-    return xor3(x[0], x[1], x[2]) ^ x[3];
+    return v;
 }
 
-template <int LVL>
-__device__ __forceinline__ void butterfly(uint32_t lg, uint32_t& reg, uint32_t& desired, bool verify) {
-    if constexpr (LVL < 4) {
-        if (LVL < static_cast<int>(lg)) {
-            reg ^= level_apply<LVL>(swz_xor<(1 << LVL)>(reg));
-            if (verify) desired |= swz_xor<(1 << LVL)>(desired);
-            butterfly<LVL + 1>(lg, reg, desired, verify);
-        }
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
     }
 }
 
@@ -402,7 +387,7 @@ __global__ void __launch_bounds__(G::kThreads) crc32_stream_kernel(PacketArgs pa
     const uint32_t J = wv < ngroups ? static_cast<uint32_t>((ngroups - 1u - wv) / wt) + 1u : 0u;
     const uint32_t ring = kLdsTableBytes + wave * G::kWaveLds;
     const uint32_t meta = ring + G::kNB * G::kStage;
-    const uint8_t* safe = reinterpret_cast<const uint8_t*>(tb.xn_lo);
+    const uint64_t zero = reinterpret_cast<uint64_t>(tb.zero);
     const uint64_t stepB = 32ull * P * G::kSB;                          // bytes per stage per piece
     auto group_pk0 = [&](uint32_t j) __attribute__((always_inline)) -> uint64_t { return (wv + static_cast<uint64_t>(j) * wt) << gsh; };
     auto meta_slot = [&](uint32_t j) __attribute__((always_inline)) -> uint32_t { return meta + (j % G::kMetaSlots) * G::kMetaSlot; };
@@ -449,16 +434,14 @@ __global__ void __launch_bounds__(G::kThreads) crc32_stream_kernel(PacketArgs pa
 
     auto produce = [&](uint32_t slotc) __attribute__((always_inline)) {
         const uint32_t buf = ring + slotc * G::kStage;
-#pragma unroll
-        for (int i = 0; i < G::kDma; ++i) {
-            const uint64_t g = pst < pr.nval[i] ? pr.cur[i] : pr.lim[i];
+        const uint32_t skip = pst == 0 ? pr.head : 0u;                   // wave-uniform
+        static_for<0, G::kDma>([&](auto ic) __attribute__((always_inline)) {
+            constexpr int i = decltype(ic)::value;
+            const bool in = pst < pr.nval[i] && !((skip >> i) & 1u);
+            const uint64_t g = in ? pr.cur[i] : zero;
             if (ABL != 2) dma16(reinterpret_cast<const void*>(g), buf + 1024u * i);
             pr.cur[i] += stepB;
-        }
-        if (pst == 0) {
-#pragma unroll
-            for (int i = 0; i < G::kDma; ++i) pr.cur[i] -= pr.hfix[i];
-        }
+        });
         if (ABL != 2) ops += G::kDma;
         marks |= static_cast<uint64_t>(ops & 0xFFFFu) << (16u * nfl);
         ++nfl;
@@ -468,7 +451,7 @@ __global__ void __launch_bounds__(G::kThreads) crc32_stream_kernel(PacketArgs pa
                 wait_vm((ops - static_cast<uint32_t>(mmarks)) & 0xFFFFu);   // metadata of group pj
                 mmarks >>= 16;
                 --nmm;
-                producer_setup<G>(pr, pa, meta_slot(pj), lg, group_pk0(pj), lane, safe);
+                producer_setup<G>(pr, pa, meta_slot(pj), lg, group_pk0(pj), lane);
                 fetch_meta(pj + G::kMetaAhead);
             } else {
                 pdone = true;
@@ -478,7 +461,7 @@ __global__ void __launch_bounds__(G::kThreads) crc32_stream_kernel(PacketArgs pa
 
     if (J) {
         wait_vm(ops - m_first);
-        producer_setup<G>(pr, pa, meta_slot(0), lg, group_pk0(0), lane, safe);
+        producer_setup<G>(pr, pa, meta_slot(0), lg, group_pk0(0), lane);
 #pragma unroll
         for (uint32_t d = 1; d <= G::kMetaAhead; ++d) fetch_meta(d);
         unroll_slots<G::kNB - 1>([&](auto sc) __attribute__((always_inline)) {
@@ -503,7 +486,7 @@ __global__ void __launch_bounds__(G::kThreads) crc32_stream_kernel(PacketArgs pa
 
     uint32_t cj = 0, cst = 0;
     Task t = consumer_setup<MODE>(pa, meta_slot(0), lg, group_pk0(0), lane);
-    uint32_t cstages = __builtin_amdgcn_readfirstlane(wave_max((t.cnt + G::kSB - 1u) >> G::kLsb));
+    uint32_t cstages = wave_max_u((t.cnt + G::kSB - 1u) >> G::kLsb);
     uint32_t nedge = next_edge_stage<G>(t, 0);
     uint32_t reg = t.reg, desired = 0;
     bool done = false;
@@ -535,9 +518,11 @@ __global__ void __launch_bounds__(G::kThreads) crc32_stream_kernel(PacketArgs pa
         marks >>= 16;
         --nfl;
         if (++cst == cstages) {
-            // finish the group: butterfly over the P lanes, then the tail correction
-            butterfly<0>(lg, reg, desired, MODE != 0);
-            if (t.k == 0 && t.tz) reg = mulmod(reg, lds_load(cinv_addr(t.tz)));
+            // finish the group: lane k sits 32k + tz bytes past the data end --
+            // undo that by x^(-8n), then XOR the P lanes
+            reg = mulmod(reg, lds_load(cinv_addr(32u * t.k + t.tz)));
+            reg = xor_lanes<0>(lg, reg);
+            if (MODE) desired = xor_lanes<0>(lg, desired);
             if (t.active && t.k == 0) {
                 if (MODE == 0) {
                     pa.out[t.pk] = finalize(reg);                        // packet.cs:159
@@ -552,7 +537,7 @@ __global__ void __launch_bounds__(G::kThreads) crc32_stream_kernel(PacketArgs pa
                 return;
             }
             t = consumer_setup<MODE>(pa, meta_slot(cj), lg, group_pk0(cj), lane);
-            cstages = __builtin_amdgcn_readfirstlane(wave_max((t.cnt + G::kSB - 1u) >> G::kLsb));
+            cstages = wave_max_u((t.cnt + G::kSB - 1u) >> G::kLsb);
             nedge = next_edge_stage<G>(t, 0);
             reg = t.reg;
             desired = 0;
@@ -716,6 +701,7 @@ struct enet_hip_context {
     uint32_t* d_image = nullptr;
     uint32_t* d_xn = nullptr;    // lo[65536] | hi[65536]
     uint32_t* d_init = nullptr;  // 32
+    uint8_t* d_zero = nullptr;   // 256 zero bytes
     int lanes_per_packet = 0;    // 0 = auto
     int wgs_per_cu = 0;          // 0 = auto (direct / gather kernels)
     int path = 0;                // 0 = stream (default geometry), 1 = direct, 2+k = stream geometry k
@@ -774,12 +760,6 @@ struct HostTables {
                 for (uint32_t j = 0; j < 256; ++j) img[(j * 256 + col_byte(t)) / 4] = row[j];
                 for (uint32_t j = 0; j < 256; ++j) row[j] = sarwate_step(row[j], 0);
             }
-            for (uint32_t lvl = 0; lvl < 4; ++lvl) {
-                const uint32_t c = cinv[32u << lvl];                   // x^(-8 * 32 * 2^lvl)
-                for (uint32_t b = 0; b < 4; ++b)
-                    for (uint32_t v = 0; v < 256; ++v)
-                        img[(256u * v + free_col(kLevelCol + 4 * lvl + b)) / 4] = gf2_mulmod(v << (8 * b), c);
-            }
             for (uint32_t r = 0; r < 32; ++r) img[init_addr(r) / 4] = init[r];
             for (uint32_t i = 0; i < static_cast<uint32_t>(kCinvEntries); ++i) img[cinv_addr(i) / 4] = cinv[i];
         }
@@ -806,7 +786,7 @@ int log2i(int v) {
 }
 
 KernelTables tables_of(const enet_hip_context* ctx) {
-    return KernelTables{ctx->d_image, ctx->d_xn, ctx->d_xn + kXnEntries, ctx->d_init};
+    return KernelTables{ctx->d_image, ctx->d_xn, ctx->d_xn + kXnEntries, ctx->d_init, ctx->d_zero};
 }
 
 unsigned grid_for(const enet_hip_context* ctx, uint64_t tasks) {
@@ -941,6 +921,8 @@ int enet_hip_context_create(int device, enet_hip_context** out) {
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_image), ht.image.size() * 4)))) break;
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_xn), ht.xn.size() * 4)))) break;
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_init), 32 * 4)))) break;
+        if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_zero), 256)))) break;
+        if ((rc = herr(hipMemset(ctx->d_zero, 0, 256)))) break;
         if ((rc = herr(hipMemcpy(ctx->d_image, ht.image.data(), ht.image.size() * 4, hipMemcpyHostToDevice)))) break;
         if ((rc = herr(hipMemcpy(ctx->d_xn, ht.xn.data(), ht.xn.size() * 4, hipMemcpyHostToDevice)))) break;
         if ((rc = herr(hipMemcpy(ctx->d_init, ht.init.data(), 32 * 4, hipMemcpyHostToDevice)))) break;
@@ -967,6 +949,7 @@ int enet_hip_context_destroy(enet_hip_context* ctx) {
     (void)hipFree(ctx->d_image);
     (void)hipFree(ctx->d_xn);
     (void)hipFree(ctx->d_init);
+    (void)hipFree(ctx->d_zero);
     (void)hipFree(ctx->d_bytes);
     (void)hipFree(ctx->d_meta);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

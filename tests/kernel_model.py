@@ -1,17 +1,18 @@
 """Host-side model of the gfx950 kernels' arithmetic (test infrastructure).
 
 Restates, in Python integers, what crc32_kernels.hip does per lane -- the 64 KiB
-LDS image (slicing tables + INIT/CINV in the free dwords), the per-lane v_perm
+LDS image (slicing tables + INIT/CINV in the free columns), the per-lane v_perm
 selectors and column bytes, the dword swaps, slicing-by-32 folding, and the two
 ways a packet is spread over P lanes:
 
   * stream kernel (crc32_stream_kernel): STRIDED blocks.  The packet's window
-    starts at the 16-byte granule holding its first byte; lane k folds window
-    blocks k, k+P, k+2P, ... with the advancing tables T'_t = T_{t+32(P-1)}, so
+    is END-aligned (packet end 16-byte aligned) or starts at the 16-byte granule
+    holding its first byte; lane k folds every P-th window block with the advancing
+    tables T'_t = T_{t+32(P-1)}, so
     after each block its register has also skipped the P-1 blocks the other
-    lanes own.  Head (lz) and tail (tz) bytes are zeroed, and each lane's
-    overshoot past the data end (32*o_k + tz bytes) is undone by one GF(2)
-    multiply by x^(-8n) (CINV table).
+    lanes own.  Head (lz) and tail (tz) bytes are zeroed; the assignment is
+    rotated so that lane k ends exactly 32k + tz bytes past the data end, undone
+    by one GF(2) multiply by x^(-8n) (CINV table) before the XOR over the lanes.
   * direct kernel (crc32_direct_kernel / gather): CONTIGUOUS segments cut at
     128-byte-aligned addresses, END-aligned windows started at INIT[rp], and the
     classic carry-combine reg(A||B) = reg(A) * x^(8|B|) ^ reg(B).
@@ -128,7 +129,6 @@ def free_col(c: int) -> int:
 
 # Free columns are 256-entry tables indexed by the row (a byte value), so a
 # lookup is one v_perm (byte -> address byte 1, column -> byte 0) + ds_read.
-KLEVEL_COL = 0            # columns 0..15: butterfly tables, level l (m = 2^l), byte b -> column 4l + b
 KINIT_COL = 16            # INIT[r], r < 32 (rows 0..31)
 KCINV_COL = 17            # CINV[n], n < 512: rows n & 255 of columns 17 + (n >> 8)
 
@@ -141,23 +141,14 @@ def cinv_addr(n: int) -> int:
     return 256 * (n & 255) + free_col(KCINV_COL + (n >> 8))
 
 
-def level_addr(lvl: int, b: int, v: int) -> int:
-    return 256 * v + free_col(KLEVEL_COL + 4 * lvl + b)
-
-
 def lds_image(P: int = 1) -> list[int]:
     """dword 64*j + 2t + (t>>4) = T'_t[j] = T_{t + 32(P-1)}[j]; free columns hold
-    the butterfly tables, INIT and CINV."""
+    INIT and CINV."""
     T = slicing_tables(32, 32 * (P - 1))
     img = [0] * (256 * 64)
     for j in range(256):
         for t in range(32):
             img[64 * j + col_byte(t) // 4] = T[t][j]
-    for lvl in range(4):
-        c = CINV[32 << lvl]                       # x^(-8 * 32m), m = 2^lvl
-        for b in range(4):
-            for v in range(256):
-                img[level_addr(lvl, b, v) // 4] = mulmod(v << (8 * b), c)
     for r in range(32):
         img[init_addr(r) // 4] = INIT[r]
     for n in range(512):
@@ -172,14 +163,6 @@ def image(P: int = 1) -> list[int]:
     if P not in _IMG_CACHE:
         _IMG_CACHE[P] = lds_image(P)
     return _IMG_CACHE[P]
-
-
-def level_apply(img: list[int], lvl: int, v: int) -> int:
-    """adv by -32*2^lvl bytes via four column lookups (the kernel's butterfly step)."""
-    out = 0
-    for b in range(4):
-        out ^= img[level_addr(lvl, b, (v >> (8 * b)) & 0xFF) // 4]
-    return out
 
 
 def v_perm(s0: int, s1: int, sel: int) -> int:
@@ -295,14 +278,9 @@ def stream_packet(pkt: bytes, P: int, addr: int = 0, lane_base: int = 0,
         if blocks:
             assert blocks[-1] + P - nb == k        # overshoot is exactly k blocks
         regs.append(reg)
-    m, lvl = 1, 0
-    while m < P:                                   # butterfly: lane k += adv_{-32m}(lane k+m)
-        for k in range(0, P, 2 * m):
-            regs[k] ^= level_apply(img, lvl, regs[k + m])
-        m, lvl = 2 * m, lvl + 1
-    total = regs[0]
-    if tz:
-        total = mulmod(total, CINV[tz])
+    total = 0
+    for k in range(P):                             # lane k sits 32k + tz bytes past the data end
+        total ^= mulmod(regs[k], img[cinv_addr(32 * k + tz) // 4])
     return total, desired
 
 

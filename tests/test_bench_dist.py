@@ -1,0 +1,91 @@
+"""bench.py's multi-rank harness on CPU (gloo, world_size 2): the barrier +
+max-over-ranks timing, the whole-job value and rank-0-only output, with a fake
+engine standing in for the GPU (the -m gpu tests and the driver's runs cover the
+real engine).  SURVEY.md §8e: shards are independent, no data-path collective."""
+import json
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+
+class FakeEngine:
+    """Answers like GpuEngine; CRCs come from the oracle (test infrastructure only)."""
+
+    def __init__(self, device, batches, lanes, wgs):
+        import oracle
+        self.batches = batches
+        self.lib = oracle.OracleLib()
+        self.steps = 0
+
+    def step(self, i):
+        self.steps += 1
+
+    def probe(self, i):
+        pass
+
+    def sync(self):
+        pass
+
+    def kernel_ms(self, fn, steps):
+        return 0.02, 0.022
+
+    def outputs(self, j):
+        b = self.batches[j]
+        return self.lib.batch(b.payload, b.off, b.lens, threads=2)
+
+
+def fake_cpu(batch, budget):
+    one = {"gibps": 0.5, "threads": 1, "packets": batch.n, "reps": 1}
+    return {"1thread": one, "all": dict(one, gibps=2.0, threads=2)}
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank(rank, ws, port, q):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(ws),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import io
+    import contextlib
+    import bench
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        bench.main(["--config", "small", "--rotate", "2", "--steps", "6", "--warmup", "1", "--gpus", str(ws)],
+                   engine_factory=FakeEngine, cpu_factory=fake_cpu)
+    q.put((rank, buf.getvalue()))
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gloo_harness():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    outs = dict(q.get(timeout=240) for _ in ps)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    assert outs[1].strip() == ""                       # only rank 0 prints
+    lines = [l for l in outs[0].splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 6 and d["scaling"] == "weak"
+    assert d["unit"] == "GiB/s" and d["higher_is_better"] is True and d["dtype"] == "u8"
+    # whole-job value: both ranks' bytes over the max-over-ranks span
+    per_rank = 6 * 2048 * 1200
+    assert d["value"] == pytest.approx(2 * per_rank / (d["ms_per_step"] * 6e-3) / 2**30, rel=0.02)
+    assert d["roofline"]["bound"] == "hbm" and d["roofline"]["peak"] == 8000.0
+    assert d["cpu_baseline"]["cores"] == 2 and d["cpu_baseline"]["kind"] == "port"
