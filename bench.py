@@ -219,6 +219,10 @@ def make_batches(cfg: str, rotate: int, rank: int):
             out.append(workloads.fixed(65536, 1200, seed=seed, name="cfg2"))
         elif cfg == "small":
             out.append(workloads.fixed(2048, 1200, seed=seed, name="small"))
+        elif cfg.startswith("fixed:"):                 # tools only: fixed:<packets>[:<bytes>]
+            parts = cfg.split(":")
+            out.append(workloads.fixed(int(parts[1]), int(parts[2]) if len(parts) > 2 else 1200, seed=seed,
+                                       name=cfg))
         else:
             out.append(workloads.mixed(262144, 64, 1400, seed=seed, name="cfg3"))
     return out

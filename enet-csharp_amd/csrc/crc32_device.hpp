@@ -15,7 +15,7 @@
 // lanes 0-31 and 32-63 served as separate groups): no conflicts whatever the
 // data (tests/test_kernel_model.py proves it).  The 32 dwords per row no table
 // uses (columns 2c+1 for c < 16, 2c for c >= 16) hold byte-indexed tables:
-// INIT[] and CINV[].  The
+// the per-lane overshoot corrections, INIT[] and CINV[].  The
 // per-lane byte order costs one dword permutation per block (two bitop3 rounds +
 // a half swap).
 #pragma once
@@ -35,10 +35,13 @@ constexpr int kCinvEntries = 512;
 // the row, i.e. by a byte value: one v_perm + ds_read per lookup.
 __host__ __device__ constexpr uint32_t col_byte(uint32_t t) { return 8u * t + 4u * (t >> 4); }
 __host__ __device__ constexpr uint32_t free_col(uint32_t c) { return 4u * (c < 16u ? 2u * c + 1u : 2u * c); }
-constexpr uint32_t kInitCol = 16;   // INIT[r], rows 0..31
-constexpr uint32_t kCinvCol = 17;   // CINV[n] = x^(-8n), n < 512: row n & 255 of column 17 + (n >> 8)
+constexpr uint32_t kCorrCol = 0;    // columns 4(k-1) + b, k = 1..7: (byte b of r) * x^(-256k)
+constexpr uint32_t kCorrLanes = 8;  // lanes-per-packet values whose corrections are tabled
+constexpr uint32_t kInitCol = 29;   // INIT[r], rows 0..31
+constexpr uint32_t kCinvCol = 30;   // CINV[n] = x^(-8n), n < 512: row n & 255 of column 30 + (n >> 8)
 __host__ __device__ constexpr uint32_t init_addr(uint32_t r) { return 256u * r + free_col(kInitCol); }
 __host__ __device__ constexpr uint32_t cinv_addr(uint32_t n) { return 256u * (n & 255u) + free_col(kCinvCol + (n >> 8)); }
+__host__ __device__ constexpr uint32_t corr_col(uint32_t k, uint32_t b) { return free_col(kCorrCol + 4u * (k - 1u) + b); }
 constexpr int kXnEntries = 65536;                  // x^(8n) for n < 65536 (+ high part)
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));

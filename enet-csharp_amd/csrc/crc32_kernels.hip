@@ -63,20 +63,20 @@ __device__ __forceinline__ u32x4 lds_load16(uint32_t addr) { return *reinterpret
 // One persistent workgroup of W waves per CU.  A wave owns groups g = wv,
 // wv + W*grid, ...; a group is 64 consecutive tasks = 64/P packets, P = 2^lg
 // (4, 8 or 16) lanes per packet.  Per packet (crc32 of bytes [a, a+L)):
-//   * window: NB whole 32-byte blocks ending at the packet end when that is
-//     16-byte aligned (lz = 32*NB - L zero bytes in front, tz = 0), else starting
-//     at the 16-byte granule holding a (lz = a & 15, tz = 32*NB - lz - L zero
-//     bytes behind).  A 16-byte piece wholly outside the packet is read from a
-//     zero buffer instead (memory-safe at page ends, and no masking); only the
-//     partial head/tail pieces of unaligned packets get byte masks;
+//   * window: NB whole 32-byte blocks ending at the 16-byte granule boundary at
+//     or after the packet end (tz < 16 zero bytes behind, lz < 32 in front).  A
+//     16-byte piece wholly in front of the packet is read from a zero buffer
+//     (memory-safe at page ends, no masking); only partial head/tail pieces of
+//     unaligned packets get byte masks;
 //   * lane k folds the window blocks w with (w + r) % P == k, r = (-NB) % P,
 //     using the ADVANCING tables T'_t = T_{t+32(P-1)} of this P: each fold also
 //     skips the P-1 blocks the other lanes own, so the P lanes of a packet walk
 //     it front to back together and one stage of a packet is ONE contiguous
 //     P*SB*32-byte chunk.  The rotation r makes lane k end exactly 32k bytes
 //     past the window end; the block-0 lane (k == r) starts at INIT[lz];
-//   * finish: lane k multiplies by CINV[32k + tz] = x^(-8(32k + tz)) (a byte-
-//     indexed free column of the image), then the P registers are XORed (DPP).
+//   * finish: lane k undoes its 32k-byte overshoot by x^(-256k) = four byte-
+//     indexed lookups in the image's correction columns, the P registers are
+//     XORed (DPP), then x^(-8 tz) for packets whose end is not 16-byte aligned.
 // No x^(8n) gathers and no alignment precondition.  Verify mode substitutes the
 // slot bytes by connectID inside the block that holds them (protocol.cs:1052-1068)
 // and collects the original bytes as `desired`.  tests/kernel_model.py restates
@@ -184,20 +184,11 @@ __device__ __forceinline__ Window packet_window(const PacketArgs& pa, uint32_t s
     const uint64_t off = static_cast<uint64_t>(meta_field(slot, lg, 1, j)) |
                          (static_cast<uint64_t>(meta_field(slot, lg, 2, j)) << 32);
     const uint64_t a = reinterpret_cast<uint64_t>(pa.bytes) + off, e = a + w.L;
-    if (w.L == 0) {
-        w.lz = w.nb = w.tz = 0;
-        w.ws = a;
-    } else if ((e & 15u) == 0) {                      // END-aligned
-        w.nb = (w.L + 31u) >> 5;
-        w.lz = 32u * w.nb - w.L;
-        w.tz = 0;
-        w.ws = e - 32ull * w.nb;
-    } else {                                          // START-aligned
-        w.lz = static_cast<uint32_t>(a & 15u);
-        w.nb = (w.lz + w.L + 31u) >> 5;
-        w.tz = 32u * w.nb - w.lz - w.L;
-        w.ws = a - w.lz;
-    }
+    // the window ends at the granule boundary at or after the packet end
+    w.tz = w.L ? static_cast<uint32_t>((0u - e) & 15u) : 0u;
+    w.nb = w.L ? (w.L + w.tz + 31u) >> 5 : 0u;
+    w.lz = 32u * w.nb - w.tz - w.L;
+    w.ws = e + w.tz - 32ull * w.nb;
     w.r = (0u - w.nb) & ((1u << lg) - 1u);
     return w;
 }
@@ -227,10 +218,8 @@ __device__ __forceinline__ void producer_setup(Producer<G>& pr, const PacketArgs
         const uint32_t b = p >> 1, h = p & 1u;
         const Window w = packet_window(pa, slot, lg, pk0, c >> lg);
         const uint32_t w0 = ((c - w.r) & (P - 1u)) + P * b;            // block of this piece at stage 0
-        // last block whose h-half holds packet bytes
-        const int32_t lastw = static_cast<int32_t>(w.nb) - ((h && w.tz >= 16u) ? 2 : 1);
-        const bool any = static_cast<int32_t>(w0) <= lastw;
-        pr.nval[i] = any ? ((static_cast<uint32_t>(lastw) - w0) >> (lg + G::kLsb)) + 1u : 0u;
+        (void)h;
+        pr.nval[i] = w0 < w.nb ? ((w.nb - 1u - w0) >> (lg + G::kLsb)) + 1u : 0u;
         if (w0 == 0 && h == 0 && w.lz >= 16u) pr.head |= 1u << i;
         pr.cur[i] = w.ws + 32ull * w0 + 16u * h;
         most = max(most, pr.nval[i]);
@@ -267,7 +256,7 @@ __device__ __forceinline__ Task consumer_setup(const PacketArgs& pa, uint32_t sl
     t.reg = t.k == w.r ? lds_load(init_addr(w.lz)) : 0u;
     // partial head / tail pieces need byte masks (whole ones come from the zero buffer)
     t.e0 = ((w.lz & 15u) && t.w0 == 0 && w.nb) ? 0u : ~0u;
-    t.e1 = ((w.tz & 15u) && t.cnt && t.w0 + P * (t.cnt - 1u) == w.nb - 1u) ? t.cnt - 1u : ~0u;
+    t.e1 = (w.tz && t.cnt && t.w0 + P * (t.cnt - 1u) == w.nb - 1u) ? t.cnt - 1u : ~0u;
     t.e2 = t.e3 = ~0u;
     t.ps = -4096;
     t.connect = 0;
@@ -354,6 +343,32 @@ __device__ __forceinline__ uint32_t xor_lanes(uint32_t lg, uint32_t v) {
         if (LVL < static_cast<int>(lg)) return xor_lanes<LVL + 1>(lg, v ^ dpp<kDppRowShl + (1 << LVL)>(v));
     }
     return v;
+}
+
+// End of a group: lane k sits 32k + tz bytes past the data end.  Undo the 32k
+// by x^(-256k) -- four byte-indexed lookups in the image's correction columns
+// (each lane starts at a different byte so the lanes sharing k spread over four
+// columns), XOR the P lanes, then undo tz (unaligned packet ends only).  Lane
+// k == 0 of each packet returns the packet's register.
+__device__ __forceinline__ uint32_t finish_packet(uint32_t lg, uint32_t k, uint32_t tz, uint32_t lane, uint32_t reg) {
+    if ((1u << lg) <= kCorrLanes) {
+        const uint32_t kk = k ? k : 1u;
+        const uint32_t rot = (lane >> lg) & 3u;
+        uint32_t x[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t b = (static_cast<uint32_t>(i) + rot) & 3u;
+            const uint32_t sel = 0x0C0C0000u | ((4u + b) << 8);      // byte1 = byte b of reg, byte0 = column
+            x[i] = lds_load(__builtin_amdgcn_perm(reg, corr_col(kk, b), sel));
+        }
+        const uint32_t c = xor3(x[0], x[1], x[2]) ^ x[3];
+        reg = k ? c : reg;
+    } else {
+        reg = mulmod(reg, lds_load(cinv_addr(32u * k)));
+    }
+    reg = xor_lanes<0>(lg, reg);
+    if (k == 0 && tz) reg = mulmod(reg, lds_load(cinv_addr(tz)));
+    return reg;
 }
 
 template <int I, int N, class F>
@@ -518,10 +533,7 @@ __global__ void __launch_bounds__(G::kThreads) crc32_stream_kernel(PacketArgs pa
         marks >>= 16;
         --nfl;
         if (++cst == cstages) {
-            // finish the group: lane k sits 32k + tz bytes past the data end --
-            // undo that by x^(-8n), then XOR the P lanes
-            reg = mulmod(reg, lds_load(cinv_addr(32u * t.k + t.tz)));
-            reg = xor_lanes<0>(lg, reg);
+            reg = finish_packet(lg, t.k, t.tz, lane, reg);
             if (MODE) desired = xor_lanes<0>(lg, desired);
             if (t.active && t.k == 0) {
                 if (MODE == 0) {
@@ -760,6 +772,10 @@ struct HostTables {
                 for (uint32_t j = 0; j < 256; ++j) img[(j * 256 + col_byte(t)) / 4] = row[j];
                 for (uint32_t j = 0; j < 256; ++j) row[j] = sarwate_step(row[j], 0);
             }
+            for (uint32_t k = 1; k < std::min<uint32_t>(kImageP[im], kCorrLanes); ++k)
+                for (uint32_t b = 0; b < 4; ++b)
+                    for (uint32_t v = 0; v < 256; ++v)
+                        img[(256u * v + corr_col(k, b)) / 4] = gf2_mulmod(v << (8 * b), cinv[32 * k]);
             for (uint32_t r = 0; r < 32; ++r) img[init_addr(r) / 4] = init[r];
             for (uint32_t i = 0; i < static_cast<uint32_t>(kCinvEntries); ++i) img[cinv_addr(i) / 4] = cinv[i];
         }

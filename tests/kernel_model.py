@@ -129,8 +129,9 @@ def free_col(c: int) -> int:
 
 # Free columns are 256-entry tables indexed by the row (a byte value), so a
 # lookup is one v_perm (byte -> address byte 1, column -> byte 0) + ds_read.
-KINIT_COL = 16            # INIT[r], r < 32 (rows 0..31)
-KCINV_COL = 17            # CINV[n], n < 512: rows n & 255 of columns 17 + (n >> 8)
+KCORR_COL = 0             # columns 4(k-1) + b, k = 1..7: byte b of a register times x^(-256k)
+KINIT_COL = 29            # INIT[r], r < 32 (rows 0..31)
+KCINV_COL = 30            # CINV[n], n < 512: rows n & 255 of columns 30 + (n >> 8)
 
 
 def init_addr(r: int) -> int:
@@ -141,14 +142,22 @@ def cinv_addr(n: int) -> int:
     return 256 * (n & 255) + free_col(KCINV_COL + (n >> 8))
 
 
+def corr_addr(k: int, b: int, v: int) -> int:
+    return 256 * v + free_col(KCORR_COL + 4 * (k - 1) + b)
+
+
 def lds_image(P: int = 1) -> list[int]:
     """dword 64*j + 2t + (t>>4) = T'_t[j] = T_{t + 32(P-1)}[j]; free columns hold
-    INIT and CINV."""
+    the per-lane correction tables (k < min(P, 8)), INIT and CINV."""
     T = slicing_tables(32, 32 * (P - 1))
     img = [0] * (256 * 64)
     for j in range(256):
         for t in range(32):
             img[64 * j + col_byte(t) // 4] = T[t][j]
+    for k in range(1, min(P, 8)):                  # lane k's overshoot of 32k bytes, undone
+        for b in range(4):                         # by four byte-indexed lookups
+            for v in range(256):
+                img[corr_addr(k, b, v) // 4] = mulmod(v << (8 * b), CINV[32 * k])
     for r in range(32):
         img[init_addr(r) // 4] = INIT[r]
     for n in range(512):
@@ -227,18 +236,16 @@ def finalize(reg: int) -> int:
 
 # ---------------------------------------------------------------- stream kernel
 def stream_window(addr: int, L: int):
-    """(lz, NB, tz).  Packet end 16-byte aligned: END-aligned window (tz = 0, lz <
-    32 leading zero bytes, the first granule may lie wholly in front of the packet
-    and is then not loaded).  Otherwise START-aligned at the packet's 16-byte
-    granule (lz = addr & 15) with tz trailing bytes zeroed."""
+    """(lz, NB, tz): the window ENDS at the 16-byte granule boundary at or after
+    the packet end (tz = that distance < 16, zeroed) and spans NB whole 32-byte
+    blocks, lz < 32 of them in front of the packet (zeroed; a 16-byte piece wholly
+    in front is read from a zero buffer).  Every byte read lies in a granule that
+    holds packet bytes or is replaced by zeros."""
     if L == 0:
         return 0, 0, 0
-    if (addr + L) % 16 == 0:
-        nb = (L + 31) // 32
-        return 32 * nb - L, nb, 0
-    lz = addr & 15
-    nb = (lz + L + 31) // 32
-    return lz, nb, 32 * nb - lz - L
+    tz = (-(addr + L)) % 16
+    nb = (L + tz + 31) // 32
+    return 32 * nb - tz - L, nb, tz
 
 
 def stream_lane_blocks(k: int, P: int, nb: int) -> list[int]:
@@ -280,7 +287,15 @@ def stream_packet(pkt: bytes, P: int, addr: int = 0, lane_base: int = 0,
         regs.append(reg)
     total = 0
     for k in range(P):                             # lane k sits 32k + tz bytes past the data end
-        total ^= mulmod(regs[k], img[cinv_addr(32 * k + tz) // 4])
+        reg = regs[k]
+        if k and k < 8:                            # x^(-256k): four byte-indexed table lookups
+            reg = (img[corr_addr(k, 0, reg & 0xFF) // 4] ^ img[corr_addr(k, 1, (reg >> 8) & 0xFF) // 4] ^
+                   img[corr_addr(k, 2, (reg >> 16) & 0xFF) // 4] ^ img[corr_addr(k, 3, reg >> 24) // 4])
+        elif k:
+            reg = mulmod(reg, img[cinv_addr(32 * k) // 4])
+        total ^= reg
+    if tz:
+        total = mulmod(total, img[cinv_addr(tz) // 4])
     return total, desired
 
 

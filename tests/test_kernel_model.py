@@ -41,6 +41,14 @@ def test_free_columns_disjoint_from_tables():
         assert img[km.init_addr(r) // 4] == km.INIT[r]
     for i in (0, 1, 31, 200, 255, 256, 511):
         assert img[km.cinv_addr(i) // 4] == km.CINV[i]
+    rng = random.Random(9)
+    for k in range(1, 8):
+        for _ in range(10):
+            v = rng.getrandbits(32)
+            got = 0
+            for b in range(4):
+                got ^= img[km.corr_addr(k, b, (v >> (8 * b)) & 0xFF) // 4]
+            assert got == km.mulmod(v, km.CINV[32 * k])
 
 
 def test_cinv_inverts_x8n():
