@@ -68,6 +68,14 @@ __device__ __forceinline__ u32x4 ldg16(const uint8_t* p) {
     return v;
 }
 
+// 16 bytes at a 16-byte aligned GLOBAL address given as an integer (an integer
+// cast to a generic pointer would make the compiler emit flat loads, which it
+// orders with vmcnt(0) + lgkmcnt(0)).
+typedef __attribute__((address_space(1))) const u32x4 global_u32x4;
+__device__ __forceinline__ u32x4 ldg16_addr(uint64_t addr) {
+    return *reinterpret_cast<global_u32x4*>(static_cast<uintptr_t>(addr));
+}
+
 // 16 bytes at A, with bytes in front of the packet start `a` read as zero.
 // Precondition: every byte of [max(A,a), A+16) belongs to the packet.
 __device__ __forceinline__ u32x4 ldg16_head(const uint8_t* A, const uint8_t* a) {

@@ -275,17 +275,22 @@ __device__ __forceinline__ Task consumer_setup(const PacketArgs& pa, uint32_t sl
     return t;
 }
 
-// First stage >= from holding a fix-up block of any lane (wave-uniform; ~0u = none).
-template <class G>
-__device__ __forceinline__ uint32_t next_edge_stage(const Task& t, uint32_t from) {
+// First stage >= from holding a fix-up block of any lane (wave-uniform; ~0u =
+// none); a stage is 2^LSB block ordinals.
+template <uint32_t LSB>
+__device__ __forceinline__ uint32_t next_edge_stage_l(const Task& t, uint32_t from) {
     uint32_t m = ~0u;
     const uint32_t e[4] = {t.e0, t.e1, t.e2, t.e3};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const uint32_t st = e[i] == ~0u ? ~0u : e[i] >> G::kLsb;
+        const uint32_t st = e[i] == ~0u ? ~0u : e[i] >> LSB;
         if (st >= from) m = min(m, st);
     }
     return wave_min_u(m);
+}
+template <class G>
+__device__ __forceinline__ uint32_t next_edge_stage(const Task& t, uint32_t from) {
+    return next_edge_stage_l<G::kLsb>(t, from);
 }
 
 // Keep bytes [lo, hi) of dword q (bytes 4q .. 4q+3 of the block).
@@ -557,6 +562,313 @@ __global__ void __launch_bounds__(G::kThreads) crc32_stream_kernel(PacketArgs pa
         }
     };
     while (!done) unroll_slots<G::kNB>(stage);
+}
+
+// ============================================================ register-stream kernel
+//
+// Same per-packet arithmetic as crc32_stream_kernel (strided lanes, advancing
+// tables, rotation, table-driven finish), but each lane loads its own blocks
+// straight into a ring of R VGPR block slots with plain 16-byte loads: the P
+// lanes of a packet read one contiguous P*32-byte chunk per step, every lane
+// keeps R blocks in flight (16 waves x R x 2 KiB per CU) and the compiler's own
+// counted vmcnt waits order the loads.  A LOAD cursor runs R steps ahead of the
+// FOLD cursor across group boundaries.  Packet metadata never uses VGPR loads
+// inside the loop (their waits would drain the ring): each wave stages the
+// metadata of a window of 2H groups in LDS and refills one half at a time.  A
+// piece wholly in front of a packet is read from the zero buffer; lanes past
+// their last block read zeros, so every load is unconditional and the ring stays
+// regular; a step whose load side had nothing to issue is a bubble.
+template <int W, int R, int H>
+struct VGeom {
+    static constexpr int kWaves = W, kR = R;
+    static constexpr int kThreads = 64 * W;
+    // metadata window half (groups): H for send; verify stages 5 fields per lane,
+    // so its half shrinks to what the LDS holds
+    static constexpr int kHalf(int mode) {
+        return mode ? ((160 * 1024 - kLdsTableBytes) / (W * 2 * 1280) < H ? (160 * 1024 - kLdsTableBytes) / (W * 2 * 1280) : H)
+                    : H;
+    }
+    static constexpr uint32_t kSlot(int mode) { return (mode ? 5u : 3u) * 256u; }   // metadata per group
+    static constexpr int kLds(int mode) { return kLdsTableBytes + W * 2 * kHalf(mode) * static_cast<int>(kSlot(mode)); }
+    static_assert(kLdsTableBytes + W * 2 * H * 3 * 256 <= 160 * 1024 && kHalf(1) >= 1, "LDS budget");
+};
+
+struct Meta {
+    uint32_t len, lo, hi, so, cid;
+};
+
+__device__ __forceinline__ Window window_of(const PacketArgs& pa, const Meta& m, bool active, uint32_t lg) {
+    Window w;
+    w.active = active;
+    w.L = active ? m.len : 0u;
+    const uint64_t off = static_cast<uint64_t>(m.lo) | (static_cast<uint64_t>(m.hi) << 32);
+    const uint64_t a = reinterpret_cast<uint64_t>(pa.bytes) + off, e = a + w.L;
+    w.tz = w.L ? static_cast<uint32_t>((0u - e) & 15u) : 0u;
+    w.nb = w.L ? (w.L + w.tz + 31u) >> 5 : 0u;
+    w.lz = 32u * w.nb - w.tz - w.L;
+    w.ws = e + w.tz - 32ull * w.nb;
+    w.r = (0u - w.nb) & ((1u << lg) - 1u);
+    return w;
+}
+
+// Load side of this lane for one group: cursors of its next block's two halves
+// in LANE order (first = original bytes 0-15 unless the lane swaps halves).
+struct LSide {
+    uint64_t cur0, cur1;
+    uint32_t cnt;
+    uint32_t hz;        // first block's original bytes 0-15 wholly in front of the packet
+};
+
+__device__ __forceinline__ LSide lside_of(const Window& w, uint32_t k, uint32_t lg, uint32_t hsb) {
+    LSide l;
+    const uint32_t P = 1u << lg;
+    const uint32_t w0 = (k - w.r) & (P - 1u);
+    l.cnt = w0 < w.nb ? ((w.nb - 1u - w0) >> lg) + 1u : 0u;
+    const uint64_t base = w.ws + 32ull * w0;
+    l.cur0 = base + 16u * hsb;
+    l.cur1 = base + 16u * (hsb ^ 1u);
+    l.hz = (w0 == 0 && w.nb && w.lz >= 16u) ? 1u : 0u;
+    return l;
+}
+
+template <int MODE>
+__device__ __forceinline__ Task task_of(const Window& w, const Meta& m, uint64_t pk, uint32_t k, uint32_t lg,
+                                        uint32_t init_reg_lane) {
+    const uint32_t P = 1u << lg;
+    Task t;
+    t.pk = pk;
+    t.active = w.active;
+    t.k = k;
+    t.w0 = (k - w.r) & (P - 1u);
+    t.nb = w.nb;
+    t.lz = w.lz;
+    t.tz = w.tz;
+    t.cnt = t.w0 < w.nb ? ((w.nb - 1u - t.w0) >> lg) + 1u : 0u;
+    t.reg = init_reg_lane;
+    t.e0 = ((w.lz & 15u) && t.w0 == 0 && w.nb) ? 0u : ~0u;
+    t.e1 = (w.tz && t.cnt && t.w0 + P * (t.cnt - 1u) == w.nb - 1u) ? t.cnt - 1u : ~0u;
+    t.e2 = t.e3 = ~0u;
+    t.ps = -4096;
+    t.connect = 0;
+    t.slot_ok = false;
+    if (MODE) {
+        t.connect = m.cid;
+        t.slot_ok = w.L >= 4u && m.so <= w.L - 4u;
+        if (t.slot_ok) {
+            t.ps = static_cast<int32_t>(w.lz + m.so);
+            const uint32_t ws_ = static_cast<uint32_t>(t.ps) >> 5, we_ = static_cast<uint32_t>(t.ps + 3) >> 5;
+            if (((ws_ + w.r) & (P - 1u)) == k) t.e2 = ws_ >> lg;
+            if (we_ != ws_ && ((we_ + w.r) & (P - 1u)) == k) t.e3 = we_ >> lg;
+        }
+    }
+    return t;
+}
+
+template <int MODE, class G, int ABL = 0>
+__global__ void __launch_bounds__(G::kThreads) crc32_vstream_kernel(PacketArgs pa, KernelTables tb) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr uint32_t F = MODE ? 5u : 3u;
+    constexpr uint32_t kSlot = F * 256u;
+    constexpr int kH = G::kHalf(MODE);
+    constexpr uint32_t kWin = 2u * kH;                     // groups staged per wave
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lg = pa.lg, P = 1u << lg;
+    const uint32_t gsh = 6u - lg;
+    const uint64_t ngroups = (pa.n + (1u << gsh) - 1u) >> gsh;
+    const uint64_t wv = static_cast<uint64_t>(blockIdx.x) * G::kWaves + wave;
+    const uint64_t wt = static_cast<uint64_t>(gridDim.x) * G::kWaves;
+    const uint32_t J = wv < ngroups ? static_cast<uint32_t>((ngroups - 1u - wv) / wt) + 1u : 0u;
+    const uint64_t zero = reinterpret_cast<uint64_t>(tb.zero);
+    const uint64_t step = 32ull * P;
+    const uint32_t k = lane & (P - 1u);
+    const uint32_t hsb = (lane >> 4) & 1u;                 // the lane's half swap (LaneSched::hs)
+    const uint32_t mbase = kLdsTableBytes + wave * kWin * kSlot;
+    auto pk_of = [&](uint32_t j) __attribute__((always_inline)) -> uint64_t {
+        return ((wv + static_cast<uint64_t>(j) * wt) << gsh) + (lane >> lg);
+    };
+    // metadata staging: group j -> LDS slot j % 2H, field f of lane l at +256f + 4l
+    auto stage_meta = [&](uint32_t j0, uint32_t cnt) __attribute__((always_inline)) {
+        uint32_t v[kH][F];
+#pragma unroll
+        for (int q = 0; q < kH; ++q) {
+            if (static_cast<uint32_t>(q) < cnt) {
+                const uint64_t pk = min(pk_of(j0 + q), pa.n - 1);
+                v[q][0] = pa.len[pk];
+                const uint32_t* o = reinterpret_cast<const uint32_t*>(pa.off) + 2 * pk;
+                v[q][1] = o[0];
+                v[q][2] = o[1];
+                if (MODE) {
+                    v[q][3] = pa.slot_off[pk];
+                    v[q][4] = pa.connect[pk];
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kH; ++q) {
+            if (static_cast<uint32_t>(q) < cnt) {
+                const uint32_t slot = mbase + ((j0 + q) % kWin) * kSlot + 4u * lane;
+#pragma unroll
+                for (uint32_t f = 0; f < F; ++f)
+                    *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(
+                        static_cast<uintptr_t>(slot + 256u * f)) = v[q][f];
+            }
+        }
+    };
+    auto read_meta = [&](uint32_t j) __attribute__((always_inline)) -> Meta {
+        const uint32_t slot = mbase + (j % kWin) * kSlot + 4u * lane;
+        Meta m;
+        m.len = lds_load(slot);
+        m.lo = lds_load(slot + 256u);
+        m.hi = lds_load(slot + 512u);
+        m.so = MODE ? lds_load(slot + 768u) : 0u;
+        m.cid = MODE ? lds_load(slot + 1024u) : 0u;
+        return m;
+    };
+
+    // prologue: table image and the first window of metadata (one drain, here only)
+    const uint32_t img = lg == 2 ? 1u : lg == 3 ? 2u : 3u;
+    fill_table<G::kThreads>(lds, tb.image + static_cast<size_t>(img) * kImageDwords);
+    uint32_t staged = min(J, kWin);                          // groups [0, staged) are in LDS
+    stage_meta(0, min(staged, static_cast<uint32_t>(kH)));
+    if (staged > static_cast<uint32_t>(kH)) stage_meta(kH, staged - kH);
+    __syncthreads();
+    if (!J) return;
+
+    // load side
+    u32x4 ra[G::kR], rb[G::kR];
+    uint32_t jl = 0, bl = 0, sl = 0, cminl = 0;
+    bool ldone = false;
+    LSide ls = lside_of(window_of(pa, read_meta(0), pk_of(0) < pa.n, lg), k, lg, hsb);
+    sl = wave_max_u(ls.cnt);
+    cminl = wave_min_u(ls.cnt);
+    uint32_t bubbles = 0;                                     // bit i: ring slot i holds no block
+    auto issue = [&](u32x4& x0, u32x4& x1, uint32_t slotbit) __attribute__((always_inline)) {
+        while (!ldone && bl == sl) {                          // next group of the load side
+            if (jl + 1 == J) {
+                ldone = true;
+                break;
+            }
+            if (jl + 1 >= staged) break;                      // metadata not staged yet: bubble
+            ++jl;
+            ls = lside_of(window_of(pa, read_meta(jl), pk_of(jl) < pa.n, lg), k, lg, hsb);
+            sl = wave_max_u(ls.cnt);
+            cminl = wave_min_u(ls.cnt);
+            bl = 0;
+        }
+        uint64_t a0 = zero, a1 = zero;
+        const bool live = !ldone && bl < sl;
+        if (live) {
+            if (bl < cminl) {
+                a0 = ls.cur0;
+                a1 = ls.cur1;
+            } else {
+                const bool v = bl < ls.cnt;
+                a0 = v ? ls.cur0 : a0;
+                a1 = v ? ls.cur1 : a1;
+            }
+            if (bl == 0 && ls.hz) {                           // head piece wholly in front
+                if (hsb) a1 = zero;
+                else a0 = zero;
+            }
+            ls.cur0 += step;
+            ls.cur1 += step;
+            ++bl;
+            bubbles &= ~slotbit;
+        } else {
+            bubbles |= slotbit;
+        }
+        if (ABL == 2) {
+            a0 = zero;
+            a1 = zero;
+        }
+        x0 = ldg16_addr(a0);
+        x1 = ldg16_addr(a1);
+    };
+    static_for<0, G::kR>([&](auto ic) __attribute__((always_inline)) {
+        constexpr int i = decltype(ic)::value;
+        issue(ra[i], rb[i], 1u << i);
+        __builtin_amdgcn_sched_barrier(0);                    // keep slot order = issue order
+    });
+
+    const LaneSched s = make_sched(lane);
+    // fold side
+    uint32_t jf = 0, bf = 0;
+    Task t{};
+    uint32_t sf = 0, cminf = 0, nedge = ~0u, reg = 0, desired = 0;
+    bool done = false;
+    auto begin_group = [&]() __attribute__((always_inline)) {
+        const Meta m = read_meta(jf);
+        const Window w = window_of(pa, m, pk_of(jf) < pa.n, lg);
+        const uint32_t init = lds_load(init_addr(w.lz));
+        t = task_of<MODE>(w, m, pk_of(jf), k, lg, k == w.r ? init : 0u);
+        sf = wave_max_u(t.cnt);
+        cminf = wave_min_u(t.cnt);
+        nedge = next_edge_stage_l<0>(t, 0);
+        reg = t.reg;
+        desired = 0;
+        bf = 0;
+    };
+    // finish the current fold group, then set up the next one with blocks (groups
+    // whose packets are all empty finish at once, as the load side skips them);
+    // refill a half of the metadata window when the fold side has left it
+    auto end_group = [&]() __attribute__((always_inline)) {
+        for (;;) {
+            reg = finish_packet(lg, t.k, t.tz, lane, reg);
+            if (MODE) desired = xor_lanes<0>(lg, desired);
+            if (t.active && t.k == 0) {
+                if (MODE == 0) {
+                    pa.out[t.pk] = finalize(reg);                // packet.cs:159
+                } else {
+                    const uint32_t comp = t.slot_ok ? finalize(reg) : 0u;
+                    pa.ok[t.pk] = (t.slot_ok && comp == desired) ? 1 : 0;
+                    if (pa.out) pa.out[t.pk] = comp;
+                }
+            }
+            if (++jf == J) {
+                done = true;
+                return;
+            }
+            if (jf % kH == 0 && staged < J && jf >= static_cast<uint32_t>(kH)) {   // the fold left a half
+                const uint32_t c = min(J - staged, static_cast<uint32_t>(kH));
+                stage_meta(staged, c);
+                staged += c;
+            }
+            begin_group();
+            if (sf) return;
+        }
+    };
+    begin_group();
+    if (!sf) end_group();
+
+    // A step folds its ring slot (if work remains and it holds a block) and ALWAYS
+    // refills it, so every path back to the loop header has issued the R slots in
+    // order and the compiler's counted vmcnt waits stay at 2R-2 instead of draining.
+    auto step_fn = [&](auto ic) __attribute__((always_inline)) {
+        constexpr int i = decltype(ic)::value;
+        if (!done && !((bubbles >> i) & 1u)) {
+            u32x4 A = ra[i], B = rb[i];
+            if (bf == nedge) {
+                const bool valid = bf < t.cnt;
+                const bool fix = valid && (bf == t.e0 || bf == t.e1 || (MODE && (bf == t.e2 || bf == t.e3)));
+                if (fix) edge_fix<MODE>(A, B, s.hs, t, t.w0 + P * bf, desired);
+                nedge = next_edge_stage_l<0>(t, bf + 1);
+            }
+            const uint32_t nr = ABL == 1 ? xor3(reg ^ A.x ^ A.y, A.z ^ A.w ^ B.x, B.y ^ B.z ^ B.w)
+                                         : fold_block_lane(reg, A, B, s);
+            if (bf < cminf) reg = nr;
+            else reg = bf < t.cnt ? nr : reg;
+            if (++bf == sf) end_group();
+        }
+        issue(ra[i], rb[i], 1u << i);                         // refill this slot R steps ahead
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    if (!done) {
+        for (;;) {
+            static_for<0, G::kR>(step_fn);
+            if (done) break;
+        }
+    }
 }
 
 // ============================================================ direct kernel
@@ -846,6 +1158,37 @@ using StreamGeoms = std::tuple<StreamGeom<16, 1, 2>, StreamGeom<11, 1, 3>, Strea
 constexpr int kNumStreamGeoms = std::tuple_size<StreamGeoms>::value;
 constexpr int kStreamDefault = 0;
 
+template <class G>
+struct VStreamVariant {
+    static void launch(int mode, int abl, unsigned grid, hipStream_t st, const PacketArgs& pa,
+                       const KernelTables& tb) {
+        if (mode == 1)
+            hipLaunchKernelGGL((crc32_vstream_kernel<1, G>), dim3(grid), dim3(G::kThreads), G::kLds(1), st, pa, tb);
+        else if (abl == 1)
+            hipLaunchKernelGGL((crc32_vstream_kernel<0, G, 1>), dim3(grid), dim3(G::kThreads), G::kLds(0), st, pa, tb);
+        else if (abl == 2)
+            hipLaunchKernelGGL((crc32_vstream_kernel<0, G, 2>), dim3(grid), dim3(G::kThreads), G::kLds(0), st, pa, tb);
+        else
+            hipLaunchKernelGGL((crc32_vstream_kernel<0, G, 0>), dim3(grid), dim3(G::kThreads), G::kLds(0), st, pa, tb);
+    }
+    static int setup() {
+        const void* fns[] = {reinterpret_cast<const void*>(crc32_vstream_kernel<0, G, 0>),
+                             reinterpret_cast<const void*>(crc32_vstream_kernel<0, G, 1>),
+                             reinterpret_cast<const void*>(crc32_vstream_kernel<0, G, 2>),
+                             reinterpret_cast<const void*>(crc32_vstream_kernel<1, G, 0>)};
+        for (int i = 0; i < 4; ++i) {
+            const hipError_t e = hipFuncSetAttribute(fns[i], hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     G::kLds(i == 3 ? 1 : 0));
+            if (e != hipSuccess) return herr(e);
+        }
+        return 0;
+    }
+};
+
+// register-stream geometries: paths 2 + kNumStreamGeoms + index
+using VStreamGeoms = std::tuple<VGeom<16, 3, 3>, VGeom<16, 2, 3>, VGeom<16, 4, 4>, VGeom<8, 4, 4>, VGeom<8, 6, 6>>;
+constexpr int kNumVStreamGeoms = std::tuple_size<VStreamGeoms>::value;
+
 template <size_t I = 0>
 void launch_stream(int geom, int mode, int abl, int num_cus, uint64_t groups, hipStream_t st,
                    const PacketArgs& pa, const KernelTables& tb) {
@@ -859,6 +1202,30 @@ void launch_stream(int geom, int mode, int abl, int num_cus, uint64_t groups, hi
             launch_stream<I + 1>(geom, mode, abl, num_cus, groups, st, pa, tb);
         }
     }
+}
+
+template <size_t I = 0>
+void launch_vstream(int geom, int mode, int abl, int num_cus, uint64_t groups, hipStream_t st,
+                    const PacketArgs& pa, const KernelTables& tb) {
+    if constexpr (I < std::tuple_size<VStreamGeoms>::value) {
+        using G = std::tuple_element_t<I, VStreamGeoms>;
+        if (geom == static_cast<int>(I)) {
+            const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(
+                1, std::min<uint64_t>((groups + G::kWaves - 1) / G::kWaves, static_cast<uint64_t>(num_cus))));
+            VStreamVariant<G>::launch(mode, abl, grid, st, pa, tb);
+        } else {
+            launch_vstream<I + 1>(geom, mode, abl, num_cus, groups, st, pa, tb);
+        }
+    }
+}
+
+template <size_t I = 0>
+int setup_vstream() {
+    if constexpr (I < std::tuple_size<VStreamGeoms>::value) {
+        const int rc = VStreamVariant<std::tuple_element_t<I, VStreamGeoms>>::setup();
+        return rc ? rc : setup_vstream<I + 1>();
+    }
+    return 0;
 }
 
 template <size_t I = 0>
@@ -877,7 +1244,10 @@ int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStr
     if (ctx->path != 1 && pa.lg >= 2 && pa.lg <= 4) {
         const uint64_t groups = (pa.n + (64u >> pa.lg) - 1) >> (6 - pa.lg);
         const int geom = ctx->path == 0 ? kStreamDefault : ctx->path - 2;
-        launch_stream(geom, mode, ctx->ablation, ctx->num_cus, groups, st, pa, tb);
+        if (geom < kNumStreamGeoms)
+            launch_stream(geom, mode, ctx->ablation, ctx->num_cus, groups, st, pa, tb);
+        else
+            launch_vstream(geom - kNumStreamGeoms, mode, ctx->ablation, ctx->num_cus, groups, st, pa, tb);
     } else {
         const uint64_t tasks = pa.n << pa.lg;
         const unsigned grid = grid_for(ctx, tasks);
@@ -943,6 +1313,7 @@ int enet_hip_context_create(int device, enet_hip_context** out) {
         if ((rc = herr(hipMemcpy(ctx->d_xn, ht.xn.data(), ht.xn.size() * 4, hipMemcpyHostToDevice)))) break;
         if ((rc = herr(hipMemcpy(ctx->d_init, ht.init.data(), 32 * 4, hipMemcpyHostToDevice)))) break;
         if ((rc = setup_stream())) break;
+        if ((rc = setup_vstream())) break;
         if ((rc = herr(hipFuncSetAttribute(reinterpret_cast<const void*>(crc32_direct_kernel<0>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTableBytes)))) break;
         if ((rc = herr(hipFuncSetAttribute(reinterpret_cast<const void*>(crc32_direct_kernel<1>),
@@ -990,7 +1361,7 @@ int enet_hip_diag_ablation(enet_hip_context* ctx, int mode) {
 }
 
 int enet_hip_set_kernel_path(enet_hip_context* ctx, int path) {
-    if (!ctx || path < 0 || path > 1 + kNumStreamGeoms) return -static_cast<int>(hipErrorInvalidValue);
+    if (!ctx || path < 0 || path > 1 + kNumStreamGeoms + kNumVStreamGeoms) return -static_cast<int>(hipErrorInvalidValue);
     ctx->path = path;
     return 0;
 }

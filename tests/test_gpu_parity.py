@@ -115,7 +115,7 @@ def test_linearity_and_determinism(ctx):
     assert (run_batch(ctx, a, off, lens, 16, 1) == ca).all()
 
 
-N_STREAM_GEOMS = 6
+N_STREAM_GEOMS = 11          # 6 LDS-ring stream geometries + 5 register-stream geometries
 
 
 @pytest.mark.parametrize("geom", range(N_STREAM_GEOMS))
