@@ -27,6 +27,8 @@
 
 #include "crc32_device.hpp"
 #include "crc32_math.hpp"
+#include "crc32_lean.hpp"
+#include "crc32_stream_common.hpp"
 #include "enet_hip.h"
 
 namespace enethip {
@@ -41,22 +43,6 @@ __device__ __forceinline__ void fill_table(uint8_t* lds, const uint32_t* image) 
     for (int i = threadIdx.x; i < kLdsTableBytes / 16; i += NT) dst[i] = src[i];
     __syncthreads();
 }
-
-struct PacketArgs {
-    const uint8_t* bytes;
-    const uint64_t* off;
-    const uint32_t* len;
-    uint64_t n;
-    uint32_t lg;  // log2(lanes per packet)
-    uint32_t* out;
-    // verify mode
-    const uint32_t* slot_off;
-    const uint32_t* connect;
-    uint8_t* ok;
-};
-
-__device__ __forceinline__ uint32_t lds_load(uint32_t addr) { return *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr)); }
-__device__ __forceinline__ u32x4 lds_load16(uint32_t addr) { return *reinterpret_cast<lds_u32x4*>(static_cast<uintptr_t>(addr)); }
 
 // ============================================================ stream kernel
 //
@@ -112,29 +98,6 @@ struct StreamGeom {
     static_assert(NB >= 2 && NB <= 4 && (SB == 1 || SB == 2 || SB == 4), "geometry");
 };
 
-// s_waitcnt vmcnt(min(n, 63)): the immediate picked by a balanced scalar
-// branch tree (n is wave-uniform).
-template <int Lo, int Hi>
-__device__ __forceinline__ void wait_vm_tree(uint32_t n) {
-    if constexpr (Lo == Hi) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Lo) : "memory");
-    } else {
-        constexpr int Mid = (Lo + Hi) / 2;
-        if (n <= static_cast<uint32_t>(Mid)) wait_vm_tree<Lo, Mid>(n);
-        else wait_vm_tree<Mid + 1, Hi>(n);
-    }
-}
-__device__ __forceinline__ void wait_vm(uint32_t n) { wait_vm_tree<0, 63>(__builtin_amdgcn_readfirstlane(n)); }
-
-__device__ __forceinline__ void dma16(const void* g, uint32_t lds_addr) {
-    __builtin_amdgcn_global_load_lds(g, reinterpret_cast<__attribute__((address_space(3))) void*>(
-                                            static_cast<uintptr_t>(lds_addr)), 16, 0, 0);
-}
-__device__ __forceinline__ void dma4(const void* g, uint32_t lds_addr) {
-    __builtin_amdgcn_global_load_lds(g, reinterpret_cast<__attribute__((address_space(3))) void*>(
-                                            static_cast<uintptr_t>(lds_addr)), 4, 0, 0);
-}
-
 
 // Lane c's run sits at buf + kRun*c, its 16-byte piece p in slot p ^ swz(c):
 // swz(c) = ((c >> log2(16/R)) & (R-1)) ^ ((c >> 4) & 1), R = pieces per run,
@@ -168,13 +131,6 @@ __device__ __forceinline__ void issue_meta(const PacketArgs& pa, uint64_t pk0, u
 __device__ __forceinline__ uint32_t meta_field(uint32_t slot, uint32_t lg, uint32_t f, uint32_t j) {
     return lds_load(slot + 4u * ((f << (6u - lg)) + j));
 }
-
-// One packet's window, seen from any lane.
-struct Window {
-    uint64_t ws;        // first window byte (16-byte aligned)
-    uint32_t L, lz, nb, tz, r;
-    bool active;
-};
 
 __device__ __forceinline__ Window packet_window(const PacketArgs& pa, uint32_t slot, uint32_t lg, uint64_t pk0,
                                                 uint32_t j) {
@@ -227,17 +183,6 @@ __device__ __forceinline__ void producer_setup(Producer<G>& pr, const PacketArgs
     pr.stages = wave_max_u(most);
 }
 
-// Consumer side: this lane's task of the group.
-struct Task {
-    uint64_t pk;
-    uint32_t k, w0, nb, lz, tz, cnt, reg;
-    uint32_t e0, e1, e2, e3;   // block ordinals needing head/tail/slot fix-ups (~0u = none)
-    bool active;
-    int32_t ps;                // verify: window position of the slot
-    uint32_t connect;
-    bool slot_ok;
-};
-
 template <int MODE>
 __device__ __forceinline__ Task consumer_setup(const PacketArgs& pa, uint32_t slot, uint32_t lg, uint64_t pk0,
                                                uint32_t lane) {
@@ -275,121 +220,9 @@ __device__ __forceinline__ Task consumer_setup(const PacketArgs& pa, uint32_t sl
     return t;
 }
 
-// First stage >= from holding a fix-up block of any lane (wave-uniform; ~0u =
-// none); a stage is 2^LSB block ordinals.
-template <uint32_t LSB>
-__device__ __forceinline__ uint32_t next_edge_stage_l(const Task& t, uint32_t from) {
-    uint32_t m = ~0u;
-    const uint32_t e[4] = {t.e0, t.e1, t.e2, t.e3};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const uint32_t st = e[i] == ~0u ? ~0u : e[i] >> LSB;
-        if (st >= from) m = min(m, st);
-    }
-    return wave_min_u(m);
-}
 template <class G>
 __device__ __forceinline__ uint32_t next_edge_stage(const Task& t, uint32_t from) {
     return next_edge_stage_l<G::kLsb>(t, from);
-}
-
-// Keep bytes [lo, hi) of dword q (bytes 4q .. 4q+3 of the block).
-__device__ __forceinline__ uint32_t keep_mask(int lo, int hi, int q) {
-    const int a = lo - 4 * q, b = hi - 4 * q;
-    const uint32_t ma = a <= 0 ? 0xFFFFFFFFu : a >= 4 ? 0u : (0xFFFFFFFFu << (8 * a));
-    const uint32_t mb = b >= 4 ? 0xFFFFFFFFu : b <= 0 ? 0u : (0xFFFFFFFFu >> (32 - 8 * b));
-    return ma & mb;
-}
-
-// Head/tail zeroing and (verify) slot substitution of block w, words in LANE
-// order (A, B swapped when hs).
-template <int MODE>
-__device__ __forceinline__ void edge_fix(u32x4& A, u32x4& B, uint32_t hs, const Task& t, uint32_t w,
-                                         uint32_t& desired) {
-    uint32_t v[8];
-    const bool sw = hs != 0;
-    const u32x4 h0 = sw ? B : A, h1 = sw ? A : B;
-    v[0] = h0.x; v[1] = h0.y; v[2] = h0.z; v[3] = h0.w;
-    v[4] = h1.x; v[5] = h1.y; v[6] = h1.z; v[7] = h1.w;
-    const int lo = (w == 0) ? static_cast<int>(t.lz) : 0;
-    const int hi = (w + 1 == t.nb) ? 32 - static_cast<int>(t.tz) : 32;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] &= keep_mask(lo, hi, q);
-    if (MODE) {
-        const int rel = t.ps - 32 * static_cast<int>(w);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int d = rel - 4 * q;
-            if (d > -4 && d < 4) {
-                uint32_t M, C;
-                if (d >= 0) {
-                    M = 0xFFFFFFFFu << (8 * d);
-                    C = t.connect << (8 * d);
-                    desired |= v[q] >> (8 * d);
-                } else {
-                    M = 0xFFFFFFFFu >> (-8 * d);
-                    C = t.connect >> (-8 * d);
-                    desired |= (v[q] & M) << (-8 * d);
-                }
-                v[q] = (v[q] & ~M) | (C & M);
-            }
-        }
-    }
-    const u32x4 n0 = {v[0], v[1], v[2], v[3]}, n1 = {v[4], v[5], v[6], v[7]};
-    A = sw ? n1 : n0;
-    B = sw ? n0 : n1;
-}
-
-// XOR of the P registers of each packet into its lane k == 0 (DPP tree inside a
-// 16-lane row: lane k takes lane k + 2^l at level l).
-template <int LVL>
-__device__ __forceinline__ uint32_t xor_lanes(uint32_t lg, uint32_t v) {
-    if constexpr (LVL < 4) {
-        if (LVL < static_cast<int>(lg)) return xor_lanes<LVL + 1>(lg, v ^ dpp<kDppRowShl + (1 << LVL)>(v));
-    }
-    return v;
-}
-
-// End of a group: lane k sits 32k + tz bytes past the data end.  Undo the 32k
-// by x^(-256k) -- four byte-indexed lookups in the image's correction columns
-// (each lane starts at a different byte so the lanes sharing k spread over four
-// columns), XOR the P lanes, then undo tz (unaligned packet ends only).  Lane
-// k == 0 of each packet returns the packet's register.
-__device__ __forceinline__ uint32_t finish_packet(uint32_t lg, uint32_t k, uint32_t tz, uint32_t lane, uint32_t reg) {
-    if ((1u << lg) <= kCorrLanes) {
-        const uint32_t kk = k ? k : 1u;
-        const uint32_t rot = (lane >> lg) & 3u;
-        uint32_t x[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t b = (static_cast<uint32_t>(i) + rot) & 3u;
-            const uint32_t sel = 0x0C0C0000u | ((4u + b) << 8);      // byte1 = byte b of reg, byte0 = column
-            x[i] = lds_load(__builtin_amdgcn_perm(reg, corr_col(kk, b), sel));
-        }
-        const uint32_t c = xor3(x[0], x[1], x[2]) ^ x[3];
-        reg = k ? c : reg;
-    } else {
-        reg = mulmod(reg, lds_load(cinv_addr(32u * k)));
-    }
-    reg = xor_lanes<0>(lg, reg);
-    if (k == 0 && tz) reg = mulmod(reg, lds_load(cinv_addr(tz)));
-    return reg;
-}
-
-template <int I, int N, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-    if constexpr (I < N) {
-        f(std::integral_constant<int, I>{});
-        static_for<I + 1, N>(f);
-    }
-}
-
-template <int N, class F>
-__device__ __forceinline__ void unroll_slots(F&& f) {
-    if constexpr (N > 0) {
-        unroll_slots<N - 1>(f);
-        f(std::integral_constant<uint32_t, N - 1>{});
-    }
 }
 
 // ABL (diagnostics only): 0 = real, 1 = no table lookups, 2 = no packet DMA.
@@ -1029,6 +862,8 @@ struct enet_hip_context {
     int lanes_per_packet = 0;    // 0 = auto
     int wgs_per_cu = 0;          // 0 = auto (direct / gather kernels)
     int path = 0;                // 0 = stream (default geometry), 1 = direct, 2+k = stream geometry k
+    uint64_t* trace = nullptr;   // diagnostics: lean-kernel per-wave timeline
+    int ablation_prio = 0;       // tuning: lean-kernel lagging-wave priority (diag_ablation mode 8)
     int ablation = 0;            // diagnostics: 1 = no lookups, 2 = no DMA (wrong CRCs by design)
     // staging for the host-memory entry points
     std::mutex mu;
@@ -1188,6 +1023,8 @@ struct VStreamVariant {
 // register-stream geometries: paths 2 + kNumStreamGeoms + index
 using VStreamGeoms = std::tuple<VGeom<16, 3, 3>, VGeom<16, 2, 3>, VGeom<16, 4, 4>, VGeom<8, 4, 4>, VGeom<8, 6, 6>>;
 constexpr int kNumVStreamGeoms = std::tuple_size<VStreamGeoms>::value;
+// lean kernel geometries (crc32_lean.hip): paths kLeanPath0 + geom; path 0 runs geom 0
+constexpr int kLeanPath0 = 2 + kNumStreamGeoms + kNumVStreamGeoms;
 
 template <size_t I = 0>
 void launch_stream(int geom, int mode, int abl, int num_cus, uint64_t groups, hipStream_t st,
@@ -1240,10 +1077,16 @@ int setup_stream() {
 int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStream_t st) {
     if (pa.n == 0) return 0;
     const KernelTables tb = tables_of(ctx);
+    const_cast<PacketArgs&>(pa).trace = ctx->trace;
+    const_cast<PacketArgs&>(pa).prio = static_cast<uint32_t>(ctx->ablation_prio);
     // the stream kernel takes 4, 8 or 16 lanes per packet; anything else runs direct
     if (ctx->path != 1 && pa.lg >= 2 && pa.lg <= 4) {
+        const bool lean_path = ctx->path >= kLeanPath0 || (ctx->path == 0 && ctx->ablation == 0);
+        if (lean_path && pa.lg <= 3)
+            return lean_launch(mode, pa.lg, ctx->path == 0 ? 0 : ctx->path - kLeanPath0, ctx->ablation,
+                               ctx->num_cus, st, pa, tb);
         const uint64_t groups = (pa.n + (64u >> pa.lg) - 1) >> (6 - pa.lg);
-        const int geom = ctx->path == 0 ? kStreamDefault : ctx->path - 2;
+        const int geom = (ctx->path == 0 || ctx->path >= kLeanPath0) ? kStreamDefault : ctx->path - 2;
         if (geom < kNumStreamGeoms)
             launch_stream(geom, mode, ctx->ablation, ctx->num_cus, groups, st, pa, tb);
         else
@@ -1314,6 +1157,7 @@ int enet_hip_context_create(int device, enet_hip_context** out) {
         if ((rc = herr(hipMemcpy(ctx->d_init, ht.init.data(), 32 * 4, hipMemcpyHostToDevice)))) break;
         if ((rc = setup_stream())) break;
         if ((rc = setup_vstream())) break;
+        if ((rc = lean_setup())) break;
         if ((rc = herr(hipFuncSetAttribute(reinterpret_cast<const void*>(crc32_direct_kernel<0>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTableBytes)))) break;
         if ((rc = herr(hipFuncSetAttribute(reinterpret_cast<const void*>(crc32_direct_kernel<1>),
@@ -1355,13 +1199,20 @@ int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgro
 }
 
 int enet_hip_diag_ablation(enet_hip_context* ctx, int mode) {
-    if (!ctx || mode < 0 || mode > 2) return -static_cast<int>(hipErrorInvalidValue);
-    ctx->ablation = mode;
+    if (!ctx || mode < 0 || mode > 31) return -static_cast<int>(hipErrorInvalidValue);
+    ctx->ablation = mode & ~8;
+    ctx->ablation_prio = (mode >> 3) & 1;
+    return 0;
+}
+
+int enet_hip_diag_trace(enet_hip_context* ctx, uint64_t* deviceBuffer) {
+    if (!ctx) return -static_cast<int>(hipErrorInvalidValue);
+    ctx->trace = deviceBuffer;
     return 0;
 }
 
 int enet_hip_set_kernel_path(enet_hip_context* ctx, int path) {
-    if (!ctx || path < 0 || path > 1 + kNumStreamGeoms + kNumVStreamGeoms) return -static_cast<int>(hipErrorInvalidValue);
+    if (!ctx || path < 0 || path >= kLeanPath0 + kLeanGeoms) return -static_cast<int>(hipErrorInvalidValue);
     ctx->path = path;
     return 0;
 }

@@ -1,0 +1,492 @@
+// crc32_lean.hip -- the lean streamed CRC32 kernel for gfx950 (MI355X): the hot
+// path of libenethip.  Path replaced: ENet.enet_crc32
+// (/root/reference/enet-csharp/ENet/c/packet.cs:142-160) over a whole batch of
+// DGRAMs, and the receive verify around it (c/protocol.cs:1052-1068).
+//
+// Arithmetic = crc32_stream_kernel's (tests/kernel_model.py):
+// P = 2^LG lanes per packet walk its 32-byte window blocks strided (lane k folds
+// blocks w with (w + r) % P == k) with the advancing slicing-by-32 tables of the
+// P image, lane k's 32k-byte overshoot is undone by four correction lookups and
+// the P registers are XORed.  What differs is the schedule, cut down to what the
+// memory stream needs (tools/dmabench.hip: this loop shape alone streams 75 MiB
+// in 12.6-13.3 us):
+//   * a stage of a packet is one contiguous P*32-byte chunk (2P pieces of 16 B);
+//     lane k of the packet DMAs pieces k and P + k, so each of the two
+//     global_load_lds_dwordx4 per stage reads P*16 contiguous bytes per packet and
+//     a lane's producer needs only its own packet's window.  Lane k's block (chunk
+//     block w0) then sits as 32 contiguous LDS bytes in instruction 2w0/P's area;
+//   * every stage issues exactly two data DMAs (a lane past its blocks, or a
+//     wave past its groups, reads the zero buffer), so the wait for a stage is
+//     the constant vmcnt(2(NB-1)) -- plus the metadata DMAs of a chunk in the
+//     one or two stages after one is issued, picked by a scalar count;
+//   * packet metadata (len, offset; slot offset and connectID for verify) is
+//     DMA'd per chunk of JM groups into one of two LDS halves, a chunk ahead;
+//   * the 8 data dwords are read with eight ds_read_b32 whose per-lane addresses
+//     already apply the lane's dword permutation D(l) (conflict-free: see
+//     LeanSched), so the fold is 8 reg-injection bitop3 + 32 v_perm + 32
+//     ds_read_b32 + 16 xor3 (the b128 form needs 18 bitop3 for the permutation);
+//   * lanes per packet is a template parameter.
+// Blocks holding a partial head/tail piece (or, in verify, the checksum slot) are
+// read in original order and go through edge_fix + fold_block, as before.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "crc32_lean.hpp"
+
+namespace enethip {
+
+// Lane schedule: lane l looks up byte m = i ^ pi(l) at step i, pi(l) = 4 D(l) + b(l),
+// D(l) the dword permutation, b(l) the byte permutation inside a dword.  pi is a
+// bit permutation of l & 31, so the 32 lanes of a half-wave read 32 different
+// tables in every lookup.  The data read of register r (original
+// dword r ^ D) of lane (packet j, lane k) hits bank 4jP + 8 (w0 mod P/2) + (r ^ D)
+// mod 32; it is conflict-free for every r and every rotation when D holds the two
+// low packet bits and the lane bit that separates w0 from w0 + P/2:
+//   P = 8 (l = 8j + k): D = l3 | l4 << 1 | l2 << 2, b = l0 | l1 << 1
+//   P = 4 (l = 4j + k): D = l3 | l4 << 1 | l1 << 2, b = l0 | l2 << 1
+// (tests/test_kernel_model.py checks both).
+struct LeanSched {
+    LaneSched a;        // col/sel for the lookups; m1/m2/hs realise D for fold_block
+    uint32_t dq[8];     // byte offset in the lane's 32-byte block of data register r
+    uint32_t dm[8];     // all-ones in the register that holds original dword 0
+};
+
+template <int LG>
+__device__ __forceinline__ LeanSched make_lean_sched(uint32_t lane) {
+    LeanSched s;
+    const uint32_t l5 = lane & 31u;
+    const uint32_t sb = LG == 3 ? 2u : 1u;                  // lane bit giving D's bit 2
+    const uint32_t ob = LG == 3 ? 1u : 2u;                  // lane bit giving b's bit 1
+    const uint32_t D = ((l5 >> 3) & 3u) | (((l5 >> sb) & 1u) << 2);
+    const uint32_t b = (l5 & 1u) | (((l5 >> ob) & 1u) << 1);
+    const uint32_t pi = 4u * D + b;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+        uint32_t r = 0;
+#pragma unroll
+        for (int h = 0; h < 4; ++h) r |= col_byte(31u - ((4u * g + h) ^ pi)) << (8 * h);
+        s.a.col[g] = r;
+    }
+#pragma unroll
+    for (int h = 0; h < 4; ++h) s.a.sel[h] = static_cast<uint32_t>(h) | ((4u + (h ^ b)) << 8) | 0x0C0C0000u;
+    s.a.m1 = 0u - (D & 1u);
+    s.a.m2 = 0u - ((D >> 1) & 1u);
+    s.a.hs = 0u - ((D >> 2) & 1u);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        s.dq[r] = 4u * (static_cast<uint32_t>(r) ^ D);
+        s.dm[r] = static_cast<uint32_t>(r) == D ? 0xFFFFFFFFu : 0u;
+    }
+    return s;
+}
+
+// One block (32 Sarwate steps, packet.cs:153) from the lane-permuted dwords x.
+__device__ __forceinline__ uint32_t fold_perm(uint32_t reg, const uint32_t (&x)[8], const LeanSched& s) {
+    uint32_t d[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) d[r] = __builtin_amdgcn_bitop3_b32(x[r], reg, s.dm[r], 0x78);   // x ^ (reg & dm)
+    uint32_t v[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) v[i] = lds_load(__builtin_amdgcn_perm(d[i >> 2], s.a.col[i >> 2], s.a.sel[i & 3]));
+    uint32_t acc = xor3(v[0], v[1], v[2]);
+#pragma unroll
+    for (int i = 3; i + 1 < 32; i += 2) acc = xor3(acc, v[i], v[i + 1]);
+    return acc ^ v[31];
+}
+
+template <int MODE, int LG, int W, int NB>
+struct LeanGeom {
+    static constexpr uint32_t P = 1u << LG, kPk = 64u >> LG;           // lanes / packets per group
+    static constexpr uint32_t kF = MODE ? 8u : 4u;                      // metadata dwords per packet (padded)
+    static constexpr uint32_t kGroupMeta = kF * kPk;                    // metadata dwords per group
+    static constexpr uint32_t kRing = NB * 2048u;                       // NB stages of 64 lanes x 32 B
+    static constexpr uint32_t kWaveLds = (160u * 1024u - kLdsTableBytes) / W / 256u * 256u;
+    static constexpr uint32_t kHalf = (kWaveLds - kRing) / 2u / 256u * 256u;
+    static constexpr uint32_t JM = kHalf / (4u * kGroupMeta);          // groups per metadata chunk
+    static constexpr uint32_t kMetaOps = JM * kGroupMeta / 64u;
+    static constexpr int kThreads = 64 * W;
+    static constexpr int kLds = kLdsTableBytes + W * static_cast<int>(kRing + 2u * kHalf);
+    static constexpr int kTableRounds = (kImageDwords / 4 + 64 * W - 1) / (64 * W);
+    static_assert(JM >= 2 && (JM & (JM - 1)) == 0 && (JM * kGroupMeta) % 64u == 0, "metadata chunk");
+    static_assert(JM + 1 > NB - 1, "producer may not run a whole chunk ahead");
+    static_assert(kLds <= 160 * 1024, "LDS budget");
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vm_n() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// vmcnt(Base + c * K) for a wave-uniform c in [0, NB-1]
+template <int Base, int K, int C>
+__device__ __forceinline__ void wait_vm_sel(uint32_t c) {
+    if constexpr (C == 0) {
+        wait_vm_n<Base>();
+    } else {
+        if (c == static_cast<uint32_t>(C)) wait_vm_n<(Base + C * K > 63 ? 63 : Base + C * K)>();
+        else wait_vm_sel<Base, K, C - 1>(c);
+    }
+}
+
+// ABL (diagnostics, wrong checksums by design): 1 = no table lookups (the fold is
+// an XOR of the data), 2 = packet DMA from an L2-resident 2 KiB slice of the table
+// images per wave (no HBM traffic), 4 = no table image load (with 1 only),
+// 16 = synthetic metadata (1200-byte packets packed from offset 0, nothing read).
+template <int MODE, int LG, int W, int NB, int ABL = 0>
+__global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, KernelTables tb) {
+    using G = LeanGeom<MODE, LG, W, NB>;
+    constexpr uint32_t P = G::P, kPk = G::kPk, JM = G::JM;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t ngroups = (pa.n + kPk - 1u) >> (6 - LG);
+    const uint64_t wv = static_cast<uint64_t>(blockIdx.x) * W + wave;
+    const uint64_t wt = static_cast<uint64_t>(gridDim.x) * W;
+    const uint32_t J = wv < ngroups ? static_cast<uint32_t>((ngroups - 1u - wv) / wt) + 1u : 0u;
+    const uint32_t ring = kLdsTableBytes + wave * (G::kRing + 2u * G::kHalf);
+    const uint32_t meta0 = ring + G::kRing;
+    const uint64_t zero = reinterpret_cast<uint64_t>(tb.zero);
+    const uint32_t k = lane & (P - 1u), pj_lane = lane >> LG;
+    // diagnostics (enet_hip_diag_trace): per-wave timestamps, 8 x u64 per wave
+    uint64_t tmark[5] = {0, 0, 0, 0, 0};
+    auto mark = [&](int i) __attribute__((always_inline)) {
+        if (pa.trace) tmark[i] = __builtin_amdgcn_s_memrealtime();
+    };
+    mark(0);
+    auto trace_end = [&]() __attribute__((always_inline)) {
+        if (pa.trace && lane == 0u) {
+            uint64_t* tr = pa.trace + 8u * wv;
+            tr[5] = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+            for (int i = 0; i < 5; ++i) tr[i] = tmark[i];
+            const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);      // HW_ID
+            const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);    // XCC_ID
+            tr[6] = hw | (static_cast<uint64_t>(xcc) << 32);
+            tr[7] = J;
+        }
+    };
+
+    // ---- metadata chunks: chunk c = this wave's groups [c JM, (c+1) JM) in half c & 1
+    auto issue_meta = [&](uint32_t c) __attribute__((always_inline)) {
+        const uint32_t half = meta0 + (c & 1u) * G::kHalf;
+#pragma unroll
+        for (uint32_t o = 0; o < G::kMetaOps; ++o) {
+            const uint32_t x = 64u * o + lane;
+            const uint32_t q = x / G::kGroupMeta, f = (x / kPk) % G::kF, p = x % kPk;
+            const uint32_t j = min(c * JM + q, J - 1u);
+            const uint64_t pk = min((wv + static_cast<uint64_t>(j) * wt) * kPk + p, pa.n - 1u);
+            const uint32_t* src = pa.len + pk;
+            if (f == 1u || f == 2u) src = reinterpret_cast<const uint32_t*>(pa.off) + 2u * pk + (f - 1u);
+            if (MODE && f == 3u) src = pa.slot_off + pk;
+            if (MODE && f == 4u) src = pa.connect + pk;
+            dma4(src, half + 256u * o);
+        }
+    };
+    auto meta_at = [&](uint32_t j, uint32_t f) __attribute__((always_inline)) -> uint32_t {
+        return lds_load(meta0 + ((j / JM) & 1u) * G::kHalf + 4u * (((j % JM) * G::kF + f) * kPk + pj_lane));
+    };
+    auto window_of = [&](uint32_t j) __attribute__((always_inline)) -> Window {
+        Window w;
+        const uint64_t pkw = (wv + static_cast<uint64_t>(j) * wt) * kPk + pj_lane;
+        w.active = pkw < pa.n;
+        w.L = w.active ? ((ABL & 16) ? 1200u : meta_at(j, 0)) : 0u;
+        const uint64_t off = (ABL & 16) ? 1200u * pkw
+                                        : static_cast<uint64_t>(meta_at(j, 1)) | (static_cast<uint64_t>(meta_at(j, 2)) << 32);
+        const uint64_t a = reinterpret_cast<uint64_t>(pa.bytes) + off, e = a + w.L;
+        w.tz = w.L ? static_cast<uint32_t>((0u - e) & 15u) : 0u;       // window ends at the granule after the end
+        w.nb = w.L ? (w.L + w.tz + 31u) >> 5 : 0u;
+        w.lz = 32u * w.nb - w.tz - w.L;
+        w.ws = e + w.tz - 32ull * w.nb;
+        w.r = (0u - w.nb) & (P - 1u);
+        return w;
+    };
+
+    // ---- prologue: metadata chunks 0 and 1, this wave's share of the table image
+    uint32_t issued = 0;                                     // metadata chunks issued so far
+    const uint32_t nchunks = (J + JM - 1u) / JM;
+    if (J && !(ABL & 16)) {
+        issue_meta(0);
+        issued = 1;
+        if (nchunks > 1) {
+            issue_meta(1);
+            issued = 2;
+        }
+    }
+    if (!(ABL & 4)) {
+        const uint32_t* src = tb.image + static_cast<size_t>(LG == 2 ? 1 : 2) * kImageDwords;
+#pragma unroll
+        for (int r = 0; r < G::kTableRounds; ++r) {
+            const uint32_t piece0 = min((static_cast<uint32_t>(r) * W + wave) * 64u,
+                                        static_cast<uint32_t>(kImageDwords / 4 - 64));
+            dma16(src + 4u * (piece0 + lane), 16u * piece0);
+        }
+    }
+    wait_vm_n<G::kTableRounds>();                            // metadata chunks 0 and 1 have landed
+    mark(1);
+
+    // ---- producer: this lane's block of its packet, one stage ahead per slot
+    uint64_t pcur = 0;                                       // piece k of the packet's next chunk
+    uint32_t pv0 = 0, pv1 = 0, pst = 0, pstages = 0, pj = 0; // stages holding pieces k / P + k
+    bool phz = false, pdone = J == 0;
+    uint32_t it = 0;                                         // loop iteration (stage) counter
+    uint32_t meta_guard = 0;                                 // from this iteration on chunk `issued - 1` has landed
+    auto producer_setup = [&](uint32_t j) __attribute__((always_inline)) {
+        const Window w = window_of(j);
+        const uint32_t w0 = (k - w.r) & (P - 1u);
+        const uint32_t cnt = w0 < w.nb ? ((w.nb - 1u - w0) >> LG) + 1u : 0u;
+        const uint32_t np = 2u * w.nb;                       // window pieces
+        pv0 = np > k ? (np - k + 2u * P - 1u) >> (LG + 1) : 0u;
+        pv1 = np > P + k ? (np - P - k + 2u * P - 1u) >> (LG + 1) : 0u;
+        pcur = w.ws + 16u * k;
+        phz = k == 0u && w.lz >= 16u;                        // piece 0 lies wholly in front
+        pstages = max(1u, wave_max_u(cnt));
+        pst = 0;
+    };
+    auto produce = [&](uint32_t slot) __attribute__((always_inline)) {
+        if (!pdone && pst == pstages) {
+            if (++pj < J) {
+                if (!(ABL & 16) && pj % JM == 0u) {          // entering chunk pj / JM
+                    const uint32_t c = pj / JM;
+                    if (c >= issued) {                        // the consumer has not prefetched it yet
+                        issue_meta(c);
+                        issued = c + 1u;
+                        wait_vm_n<0>();
+                    } else if (c + 1u == issued && it < meta_guard) {
+                        wait_vm_n<0>();                       // prefetched, landing not yet guaranteed
+                    }
+                }
+                producer_setup(pj);
+            } else {
+                pdone = true;
+            }
+        }
+        const bool v0 = !pdone && pst < pv0 && !(pst == 0u && phz);
+        const bool v1 = !pdone && pst < pv1;
+        uint64_t a0 = v0 ? pcur : zero, a1 = v1 ? pcur + 16u * P : zero;
+        if (ABL & 2) {
+            const uint64_t l2 = reinterpret_cast<uint64_t>(tb.image) + (wv % 128u) * 2048u + 16u * lane;
+            a0 = l2;
+            a1 = l2 + 1024u;
+        }
+        dma16(reinterpret_cast<const void*>(a0), ring + 2048u * slot);
+        dma16(reinterpret_cast<const void*>(a1), ring + 2048u * slot + 1024u);
+        pcur += 32u * P;
+        ++pst;
+    };
+
+    if (J) {
+        producer_setup(0);
+        unroll_slots<NB - 1>([&](auto sc) __attribute__((always_inline)) { produce(decltype(sc)::value); });
+    }
+    if (!J) {                                                // no groups: the table share, then leave
+        wait_vm_n<0>();
+        mark(2);
+        __builtin_amdgcn_s_barrier();
+        mark(3);
+        trace_end();
+        return;
+    }
+
+    const LeanSched s = make_lean_sched<LG>(lane);
+    uint32_t rb = 0;                                         // LDS address (ring slot 0) of the lane's block
+    uint32_t ra[8];                                          // ... and of its permuted data registers
+
+    // ---- consumer
+    uint32_t cj = 0, cst = 0, cstages = 0, nedge = ~0u, reg = 0, desired = 0;
+    Task t{};
+    auto consumer_setup = [&](uint32_t j) __attribute__((always_inline)) {
+        const Window w = window_of(j);
+        t.pk = (wv + static_cast<uint64_t>(j) * wt) * kPk + pj_lane;
+        t.active = w.active;
+        t.k = k;
+        t.w0 = (k - w.r) & (P - 1u);
+        t.nb = w.nb;
+        t.lz = w.lz;
+        t.tz = w.tz;
+        t.cnt = t.w0 < w.nb ? ((w.nb - 1u - t.w0) >> LG) + 1u : 0u;
+        const uint32_t init = lds_load(init_addr(w.lz));
+        t.reg = k == w.r ? init : 0u;
+        t.e0 = ((w.lz & 15u) && t.w0 == 0u && w.nb) ? 0u : ~0u;
+        t.e1 = (w.tz && t.cnt && t.w0 + P * (t.cnt - 1u) == w.nb - 1u) ? t.cnt - 1u : ~0u;
+        t.e2 = t.e3 = ~0u;
+        t.ps = -4096;
+        t.connect = 0;
+        t.slot_ok = false;
+        if (MODE) {
+            const uint32_t so = meta_at(j, 3);
+            t.connect = meta_at(j, 4);
+            t.slot_ok = w.L >= 4u && so <= w.L - 4u;
+            if (t.slot_ok) {
+                t.ps = static_cast<int32_t>(w.lz + so);
+                const uint32_t ws_ = static_cast<uint32_t>(t.ps) >> 5, we_ = static_cast<uint32_t>(t.ps + 3) >> 5;
+                if (((ws_ + w.r) & (P - 1u)) == k) t.e2 = ws_ >> LG;
+                if (we_ != ws_ && ((we_ + w.r) & (P - 1u)) == k) t.e3 = we_ >> LG;
+            }
+        }
+        rb = ring + 1024u * ((2u * t.w0) >> LG) + 16u * (pj_lane * P + ((2u * t.w0) & (P - 1u)));
+#pragma unroll
+        for (int r = 0; r < 8; ++r) ra[r] = rb + s.dq[r];
+        cstages = max(1u, wave_max_u(t.cnt));
+        nedge = next_edge_stage_l<0>(t, 0);
+        reg = t.reg;
+        desired = 0;
+        cst = 0;
+    };
+
+    uint32_t mbits = 0;                                      // bit u: iteration it-1-u issued a metadata chunk
+    bool done = false;
+    auto iteration = [&](auto sc) __attribute__((always_inline)) {
+        constexpr uint32_t S = decltype(sc)::value;          // ring slot consumed by this iteration
+        if (done) return;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // WAR: the slot refilled below was read last iteration
+        produce((S + NB - 1) % NB);
+        wait_vm_sel<2 * (NB - 1), static_cast<int>(G::kMetaOps), NB - 1>(
+            __builtin_popcount(mbits & ((1u << (NB - 1)) - 1u)));   // stage S has landed
+        mbits <<= 1;
+        if (pa.prio) {
+            // tail fairness: a wave with more stages left than its CU neighbours is
+            // issued first (s_setprio: 0..3), so lagging waves catch up
+            const uint32_t rem = (J - 1u - cj) * cstages + (cstages - cst);
+            if (rem >= 8u) __builtin_amdgcn_s_setprio(3);
+            else if (rem >= 5u) __builtin_amdgcn_s_setprio(2);
+            else if (rem >= 3u) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+        if (it == 0u) {
+            // first fold: every wave's share of the table image must have landed (it
+            // was issued before this wave's stages, so the wait above covers it)
+            mark(2);
+            __builtin_amdgcn_s_barrier();
+            mark(3);
+            mark(4);
+            consumer_setup(0);                               // reads INIT[] from the table
+        }
+        uint32_t nr;
+        if (cst == nedge) {                                  // head/tail/slot fix-ups: original dword order
+            u32x4 A = lds_load16(rb + 2048u * S), B = lds_load16(rb + 2048u * S + 16u);
+            const bool fix = cst < t.cnt && (cst == t.e0 || cst == t.e1 || (MODE && (cst == t.e2 || cst == t.e3)));
+            if (fix) edge_fix<MODE>(A, B, 0u, t, t.w0 + P * cst, desired);
+            nr = fold_block(reg, A, B, s.a);
+            nedge = next_edge_stage_l<0>(t, cst + 1u);
+        } else {
+            uint32_t x[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) x[r] = lds_load(ra[r] + 2048u * S);
+            nr = (ABL & 1) ? xor3(reg ^ x[0] ^ x[1], x[2] ^ x[3] ^ x[4], x[5] ^ x[6] ^ x[7]) : fold_perm(reg, x, s);
+        }
+        reg = cst < t.cnt ? nr : reg;
+        if (++cst == cstages) {
+            reg = finish_packet(LG, t.k, t.tz, lane, reg);
+            if (MODE) desired = xor_lanes<0>(LG, desired);
+            if (t.active && t.k == 0u) {
+                if (MODE == 0) {
+                    pa.out[t.pk] = finalize(reg);            // packet.cs:159
+                } else {
+                    const uint32_t comp = t.slot_ok ? finalize(reg) : 0u;
+                    pa.ok[t.pk] = (t.slot_ok && comp == desired) ? 1 : 0;   // protocol.cs:1066-1068
+                    if (pa.out) pa.out[t.pk] = comp;
+                }
+            }
+            if (++cj == J) {
+                done = true;
+                return;
+            }
+            if (!(ABL & 16) && cj % JM == 0u) {             // the consumer left chunk cj/JM - 1: prefetch the next
+                const uint32_t c = cj / JM + 1u;
+                if (c < nchunks && c >= issued) {
+                    issue_meta(c);
+                    issued = c + 1u;
+                    meta_guard = it + NB + 1u;               // issued after data(it): landed by wait(it + NB)
+                    mbits |= 1u;
+                }
+            }
+            consumer_setup(cj);
+        }
+        ++it;
+    };
+    while (!done) unroll_slots<NB>(iteration);
+    wait_vm_n<0>();                                          // no LDS-DMA may outlive the wave
+    trace_end();
+}
+
+// ---------------------------------------------------------------- host side
+
+template <int W, int NB>
+struct LeanVariant {
+    template <int MODE, int LG>
+    static const void* fn() {
+        return reinterpret_cast<const void*>(crc32_lean_kernel<MODE, LG, W, NB>);
+    }
+    static int setup() {
+        const void* fns[4] = {fn<0, 2>(), fn<0, 3>(), fn<1, 2>(), fn<1, 3>()};
+        const int lds[4] = {LeanGeom<0, 2, W, NB>::kLds, LeanGeom<0, 3, W, NB>::kLds, LeanGeom<1, 2, W, NB>::kLds,
+                            LeanGeom<1, 3, W, NB>::kLds};
+        for (int i = 0; i < 4; ++i) {
+            const hipError_t e = hipFuncSetAttribute(fns[i], hipFuncAttributeMaxDynamicSharedMemorySize, lds[i]);
+            if (e != hipSuccess) return -static_cast<int>(e);
+        }
+        return 0;
+    }
+    template <int MODE, int LG>
+    static void go(int num_cus, hipStream_t st, const PacketArgs& pa, const KernelTables& tb) {
+        using G = LeanGeom<MODE, LG, W, NB>;
+        const uint64_t groups = (pa.n + G::kPk - 1u) / G::kPk;
+        const unsigned grid = static_cast<unsigned>(
+            std::max<uint64_t>(1, std::min<uint64_t>((groups + W - 1) / W, static_cast<uint64_t>(num_cus))));
+        hipLaunchKernelGGL((crc32_lean_kernel<MODE, LG, W, NB>), dim3(grid), dim3(G::kThreads), G::kLds, st, pa, tb);
+    }
+    template <int LG, int ABL>
+    static void go_abl(int num_cus, hipStream_t st, const PacketArgs& pa, const KernelTables& tb) {
+        using G = LeanGeom<0, LG, W, NB>;
+        static bool set = false;
+        if (!set) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(crc32_lean_kernel<0, LG, W, NB, ABL>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, G::kLds);
+            set = true;
+        }
+        const uint64_t groups = (pa.n + G::kPk - 1u) / G::kPk;
+        const unsigned grid = static_cast<unsigned>(
+            std::max<uint64_t>(1, std::min<uint64_t>((groups + W - 1) / W, static_cast<uint64_t>(num_cus))));
+        hipLaunchKernelGGL((crc32_lean_kernel<0, LG, W, NB, ABL>), dim3(grid), dim3(G::kThreads), G::kLds, st, pa,
+                           tb);
+    }
+    static void launch(int mode, int lg, int abl, int num_cus, hipStream_t st, const PacketArgs& pa,
+                       const KernelTables& tb) {
+        if (mode == 0 && abl) {
+            switch (abl) {                                   // diagnostics: 8-lane packets only
+                case 1: go_abl<3, 1>(num_cus, st, pa, tb); break;
+                case 2: go_abl<3, 2>(num_cus, st, pa, tb); break;
+                case 3: go_abl<3, 3>(num_cus, st, pa, tb); break;
+                case 5: go_abl<3, 5>(num_cus, st, pa, tb); break;
+                case 17: go_abl<3, 17>(num_cus, st, pa, tb); break;
+                case 21: go_abl<3, 21>(num_cus, st, pa, tb); break;
+                case 16: go_abl<3, 16>(num_cus, st, pa, tb); break;
+                default: break;
+            }
+            return;
+        }
+        if (mode == 0) {
+            if (lg == 2) go<0, 2>(num_cus, st, pa, tb);
+            else go<0, 3>(num_cus, st, pa, tb);
+        } else {
+            if (lg == 2) go<1, 2>(num_cus, st, pa, tb);
+            else go<1, 3>(num_cus, st, pa, tb);
+        }
+    }
+};
+
+int lean_setup() {
+    int rc = LeanVariant<16, 2>::setup();
+    return rc ? rc : LeanVariant<12, 3>::setup();
+}
+
+int lean_launch(int mode, int lg, int geom, int abl, int num_cus, hipStream_t st, const PacketArgs& pa,
+                const KernelTables& tb) {
+    if (lg != 2 && lg != 3) return -static_cast<int>(hipErrorInvalidValue);
+    if (geom == 1) LeanVariant<12, 3>::launch(mode, lg, 0, num_cus, st, pa, tb);
+    else LeanVariant<16, 2>::launch(mode, lg, abl, num_cus, st, pa, tb);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : -static_cast<int>(e);
+}
+
+}  // namespace enethip

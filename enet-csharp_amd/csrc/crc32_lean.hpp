@@ -1,0 +1,21 @@
+// crc32_lean.hpp -- host-side entry of the lean streamed CRC32 kernel
+// (crc32_lean.hip), called by the C-ABI launch dispatch in crc32_kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "crc32_stream_common.hpp"
+
+namespace enethip {
+
+constexpr int kLeanGeoms = 2;   // 0: 16 waves x 2 stages, 1: 12 waves x 3 stages
+
+// Set the dynamic-LDS attribute of every lean kernel instance (once per context).
+int lean_setup();
+
+// Launch the lean kernel for lanes-per-packet 2^lg (lg = 2 or 3) and MODE 0 (crc)
+// or 1 (receive verify); abl != 0 selects a diagnostic ablation (geometry 0, crc
+// only; wrong checksums by design).  Returns 0 or -hipError_t.
+int lean_launch(int mode, int lg, int geom, int abl, int num_cus, hipStream_t st, const PacketArgs& pa,
+                const KernelTables& tb);
+
+}  // namespace enethip

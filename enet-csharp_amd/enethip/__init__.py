@@ -31,7 +31,7 @@ EXPORTED_SYMBOLS = (
     "enet_hip_crc32_gather_device", "enet_hip_crc32_batch_multi", "enet_hip_device_alloc",
     "enet_hip_device_free", "enet_hip_host_alloc", "enet_hip_host_free", "enet_hip_memcpy_h2d",
     "enet_hip_memcpy_d2h", "enet_hip_synchronize", "enet_hip_read_probe_device", "enet_hip_set_kernel_path",
-    "enet_hip_diag_ablation",
+    "enet_hip_diag_ablation", "enet_hip_diag_trace",
 )
 
 
@@ -74,6 +74,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.enet_hip_set_tuning.argtypes = [vp, i32, i32]
     L.enet_hip_diag_ablation.restype = i32
     L.enet_hip_diag_ablation.argtypes = [vp, i32]
+    L.enet_hip_diag_trace.restype = i32
+    L.enet_hip_diag_trace.argtypes = [vp, vp]
     L.enet_hip_set_kernel_path.restype = i32
     L.enet_hip_set_kernel_path.argtypes = [vp, i32]
     L.enet_hip_crc32_batch_device.restype = i32
@@ -172,6 +174,11 @@ class Context:
     def diag_ablation(self, mode: int) -> None:
         """Diagnostics only: 1 = no lookups, 2 = no DMA (wrong CRCs by design)."""
         _check("enet_hip_diag_ablation", self.lib.enet_hip_diag_ablation(self.handle, int(mode)))
+
+    def diag_trace(self, device_ptr) -> None:
+        """Diagnostics only: per-wave timeline buffer (4 x u64 per wave) or None."""
+        p = _ptr(device_ptr) if device_ptr is not None else None
+        _check("enet_hip_diag_trace", self.lib.enet_hip_diag_trace(self.handle, p))
 
     def close(self) -> None:
         if getattr(self, "handle", None):

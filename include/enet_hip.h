@@ -138,6 +138,14 @@ ENET_HIP_API int enet_hip_read_probe_device(enet_hip_context* ctx, const uint8_t
  * design and exist only to price the two halves of the kernel (tools/). */
 ENET_HIP_API int enet_hip_diag_ablation(enet_hip_context* ctx, int mode);
 
+/* ---- diagnostics: per-wave timeline of the lean stream kernel ----
+ * With a non-null device buffer of 8 x uint64 per wave (waves = grid x waves per
+ * workgroup), every lean launch records per wave (s_memrealtime, 100 MHz):
+ * start, metadata landed, table landed, after the table barrier, first stage
+ * landed, end, HW_ID | XCC_ID << 32, groups.  NULL turns it off.  Checksums are
+ * unaffected. */
+ENET_HIP_API int enet_hip_diag_trace(enet_hip_context* ctx, uint64_t* deviceBuffer);
+
 /* ---- small memory helpers (so C#/ctypes hosts need no HIP binding) ---- */
 ENET_HIP_API int enet_hip_device_alloc(enet_hip_context* ctx, size_t bytes, void** out);
 ENET_HIP_API int enet_hip_device_free(enet_hip_context* ctx, void* ptr);

@@ -347,3 +347,107 @@ def crc_packet(pkt: bytes, lanes: int = 1, lane_base: int = 0, addr: int = 0) ->
             reg = mulmod(reg, x8n(after))
         total ^= reg
     return finalize(total)
+
+
+# ---------------------------------------------------------------- lean kernel
+def lean_sched(lane: int, P: int):
+    """crc32_lean.hip's LeanSched: pi(l) = 4 D(l) + b(l); D = l3 | l4 << 1 | s << 2
+    with s = l2 (P = 8) or l1 (P = 4); b = l0 | o << 1 with o the other bit."""
+    l5 = lane & 31
+    sb, ob = (2, 1) if P == 8 else (1, 2)
+    D = ((l5 >> 3) & 3) | (((l5 >> sb) & 1) << 2)
+    b = (l5 & 1) | (((l5 >> ob) & 1) << 1)
+    pi = 4 * D + b
+    col = []
+    for g in range(8):
+        r = 0
+        for h in range(4):
+            r |= col_byte(31 - ((4 * g + h) ^ pi)) << (8 * h)
+        col.append(r)
+    sel = [h | ((4 + (h ^ b)) << 8) | 0x0C0C0000 for h in range(4)]
+    dq = [4 * (r ^ D) for r in range(8)]
+    return D, col, sel, dq
+
+
+def lean_block_address(lane: int, P: int, w0: int) -> int:
+    """LDS byte offset (ring slot 0) of lane (j, k)'s 32-byte block: pieces 2w0,
+    2w0+1 of the packet's chunk, DMA'd by lanes (j, 2w0 mod P), (j, 2w0 mod P + 1)
+    of instruction 2w0 // P."""
+    j = lane // P
+    return 1024 * ((2 * w0) // P) + 16 * (j * P + (2 * w0) % P)
+
+
+def lean_group(arena: bytes, offs: list[int], lens: list[int], P: int, check_banks: bool = True) -> list[int]:
+    """One group (64/P packets, 64 lanes) through the lean kernel's data path:
+    producer DMA of pieces k and P + k per lane per stage into the 2 KiB ring slot,
+    consumer permuted dword reads (bank-checked), fold with the lean schedule,
+    lane corrections, lane XOR, tz correction.  Returns the finalized CRCs."""
+    npk = 64 // P
+    assert len(offs) == npk
+    img = image(P)
+    wins = [stream_window(offs[j], lens[j]) for j in range(npk)]   # (lz, nb, tz)
+    stages = max(1, max(((nb + P - 1) // P) for _, nb, _ in wins))
+    regs = [0] * 64
+    rot = [(-nb) % P for _, nb, _ in wins]
+    for lane in range(64):
+        j, k = divmod(lane, P)
+        lz, nb, tz = wins[j]
+        if k == rot[j]:
+            regs[lane] = INIT[lz]
+    for s in range(stages):
+        slot = bytearray(2048)
+        for lane in range(64):                     # producer: own packet, pieces k and P + k
+            j, k = divmod(lane, P)
+            lz, nb, tz = wins[j]
+            ws = offs[j] + lens[j] + tz - 32 * nb
+            for i, q in enumerate((k, P + k)):
+                piece = 2 * P * s + q              # window piece index
+                ok = piece < 2 * nb and not (s == 0 and q == 0 and lz >= 16)
+                a = ws + 16 * piece
+                data = arena[a:a + 16] if ok else bytes(16)
+                slot[1024 * i + 16 * lane:1024 * i + 16 * lane + 16] = data
+        banks = [[None] * 64 for _ in range(8)]
+        for lane in range(64):                     # consumer
+            j, k = divmod(lane, P)
+            lz, nb, tz = wins[j]
+            w0 = (k - rot[j]) % P
+            cnt = (nb - 1 - w0) // P + 1 if w0 < nb else 0
+            D, col, sel, dq = lean_sched(lane, P)
+            rb = lean_block_address(lane, P, w0)
+            x = []
+            for r in range(8):
+                a = rb + dq[r]
+                banks[r][lane] = (a // 4) % 32
+                x.append(int.from_bytes(slot[a:a + 4], "little"))
+            if s >= cnt:
+                continue
+            w = w0 + P * s                         # window block folded now
+            blk = bytearray(b"".join(v.to_bytes(4, "little") for v in [x[r ^ D] for r in range(8)]))
+            for t in range(32):                    # edge_fix: head / tail bytes outside the packet
+                if (w == 0 and t < lz) or (w == nb - 1 and t >= 32 - tz):
+                    blk[t] = 0
+            xs = [int.from_bytes(blk[4 * (r ^ D):4 * (r ^ D) + 4], "little") for r in range(8)]
+            d = [xs[r] ^ (regs[lane] if r == D else 0) for r in range(8)]
+            acc = 0
+            for i in range(32):
+                addr = v_perm(d[i >> 2], col[i >> 2], sel[i & 3])
+                acc ^= img[addr // 4]
+            regs[lane] = acc
+        if check_banks:
+            for r in range(8):
+                for h in (0, 32):
+                    assert len(set(banks[r][h:h + 32])) == 32, ("bank conflict", r, h)
+    out = []
+    for j in range(npk):
+        lz, nb, tz = wins[j]
+        total = 0
+        for k in range(P):
+            reg = regs[j * P + k]
+            if k:
+                reg = (img[corr_addr(k, 0, reg & 0xFF) // 4] ^ img[corr_addr(k, 1, (reg >> 8) & 0xFF) // 4] ^
+                       img[corr_addr(k, 2, (reg >> 16) & 0xFF) // 4] ^ img[corr_addr(k, 3, reg >> 24) // 4])
+            total ^= reg
+        if tz:
+            total = mulmod(total, img[cinv_addr(tz) // 4])
+        out.append(finalize(total))
+    return out

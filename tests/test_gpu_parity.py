@@ -115,7 +115,8 @@ def test_linearity_and_determinism(ctx):
     assert (run_batch(ctx, a, off, lens, 16, 1) == ca).all()
 
 
-N_STREAM_GEOMS = 11          # 6 LDS-ring stream geometries + 5 register-stream geometries
+N_STREAM_GEOMS = 13          # 6 LDS-ring + 5 register-stream geometries + 2 lean-kernel geometries
+LEAN_PATHS = (13, 14)        # crc32_lean.hip geometries (path 0 runs the first for 4 and 8 lanes)
 
 
 @pytest.mark.parametrize("geom", range(N_STREAM_GEOMS))
@@ -135,6 +136,40 @@ def test_stream_geometries(ctx, golden, oracle_lib, geom):
         assert (run_batch(ctx, small.payload, small.off, small.lens, 4) == exp_s).all()
     finally:
         ctx.set_kernel_path(0)
+
+
+def _verify_expect(oracle_lib, payload, off, lens, slot, conn):
+    return oracle_lib.verify(payload, off, lens, slot, conn)
+
+
+@pytest.mark.parametrize("path", LEAN_PATHS)
+def test_lean_many_chunks(ctx, oracle_lib, path):
+    """Many metadata chunks per wave (tiny packets: one-stage groups, so the
+    producer runs into chunks the consumer has not prefetched yet) and long
+    packets (many stages per group), crc and verify, 4 and 8 lanes."""
+    tiny = workloads.mixed(1_200_000, 0, 40, seed=77, len_seed=78)
+    exp_t = oracle_lib.batch(tiny.payload, tiny.off, tiny.lens, threads=16)
+    big = workloads.mixed(40_000, 2000, 9000, seed=79, len_seed=80)
+    exp_b = oracle_lib.batch(big.payload, big.off, big.lens, threads=16)
+    rng = np.random.default_rng(81)
+    vp, vo, vl, vs, vc = _verify_inputs(rng, 300_000)
+    exp_ok, exp_comp = oracle_lib.verify(vp, vo, vl, vs, vc)
+    try:
+        ctx.set_kernel_path(path)
+        for lanes in (4, 8):
+            assert (run_batch(ctx, tiny.payload, tiny.off, tiny.lens, lanes) == exp_t).all(), ("tiny", lanes)
+            assert (run_batch(ctx, big.payload, big.off, big.lens, lanes) == exp_b).all(), ("big", lanes)
+            ctx.set_tuning(lanes, 0)
+            d_ok = torch.zeros(len(vo), dtype=torch.uint8, device="cuda")
+            d_comp = torch.zeros(len(vo), dtype=torch.int32, device="cuda")
+            ctx.verify_batch_device(dev(vp), dev(vo), dev(vl), dev(vs), dev(vc), len(vo), d_ok, d_comp,
+                                    stream=torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            assert (d_ok.cpu().numpy() == exp_ok).all(), ("verify ok", lanes)
+            assert (d_comp.cpu().numpy().view(np.uint32) == exp_comp).all(), ("verify crc", lanes)
+    finally:
+        ctx.set_kernel_path(0)
+        ctx.set_tuning(0, 0)
 
 
 def test_host_entry_point(ctx, oracle_lib):

@@ -5,7 +5,7 @@ import re
 import sys
 from collections import Counter
 
-S = "enet-csharp_amd/build/crc32_kernels-hip-amdgcn-amd-amdhsa-gfx950.s"
+S = sys.argv[3] if len(sys.argv) > 3 else "enet-csharp_amd/build/crc32_kernels-hip-amdgcn-amd-amdhsa-gfx950.s"
 pat = sys.argv[1]
 mn = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 lines = open(S).read().split("\n")
