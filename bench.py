@@ -41,6 +41,9 @@ def parse(argv=None):
     ap.add_argument("--rotate", type=int, default=5, help="distinct resident batches cycled through")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per packet (0 = library default)")
     ap.add_argument("--wgs", type=int, default=0, help="workgroups per CU (0 = library default)")
+    ap.add_argument("--streams", type=int, default=4,
+                    help="HIP streams the captured steps rotate over: batches are independent, so a "
+                         "launch's prologue overlaps the previous launch's tail (1 = serial)")
     ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "small"],
                     help="cfg2 = the metric's workload; cfg3 = mixed lengths; small = harness tests only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -118,6 +121,7 @@ class GpuEngine:
         self.ctx = enethip.Context(device, lanes, wgs)
         self.stream = torch.cuda.Stream()          # dedicated stream: handle != 0
         self.h = self.stream.cuda_stream
+        self.streams = [self.stream]
         self.bufs = []
         for b in batches:
             self.bufs.append(dict(
@@ -130,9 +134,13 @@ class GpuEngine:
         self.graph = None
         torch.cuda.synchronize()
 
-    def step(self, i: int):
+    def set_streams(self, n: int):
+        self.streams = [self.stream] + [self.torch.cuda.Stream() for _ in range(max(1, n) - 1)]
+
+    def step(self, i: int, stream=None):
         b = self.bufs[i % len(self.bufs)]
-        self.ctx.crc32_batch_device(b["payload"], b["off"], b["lens"], b["n"], b["out"], self.h)
+        h = self.h if stream is None else stream.cuda_stream
+        self.ctx.crc32_batch_device(b["payload"], b["off"], b["lens"], b["n"], b["out"], h)
 
     def probe(self, i: int):
         b = self.bufs[i % len(self.bufs)]
@@ -144,13 +152,19 @@ class GpuEngine:
     def capture(self, steps: int):
         """Capture `steps` launches (rotating batches) into one HIP graph: the timed
         region then replays it with one host call, so host launch overhead (Python +
-        ctypes) cannot starve the GPU.  Each graph node is one ordinary launch."""
+        ctypes) cannot starve the GPU.  Each graph node is one ordinary launch; step i
+        goes to stream i % len(streams) (independent batches: consecutive launches may
+        overlap at their boundary, every launch still checksums its whole batch)."""
         torch = self.torch
         self.sync()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=self.stream):
+            for s in self.streams[1:]:
+                s.wait_stream(self.stream)
             for i in range(steps):
-                self.step(i)
+                self.step(i, self.streams[i % len(self.streams)])
+            for s in self.streams[1:]:
+                self.stream.wait_stream(s)
         self.sync()
         self.graph = g
 
@@ -245,6 +259,8 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
     dist = dist_init(ws)
     batches = make_batches(args.config, args.rotate, rank)
     eng = (engine_factory or GpuEngine)(local, batches, args.lanes, args.wgs)
+    if hasattr(eng, "set_streams"):
+        eng.set_streams(args.streams)
 
     # correctness gate (untimed): first resident batch vs the oracle
     eng.step(0)
@@ -259,7 +275,15 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
         eng.step(i)
     if hasattr(eng, "capture"):
         eng.capture(args.steps)
-        eng.replay()                      # one untimed replay (graph upload / warm)
+        for bf in eng.bufs:               # one untimed replay (graph upload / warm), checked:
+            bf["out"].zero_()             # every rotating batch's CRCs from the graph vs the oracle
+        eng.replay()
+        eng.sync()
+        lib = oracle.OracleLib()
+        for j in range(min(args.steps, len(batches))):
+            ref = lib.batch(batches[j].payload, batches[j].off, batches[j].lens, threads=8)
+            if not (eng.outputs(j) == ref).all():
+                raise SystemExit(f"bench.py: graph replay CRCs of batch {j} differ from the oracle")
         secs = timed_region(dist, eng.sync, 1, eng.replay)
     else:
         secs = timed_region(dist, eng.sync, args.steps, eng.step)
@@ -304,6 +328,7 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
                 "payload_bytes_per_step": int(per_launch),
                 "parallelism": f"{ws} independent shards (no collective)",
                 "lanes_per_packet": args.lanes or "default",
+                "streams": args.streams,
             },
             "hbm_read_frac": round(value * GIB / 1e9 / (HBM_PEAK_GBPS * ws), 4),
             "roofline": {
@@ -313,7 +338,7 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": (traffic or {}).get("hbm_bytes_per_launch"),
-                "kernel": "crc32_stream_kernel<0, StreamGeom<16,1,2>>",
+                "kernel": "crc32_lean_kernel<0, 3, 16, 2>",
                 "kernel_ms": round(k_ms, 5),
                 "span_ms_per_step": round(span_ms, 5),
                 "read_probe_GBps": round(probe, 1),

@@ -43,6 +43,13 @@ __host__ __device__ constexpr uint32_t init_addr(uint32_t r) { return 256u * r +
 __host__ __device__ constexpr uint32_t cinv_addr(uint32_t n) { return 256u * (n & 255u) + free_col(kCinvCol + (n >> 8)); }
 __host__ __device__ constexpr uint32_t corr_col(uint32_t k, uint32_t b) { return free_col(kCorrCol + 4u * (k - 1u) + b); }
 constexpr int kXnEntries = 65536;                  // x^(8n) for n < 65536 (+ high part)
+// Lean-kernel table basis (crc32_lean.hip): every image column but INIT and CINV
+// is GF(2)-linear in the row index, so rows 2^b (b < 8) rebuild it; row 8 holds
+// INIT[0..31] | CINV[0..31], the only INIT/CINV rows that kernel reads.
+constexpr int kBasisRows = 9;
+constexpr int kBasisDwords = kBasisRows * 64;      // per image
+constexpr uint32_t kInitDword = free_col(kInitCol) / 4u;
+constexpr uint32_t kCinvDword = free_col(kCinvCol) / 4u;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // LDS dword addressed by an absolute byte address.  The table is the first thing
@@ -58,6 +65,7 @@ struct KernelTables {
     const uint32_t* xn_hi;  // x^(8*65536*q) mod P, q < 65536
     const uint32_t* init;   // INIT[r], r < 32
     const uint8_t* zero;    // 256 zero bytes: DMA source of pieces wholly outside a packet
+    const uint32_t* basis;  // kBasisDwords per image (lean kernel)
 };
 
 // ------------------------------------------------------------------ device helpers

@@ -859,6 +859,7 @@ struct enet_hip_context {
     uint32_t* d_xn = nullptr;    // lo[65536] | hi[65536]
     uint32_t* d_init = nullptr;  // 32
     uint8_t* d_zero = nullptr;   // 256 zero bytes
+    uint32_t* d_basis = nullptr; // lean-kernel table basis, kBasisDwords per image
     int lanes_per_packet = 0;    // 0 = auto
     int wgs_per_cu = 0;          // 0 = auto (direct / gather kernels)
     int path = 0;                // 0 = stream (default geometry), 1 = direct, 2+k = stream geometry k
@@ -896,8 +897,11 @@ constexpr int kImages = 4;                             // P = 1, 4, 8, 16
 constexpr int kImageP[kImages] = {1, 4, 8, 16};
 
 struct HostTables {
-    std::vector<uint32_t> image, xn, init;
-    HostTables() : image(static_cast<size_t>(kImages) * kImageDwords), xn(2 * kXnEntries), init(32) {
+    std::vector<uint32_t> image, xn, init, basis;
+    bool basis_ok = true;   // the basis rebuilds every image dword the lean kernel reads
+    HostTables()
+        : image(static_cast<size_t>(kImages) * kImageDwords), xn(2 * kXnEntries), init(32),
+          basis(static_cast<size_t>(kImages) * kBasisDwords) {
         init[0] = 0xFFFFFFFFu;
         for (int r = 1; r < 32; ++r) init[r] = unstep_zero(init[r - 1]);
         std::vector<uint32_t> cinv(kCinvEntries);
@@ -925,6 +929,27 @@ struct HostTables {
                         img[(256u * v + corr_col(k, b)) / 4] = gf2_mulmod(v << (8 * b), cinv[32 * k]);
             for (uint32_t r = 0; r < 32; ++r) img[init_addr(r) / 4] = init[r];
             for (uint32_t i = 0; i < static_cast<uint32_t>(kCinvEntries); ++i) img[cinv_addr(i) / 4] = cinv[i];
+            // lean-kernel basis: image rows 2^b of the linear columns, then INIT | CINV
+            uint32_t* bs = basis.data() + static_cast<size_t>(im) * kBasisDwords;
+            auto nonlinear = [](uint32_t d) { return d == kInitDword || d == kCinvDword || d == kCinvDword + 2u; };
+            for (uint32_t b = 0; b < 8; ++b)
+                for (uint32_t d = 0; d < 64; ++d) bs[64 * b + d] = nonlinear(d) ? 0u : img[64u * (1u << b) + d];
+            for (uint32_t r = 0; r < 32; ++r) {
+                bs[512 + r] = init[r];
+                bs[544 + r] = cinv[r];
+            }
+            // what crc32_lean.hip rebuilds must equal the image wherever that kernel
+            // looks (INIT rows < 32, CINV rows < 16; CINV n >= 256 never)
+            for (uint32_t j = 0; j < 256; ++j)
+                for (uint32_t d = 0; d < 64; ++d) {
+                    if (d == kCinvDword + 2u || ((d == kInitDword || d == kCinvDword) && j >= 32)) continue;
+                    uint32_t v = 0;
+                    for (uint32_t b = 0; b < 8; ++b)
+                        if ((j >> b) & 1u) v ^= bs[64 * b + d];
+                    if (d == kInitDword) v = bs[512 + j];
+                    if (d == kCinvDword) v = bs[544 + j];
+                    if (v != img[64 * j + d]) basis_ok = false;
+                }
         }
         // x^(8n) for n < 65536: one zero-byte step per n
         xn[0] = kOneReflected;
@@ -949,7 +974,7 @@ int log2i(int v) {
 }
 
 KernelTables tables_of(const enet_hip_context* ctx) {
-    return KernelTables{ctx->d_image, ctx->d_xn, ctx->d_xn + kXnEntries, ctx->d_init, ctx->d_zero};
+    return KernelTables{ctx->d_image, ctx->d_xn, ctx->d_xn + kXnEntries, ctx->d_init, ctx->d_zero, ctx->d_basis};
 }
 
 unsigned grid_for(const enet_hip_context* ctx, uint64_t tasks) {
@@ -1155,6 +1180,12 @@ int enet_hip_context_create(int device, enet_hip_context** out) {
         if ((rc = herr(hipMemcpy(ctx->d_image, ht.image.data(), ht.image.size() * 4, hipMemcpyHostToDevice)))) break;
         if ((rc = herr(hipMemcpy(ctx->d_xn, ht.xn.data(), ht.xn.size() * 4, hipMemcpyHostToDevice)))) break;
         if ((rc = herr(hipMemcpy(ctx->d_init, ht.init.data(), 32 * 4, hipMemcpyHostToDevice)))) break;
+        if (!ht.basis_ok) {
+            rc = -static_cast<int>(hipErrorInvalidImage);
+            break;
+        }
+        if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_basis), ht.basis.size() * 4)))) break;
+        if ((rc = herr(hipMemcpy(ctx->d_basis, ht.basis.data(), ht.basis.size() * 4, hipMemcpyHostToDevice)))) break;
         if ((rc = setup_stream())) break;
         if ((rc = setup_vstream())) break;
         if ((rc = lean_setup())) break;
@@ -1181,6 +1212,7 @@ int enet_hip_context_destroy(enet_hip_context* ctx) {
     (void)hipFree(ctx->d_xn);
     (void)hipFree(ctx->d_init);
     (void)hipFree(ctx->d_zero);
+    (void)hipFree(ctx->d_basis);
     (void)hipFree(ctx->d_bytes);
     (void)hipFree(ctx->d_meta);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

@@ -25,7 +25,11 @@
 //     already apply the lane's dword permutation D(l) (conflict-free: see
 //     LeanSched), so the fold is 8 reg-injection bitop3 + 32 v_perm + 32
 //     ds_read_b32 + 16 xor3 (the b128 form needs 18 bitop3 for the permutation);
-//   * lanes per packet is a template parameter.
+//   * lanes per packet is a template parameter;
+//   * the 64 KiB table image is not copied into every CU: waves 0..8 DMA one
+//     256-byte row each of a 2.3 KiB basis (KernelTables::basis) and every wave
+//     rebuilds 256/W rows from it between two raw barriers, while its first
+//     stages are already in flight.
 // Blocks holding a partial head/tail piece (or, in verify, the checksum slot) are
 // read in original order and go through edge_fix + fold_block, as before.
 #include <hip/hip_runtime.h>
@@ -107,9 +111,9 @@ struct LeanGeom {
     static constexpr uint32_t kMetaOps = JM * kGroupMeta / 64u;
     static constexpr int kThreads = 64 * W;
     static constexpr int kLds = kLdsTableBytes + W * static_cast<int>(kRing + 2u * kHalf);
-    static constexpr int kTableRounds = (kImageDwords / 4 + 64 * W - 1) / (64 * W);
     static_assert(JM >= 2 && (JM & (JM - 1)) == 0 && (JM * kGroupMeta) % 64u == 0, "metadata chunk");
-    static_assert(JM + 1 > NB - 1, "producer may not run a whole chunk ahead");
+    static_assert(JM + 2 > NB, "the prologue stages (pj <= NB-2) stay in chunk 0: chunk 1 is issued after barrier B");
+    static_assert(W >= kBasisRows && kHalf >= 256u, "waves 0..8 each stage one basis row in their half 1");
     static_assert(kLds <= 160 * 1024, "LDS budget");
 };
 
@@ -201,27 +205,21 @@ __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, Kerne
         return w;
     };
 
-    // ---- prologue: metadata chunks 0 and 1, this wave's share of the table image
+    // ---- prologue: basis row `wave` of the table (waves < kBasisRows) into this
+    // wave's metadata half 1 -- chunk 1 goes there only after barrier B below --
+    // and metadata chunk 0
+    auto basis_row = [&](uint32_t b) __attribute__((always_inline)) -> uint32_t {
+        return kLdsTableBytes + b * (G::kRing + 2u * G::kHalf) + G::kRing + G::kHalf;
+    };
+    if (!(ABL & 4) && wave < static_cast<uint32_t>(kBasisRows))
+        dma4(tb.basis + static_cast<size_t>(LG == 2 ? 1 : 2) * kBasisDwords + 64u * wave + lane, basis_row(wave));
     uint32_t issued = 0;                                     // metadata chunks issued so far
     const uint32_t nchunks = (J + JM - 1u) / JM;
     if (J && !(ABL & 16)) {
         issue_meta(0);
         issued = 1;
-        if (nchunks > 1) {
-            issue_meta(1);
-            issued = 2;
-        }
     }
-    if (!(ABL & 4)) {
-        const uint32_t* src = tb.image + static_cast<size_t>(LG == 2 ? 1 : 2) * kImageDwords;
-#pragma unroll
-        for (int r = 0; r < G::kTableRounds; ++r) {
-            const uint32_t piece0 = min((static_cast<uint32_t>(r) * W + wave) * 64u,
-                                        static_cast<uint32_t>(kImageDwords / 4 - 64));
-            dma16(src + 4u * (piece0 + lane), 16u * piece0);
-        }
-    }
-    wait_vm_n<G::kTableRounds>();                            // metadata chunks 0 and 1 have landed
+    wait_vm_n<0>();                                          // basis row and metadata chunk 0 have landed
     mark(1);
 
     // ---- producer: this lane's block of its packet, one stage ahead per slot
@@ -230,6 +228,7 @@ __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, Kerne
     bool phz = false, pdone = J == 0;
     uint32_t it = 0;                                         // loop iteration (stage) counter
     uint32_t meta_guard = 0;                                 // from this iteration on chunk `issued - 1` has landed
+    uint32_t mbits = 0;                                      // bit u: iteration it-1-u issued a metadata chunk
     auto producer_setup = [&](uint32_t j) __attribute__((always_inline)) {
         const Window w = window_of(j);
         const uint32_t w0 = (k - w.r) & (P - 1u);
@@ -278,13 +277,61 @@ __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, Kerne
         producer_setup(0);
         unroll_slots<NB - 1>([&](auto sc) __attribute__((always_inline)) { produce(decltype(sc)::value); });
     }
-    if (!J) {                                                // no groups: the table share, then leave
-        wait_vm_n<0>();
-        mark(2);
-        __builtin_amdgcn_s_barrier();
-        mark(3);
+
+    // ---- the table image, rebuilt in LDS while the first stages are in flight.
+    // Wave w writes rows w, w + W, ...: row j = XOR of the basis rows b with bit b
+    // of j set, except the INIT and CINV dwords (not linear in j), whose rows < 32
+    // come from basis row 8.  Raw s_barrier: the stage DMAs stay in flight.
+    __builtin_amdgcn_s_barrier();                            // (A) every basis row has landed
+    if (!(ABL & 4)) {
+        uint32_t bb[8];
+#pragma unroll
+        for (int b = 0; b < 8; ++b) bb[b] = lds_load(basis_row(b) + 4u * lane);
+        const bool nonlin = lane == kInitDword || lane == kCinvDword;
+        const uint32_t row8 = basis_row(8) + (lane == kInitDword ? 0u : 128u);
+        if constexpr (W == 16) {
+            // rows wave + 16 i with i in Gray-code order: one XOR per row (the VALU
+            // cost of the generic loop below, ~1 us per CU, sat on the startup path)
+            uint32_t v = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) v ^= ((wave >> b) & 1u) ? bb[b] : 0u;
+#pragma unroll
+            for (uint32_t q = 0; q < 16u; ++q) {
+                const uint32_t i = q ^ (q >> 1);
+                if (q) v ^= bb[4 + __builtin_ctz(q)];
+                uint32_t x = v;
+                if (i < 2u) {                                // rows < 32: INIT / CINV
+                    const uint32_t e = lds_load(row8 + 4u * (wave + 16u * i));
+                    x = nonlin ? e : x;
+                }
+                lds_store(256u * (wave + 16u * i) + 4u * lane, x);
+            }
+        } else {
+            for (uint32_t j = wave; j < 256u; j += W) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int b = 0; b < 8; ++b) v ^= ((j >> b) & 1u) ? bb[b] : 0u;
+                if (j < 32u) {
+                    const uint32_t e = lds_load(row8 + 4u * j);
+                    v = nonlin ? e : v;
+                }
+                lds_store(256u * j + 4u * lane, v);
+            }
+        }
+    }
+    mark(2);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                            // (B) the image is complete, the basis rows read
+    mark(3);
+    if (!J) {                                                // no groups: this wave only helped build the table
         trace_end();
         return;
+    }
+    if (!(ABL & 16) && nchunks > 1u) {                       // chunk 1 into half 1, now free
+        issue_meta(1);
+        issued = 2;
+        meta_guard = NB;                                     // issued before data(0): covered by wait(NB - 1)
+        mbits = 1u;                                          // counted by the waits of iterations 0 .. NB-2
     }
 
     const LeanSched s = make_lean_sched<LG>(lane);
@@ -333,7 +380,8 @@ __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, Kerne
         cst = 0;
     };
 
-    uint32_t mbits = 0;                                      // bit u: iteration it-1-u issued a metadata chunk
+    consumer_setup(0);                                       // reads INIT[] from the finished image
+    mark(4);
     bool done = false;
     auto iteration = [&](auto sc) __attribute__((always_inline)) {
         constexpr uint32_t S = decltype(sc)::value;          // ring slot consumed by this iteration
@@ -351,15 +399,6 @@ __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, Kerne
             else if (rem >= 5u) __builtin_amdgcn_s_setprio(2);
             else if (rem >= 3u) __builtin_amdgcn_s_setprio(1);
             else __builtin_amdgcn_s_setprio(0);
-        }
-        if (it == 0u) {
-            // first fold: every wave's share of the table image must have landed (it
-            // was issued before this wave's stages, so the wait above covers it)
-            mark(2);
-            __builtin_amdgcn_s_barrier();
-            mark(3);
-            mark(4);
-            consumer_setup(0);                               // reads INIT[] from the table
         }
         uint32_t nr;
         if (cst == nedge) {                                  // head/tail/slot fix-ups: original dword order

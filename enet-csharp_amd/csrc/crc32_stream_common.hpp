@@ -33,6 +33,9 @@ struct PacketArgs {
 
 __device__ __forceinline__ uint32_t lds_load(uint32_t addr) { return *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr)); }
 __device__ __forceinline__ u32x4 lds_load16(uint32_t addr) { return *reinterpret_cast<lds_u32x4*>(static_cast<uintptr_t>(addr)); }
+__device__ __forceinline__ void lds_store(uint32_t addr, uint32_t v) {
+    *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(static_cast<uintptr_t>(addr)) = v;
+}
 
 // s_waitcnt vmcnt(min(n, 63)): the immediate picked by a balanced scalar
 // branch tree (n is wave-uniform).

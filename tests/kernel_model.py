@@ -174,6 +174,48 @@ def image(P: int = 1) -> list[int]:
     return _IMG_CACHE[P]
 
 
+KBASIS_ROWS = 9
+KINIT_DWORD = free_col(KINIT_COL) // 4      # 58
+KCINV_DWORD = free_col(KCINV_COL) // 4      # 60 (CINV n < 256)
+
+
+def table_basis(P: int) -> list[int]:
+    """The lean kernel's 9 x 64-dword table basis (HostTables::basis,
+    csrc/crc32_kernels.hip): row b < 8 = image row 2^b with the INIT / CINV dwords
+    zeroed (every other column is GF(2)-linear in the row index), row 8 =
+    INIT[0..31] | CINV[0..31]."""
+    img = image(P)
+    skip = (KINIT_DWORD, KCINV_DWORD, KCINV_DWORD + 2)
+    B = [0 if d in skip else img[64 * (1 << b) + d] for b in range(8) for d in range(64)]
+    return B + INIT[:32] + CINV[:32]
+
+
+def image_from_basis(B: list[int]) -> list[int]:
+    """crc32_lean.hip's in-LDS rebuild: row j = XOR of basis rows b with bit b of j
+    set; INIT / CINV rows < 32 from basis row 8 (rows >= 32 of those columns, and
+    CINV n >= 256, are never read by that kernel)."""
+    img = [0] * (256 * 64)
+    for j in range(256):
+        row = [0] * 64
+        for b in range(8):
+            if (j >> b) & 1:
+                row = [x ^ y for x, y in zip(row, B[64 * b:64 * b + 64])]
+        if j < 32:
+            row[KINIT_DWORD] = B[512 + j]
+            row[KCINV_DWORD] = B[544 + j]
+        img[64 * j:64 * j + 64] = row
+    return img
+
+
+_RB_CACHE: dict[int, list[int]] = {}
+
+
+def rebuilt_image(P: int) -> list[int]:
+    if P not in _RB_CACHE:
+        _RB_CACHE[P] = image_from_basis(table_basis(P))
+    return _RB_CACHE[P]
+
+
 def v_perm(s0: int, s1: int, sel: int) -> int:
     """V_PERM_B32: byte_permute({S0, S1}, sel); S1 = bytes 0-3, S0 = bytes 4-7."""
     data = (s1 & 0xFFFFFFFF) | ((s0 & 0xFFFFFFFF) << 32)
@@ -384,7 +426,7 @@ def lean_group(arena: bytes, offs: list[int], lens: list[int], P: int, check_ban
     lane corrections, lane XOR, tz correction.  Returns the finalized CRCs."""
     npk = 64 // P
     assert len(offs) == npk
-    img = image(P)
+    img = rebuilt_image(P)                         # the image as the kernel rebuilds it in LDS
     wins = [stream_window(offs[j], lens[j]) for j in range(npk)]   # (lz, nb, tz)
     stages = max(1, max(((nb + P - 1) // P) for _, nb, _ in wins))
     regs = [0] * 64
@@ -393,7 +435,7 @@ def lean_group(arena: bytes, offs: list[int], lens: list[int], P: int, check_ban
         j, k = divmod(lane, P)
         lz, nb, tz = wins[j]
         if k == rot[j]:
-            regs[lane] = INIT[lz]
+            regs[lane] = img[init_addr(lz) // 4]
     for s in range(stages):
         slot = bytearray(2048)
         for lane in range(64):                     # producer: own packet, pieces k and P + k

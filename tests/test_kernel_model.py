@@ -181,3 +181,16 @@ def test_lean_group_model_matches_oracle(P):
             pkt = arena[offs[j]:offs[j] + lens[j]]
             exp = int.from_bytes((zlib.crc32(pkt) & 0xFFFFFFFF).to_bytes(4, "little"), "big")
             assert got[j] == exp, (trial, j, lens[j], offs[j])
+
+
+@pytest.mark.parametrize("P", [4, 8])
+def test_image_from_basis(P):
+    """The lean kernel rebuilds its LDS image from a 9-row basis: equal to the
+    host image at every dword it can read (all but INIT/CINV rows >= 32 and CINV
+    n >= 256)."""
+    img, rb = km.image(P), km.rebuilt_image(P)
+    for j in range(256):
+        for d in range(64):
+            if d == km.KCINV_DWORD + 2 or (d in (km.KINIT_DWORD, km.KCINV_DWORD) and j >= 32):
+                continue
+            assert rb[64 * j + d] == img[64 * j + d], (j, d)

@@ -1,0 +1,12 @@
+set -o pipefail
+out=gpurun_out/g20
+mkdir -p $out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+tools/gpu_step.sh 400 $out/pytest.log python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread || exit 1
+grep -q " passed" $out/pytest.log || exit 1
+tools/gpu_step.sh 200 $out/smoke.log python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
+tools/gpu_step.sh 300 $out/bench.json python bench.py || exit 1
+tools/gpu_step.sh 300 $out/bench_s1.json python bench.py --streams 1 --no-cpu-baseline || exit 1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/bench_trace -o run --output-format csv -- python3 bench.py --steps 50 --warmup 10 --cpu-seconds 2 > $out/bench_under_rocprof.json 2> $out/bench_under_rocprof.err || exit 1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $out/fetch -o run --output-format csv -- python3 tools/profile_one.py --reps 20 --probe > $out/fetch.log 2>&1 || exit 1
+python3 tools/traffic.py $out/fetch 78643200 $out/traffic_cfg2.json > /dev/null
