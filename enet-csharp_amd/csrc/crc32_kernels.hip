@@ -7,8 +7,10 @@
 // algebraically identical route.
 //
 // Kernels:
-//   * crc32_stream_kernel -- the hot path: persistent, LDS-DMA streamed, strided
-//     lane->block assignment (4/8/16 lanes per packet), any alignment.
+//   * crc32_lean_kernel (crc32_lean.hip) -- the hot path for 4 and 8 lanes per
+//     packet: persistent, LDS-DMA streamed, strided lanes, table rebuilt in LDS;
+//   * crc32_stream_kernel -- the same arithmetic with per-lane-run staging: 16
+//     lanes per packet and the sweep geometries (enet_hip_set_kernel_path).
 //   * crc32_direct_kernel -- general fallback (any lanes per packet): blocks
 //     loaded into VGPRs, contiguous segments joined by the carry-combine.
 //   * crc32_gather_kernel -- one lane per DGRAM over an ENetBuffer gather list.
