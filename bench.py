@@ -41,7 +41,7 @@ def parse(argv=None):
     ap.add_argument("--rotate", type=int, default=5, help="distinct resident batches cycled through")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per packet (0 = library default)")
     ap.add_argument("--wgs", type=int, default=0, help="workgroups per CU (0 = library default)")
-    ap.add_argument("--streams", type=int, default=4,
+    ap.add_argument("--streams", type=int, default=6,
                     help="HIP streams the captured steps rotate over: batches are independent, so a "
                          "launch's prologue overlaps the previous launch's tail (1 = serial)")
     ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "small"],

@@ -88,6 +88,16 @@ namespace enet
                                                               uint* segLengths, uint* segFirst, nuint dgramCount,
                                                               uint* output, IntPtr stream);
 
+        // receive-side fragment reassembly, c/protocol.cs:529-637
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_fragment_reassemble_device(IntPtr ctx, byte* bytes, ulong* cmdOffsets,
+                                                                     uint* cmdAvail, int* slots, nuint count,
+                                                                     uint maximumPacketSize, byte* msgBytes,
+                                                                     ulong* msgOffsets, uint* msgLengths,
+                                                                     uint* msgFragCounts, uint* fragments,
+                                                                     uint wordsPerMsg, uint* remaining,
+                                                                     nuint slotCount, sbyte* status, IntPtr stream);
+
         [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
         public static extern int enet_hip_crc32_batch_multi(IntPtr* contexts, int contextCount, byte* bytes,
                                                             nuint byteCount, ulong* offsets, uint* lengths,
@@ -174,6 +184,16 @@ namespace enet
             => EnetHip.Check("enet_hip_verify_batch_device",
                 EnetHipNative.enet_hip_verify_batch_device(Handle, bytes, offsets, lengths, slotOffsets, connectIds,
                     count, ok, computed, stream));
+
+        public void FragmentReassembleDevice(byte* bytes, ulong* cmdOffsets, uint* cmdAvail, int* slots, nuint count,
+                                             uint maximumPacketSize, byte* msgBytes, ulong* msgOffsets,
+                                             uint* msgLengths, uint* msgFragCounts, uint* fragments, uint wordsPerMsg,
+                                             uint* remaining, nuint slotCount, sbyte* status,
+                                             IntPtr stream = default)
+            => EnetHip.Check("enet_hip_fragment_reassemble_device",
+                EnetHipNative.enet_hip_fragment_reassemble_device(Handle, bytes, cmdOffsets, cmdAvail, slots, count,
+                    maximumPacketSize, msgBytes, msgOffsets, msgLengths, msgFragCounts, fragments, wordsPerMsg,
+                    remaining, slotCount, status, stream));
 
         public void Synchronize() => EnetHip.Check("enet_hip_synchronize", EnetHipNative.enet_hip_synchronize(Handle));
 

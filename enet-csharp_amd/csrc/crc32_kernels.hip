@@ -32,6 +32,7 @@
 #include "crc32_lean.hpp"
 #include "crc32_stream_common.hpp"
 #include "enet_hip.h"
+#include "fragment_kernels.hpp"
 
 namespace enethip {
 
@@ -874,6 +875,11 @@ struct enet_hip_context {
     size_t d_bytes_cap = 0;
     uint8_t* d_meta = nullptr;  // off | len | out
     size_t d_meta_cap = 0;
+    // fragment reassembly claim words (all ~0 between calls)
+    uint32_t* d_claim = nullptr;
+    size_t d_claim_cap = 0;     // words
+    uint8_t* d_frag_desc = nullptr;   // copy descriptors, 28 B per command
+    size_t d_frag_desc_cap = 0;
 };
 
 namespace {
@@ -1217,6 +1223,8 @@ int enet_hip_context_destroy(enet_hip_context* ctx) {
     (void)hipFree(ctx->d_basis);
     (void)hipFree(ctx->d_bytes);
     (void)hipFree(ctx->d_meta);
+    (void)hipFree(ctx->d_claim);
+    (void)hipFree(ctx->d_frag_desc);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return 0;
@@ -1300,6 +1308,44 @@ int enet_hip_crc32_gather_device(enet_hip_context* ctx, const uint8_t* bytes, co
     hipLaunchKernelGGL(crc32_gather_kernel, dim3(grid), dim3(kThreads), kLdsTableBytes,
                        stream ? static_cast<hipStream_t>(stream) : ctx->stream, ga, tables_of(ctx));
     return herr(hipGetLastError());
+}
+
+int enet_hip_fragment_reassemble_device(enet_hip_context* ctx, const uint8_t* bytes, const uint64_t* cmdOffsets,
+                                        const uint32_t* cmdAvail, const int32_t* slots, size_t count,
+                                        uint32_t maximumPacketSize, uint8_t* msgBytes, const uint64_t* msgOffsets,
+                                        const uint32_t* msgLengths, const uint32_t* msgFragCounts, uint32_t* fragments,
+                                        uint32_t wordsPerMsg, uint32_t* remaining, size_t slotCount, int8_t* status,
+                                        void* stream) {
+    if (!ctx) return -static_cast<int>(hipErrorInvalidValue);
+    if (count == 0) return 0;
+    if (!bytes || !cmdOffsets || !cmdAvail || !slots || !status || (slotCount && (!msgBytes || !msgOffsets ||
+        !msgLengths || !msgFragCounts || !fragments || !remaining || wordsPerMsg == 0)))
+        return -static_cast<int>(hipErrorInvalidValue);
+    if (slotCount > (static_cast<size_t>(1) << 31) || wordsPerMsg > (1u << 15)) return -static_cast<int>(hipErrorInvalidValue);
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ENH_CHECK(hipSetDevice(ctx->device));
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    const size_t need = std::max<size_t>(1, slotCount * wordsPerMsg * 32u);
+    if (need > ctx->d_claim_cap) {
+        // a fresh claim area, ~0 everywhere; the release kernel restores that after each call
+        ENH_CHECK(hipStreamSynchronize(st));
+        (void)hipFree(ctx->d_claim);
+        ctx->d_claim = nullptr;
+        ctx->d_claim_cap = 0;
+        ENH_CHECK(hipMalloc(reinterpret_cast<void**>(&ctx->d_claim), need * 4));
+        ctx->d_claim_cap = need;
+        ENH_CHECK(hipMemsetAsync(ctx->d_claim, 0xFF, need * 4, st));
+    }
+    int rc;
+    if ((rc = ensure(&ctx->d_frag_desc, &ctx->d_frag_desc_cap, count * 28 + 64))) return rc;
+    uint64_t* d_src = reinterpret_cast<uint64_t*>(ctx->d_frag_desc);
+    uint64_t* d_dst = d_src + count;
+    uint64_t* d_cl = d_dst + count;
+    uint32_t* d_len = reinterpret_cast<uint32_t*>(d_cl + count);
+    FragArgs a{bytes, cmdOffsets, cmdAvail, slots, count, maximumPacketSize, msgBytes, msgOffsets, msgLengths,
+               msgFragCounts, fragments, wordsPerMsg, remaining, slotCount, status, ctx->d_claim,
+               d_src, d_dst, d_len, d_cl};
+    return fragment_reassemble_launch(a, ctx->num_cus, st);
 }
 
 int enet_hip_crc32_batch_host(enet_hip_context* ctx, const uint8_t* bytes, size_t byteCount,

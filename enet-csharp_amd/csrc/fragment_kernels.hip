@@ -1,0 +1,180 @@
+// fragment_kernels.hip -- batched fragment reassembly for gfx950 (MI355X): the
+// data movement of ENet's receive-side fragment handler for a whole batch of
+// SEND_FRAGMENT commands.
+// Reference: /root/reference/enet-csharp/ENet/c/protocol.cs:529-637
+// (enet_protocol_handle_send_fragment); the send-side split that produces the
+// fragments is c/peer.cs:130-196; the command layout include/protocol.cs:156-165.
+//
+// What stays with the caller: the channel / sequence-window search that finds
+// (or creates) the reassembly command (protocol.cs:540-545, 553-617).  The caller
+// passes, per command, the reassembly slot it matched.  What runs here, per
+// command, in the reference's order:
+//   * the -1 checks of protocol.cs:546-552 and 571-577, and the startCommand
+//     consistency check of 598-601 (totalLength / fragmentCount vs the slot);
+//   * duplicate suppression by the slot's fragment bitmap (619-623), first
+//     command in batch order wins, exactly as the sequential reference;
+//   * fragmentsRemaining countdown (621) and the memcpy of the fragment data to
+//     packet->data + fragmentOffset, length clamped as at 625-626.
+// Memory: HBM-bound byte copy, 1 byte read + 1 byte written per fragment byte.
+//
+// Three launches on one stream:
+//   1. frag_claim_kernel  (thread per command): parse, validate, atomicMin of the
+//      command index into the claim word of its (slot, fragmentNumber);
+//   2. frag_decide_kernel (thread per command): the claim winner tests-and-sets
+//      the bitmap bit (a bit set by an earlier batch = duplicate), decrements
+//      remaining and writes a copy descriptor;
+//   3. frag_copy_kernel   (wave per two commands): the copies with 16-byte lanes, and the
+//      claim words back to ~0.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "fragment_kernels.hpp"
+
+namespace enethip {
+
+namespace {
+
+constexpr uint32_t kMaxFragmentCount = 1024u * 1024u;   // ENET_PROTOCOL_MAXIMUM_FRAGMENT_COUNT, include/protocol.cs:19
+constexpr uint32_t kCmdBytes = 24u;                      // sizeof(ENetProtocolSendFragment)
+
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+
+struct Frag {
+    uint32_t len, count, number, total, offset;
+    int32_t slot;
+    bool valid;
+};
+
+// Parse + validate command i (the -1 paths of protocol.cs:546-552, 571-577, 598-601).
+__device__ __forceinline__ Frag parse(const FragArgs& a, uint64_t i) {
+    Frag f{};
+    f.slot = a.slots[i];
+    f.valid = false;
+    if (f.slot < 0 || static_cast<uint64_t>(f.slot) >= a.slot_count) return f;
+    // the 24-byte command as two overlapping unaligned 16-byte loads (bytes 0-15, 8-23)
+    const uint8_t* c = a.bytes + a.cmd_off[i];
+    u32x4v h0, h1;
+    __builtin_memcpy(&h0, c, 16);
+    __builtin_memcpy(&h1, c + 8, 16);
+    f.len = __builtin_bswap32(h0.y) & 0xFFFFu;            // sendFragment.dataLength, bytes 6-7
+    f.count = __builtin_bswap32(h1.x);                    // bytes 8-11
+    f.number = __builtin_bswap32(h1.y);
+    f.total = __builtin_bswap32(h1.z);
+    f.offset = __builtin_bswap32(h1.w);
+    if (f.len == 0 || f.len > a.max_packet || f.len > a.cmd_avail[i]) return f;                 // 546-552
+    if (f.count > kMaxFragmentCount || f.number >= f.count || f.total > a.max_packet || f.total < f.count ||
+        f.offset >= f.total || f.len > f.total - f.offset)
+        return f;                                                                              // 571-577
+    if (f.total != a.msg_len[f.slot] || f.count != a.msg_count[f.slot]) return f;              // 598-601
+    if (f.count > 32u * a.words) return f;               // bitmap smaller than fragmentCount bits: rejected
+    f.valid = true;
+    return f;
+}
+
+__device__ __forceinline__ uint64_t claim_index(const FragArgs& a, const Frag& f) {
+    return (static_cast<uint64_t>(f.slot) * a.words << 5) + f.number;
+}
+
+__global__ void __launch_bounds__(256) frag_claim_kernel(FragArgs a) {
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+        const Frag f = parse(a, i);
+        if (f.valid) atomicMin(a.claim + claim_index(a, f), static_cast<uint32_t>(i));
+        a.status[i] = f.valid ? 0 : (f.slot < 0 ? 0 : -1);
+    }
+}
+
+// Thread per command: the claim winner tests-and-sets the bitmap bit (a bit set
+// by an earlier batch = duplicate) and decrements remaining; every command gets a
+// copy descriptor (len 0 = nothing to copy) for the copy kernel.
+__global__ void __launch_bounds__(256) frag_decide_kernel(FragArgs a) {
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+        const Frag f = parse(a, i);
+        uint32_t len = 0;
+        uint64_t src = 0, dst = 0, cidx = ~0ull;
+        if (f.valid) {
+            cidx = claim_index(a, f);
+            if (a.claim[cidx] == static_cast<uint32_t>(i)) {             // first command of the batch for it
+                const uint32_t bit = 1u << (f.number & 31u);
+                const uint32_t old =
+                    atomicOr(a.fragments + static_cast<uint64_t>(f.slot) * a.words + (f.number >> 5), bit);   // 619, 623
+                if (!(old & bit)) {
+                    atomicSub(a.remaining + f.slot, 1u);                 // --fragmentsRemaining (621)
+                    a.status[i] = 1;
+                    len = min(f.len, a.msg_len[f.slot] - f.offset);      // clamp (625-626)
+                    src = a.cmd_off[i] + kCmdBytes;
+                    dst = a.msg_off[f.slot] + f.offset;
+                }
+            }
+        }
+        a.copy_src[i] = src;
+        a.copy_dst[i] = dst;
+        a.copy_len[i] = len;
+        a.copy_claim[i] = cidx;
+    }
+}
+
+// Wave per two commands (i, i + wstride, their copies overlapped):
+// memcpy(packet->data + fragmentOffset, command + 24, length) (protocol.cs:628-630)
+// with 16-byte lanes; lane 0 also returns each command's claim word to ~0 (every
+// decide read is done).
+__device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint32_t L, uint32_t x) {
+    if (x + 16u <= L) {
+        u32x4v v;
+        __builtin_memcpy(&v, src + x, 16);                // unaligned 16-byte access (gfx950 unaligned mode)
+        __builtin_memcpy(dst + x, &v, 16);
+    } else {
+        for (uint32_t b = x; b < L; ++b) dst[b] = src[b];
+    }
+}
+
+__global__ void __launch_bounds__(256) frag_copy_kernel(FragArgs a) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t wstride = static_cast<uint64_t>(gridDim.x) * (blockDim.x >> 6);
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6); i < a.n;
+         i += 2 * wstride) {
+        const uint64_t j = i + wstride;
+        const bool hj = j < a.n;
+        const uint32_t Li = a.copy_len[i], Lj = hj ? a.copy_len[j] : 0u;
+        const uint64_t ci = a.copy_claim[i], cj = hj ? a.copy_claim[j] : ~0ull;
+        const uint8_t* si = a.bytes + a.copy_src[i];
+        const uint8_t* sj = a.bytes + (hj ? a.copy_src[j] : 0u);
+        uint8_t* di = a.msg_bytes + a.copy_dst[i];
+        uint8_t* dj = a.msg_bytes + (hj ? a.copy_dst[j] : 0u);
+        if (lane == 0) {
+            if (ci != ~0ull) a.claim[ci] = ~0u;
+            if (cj != ~0ull) a.claim[cj] = ~0u;
+        }
+        const uint32_t L = max(Li, Lj);
+        for (uint32_t x = 16u * lane; x < L; x += 1024u) {
+            // loads of both commands first, then the stores
+            const bool fi = x + 16u <= Li, fj = x + 16u <= Lj;
+            u32x4v vi = {0, 0, 0, 0}, vj = {0, 0, 0, 0};
+            if (fi) __builtin_memcpy(&vi, si + x, 16);
+            if (fj) __builtin_memcpy(&vj, sj + x, 16);
+            if (fi) __builtin_memcpy(di + x, &vi, 16);
+            else if (x < Li) copy_span(si, di, Li, x);
+            if (fj) __builtin_memcpy(dj + x, &vj, 16);
+            else if (x < Lj) copy_span(sj, dj, Lj, x);
+        }
+    }
+}
+
+}  // namespace
+
+int fragment_reassemble_launch(const FragArgs& a, int num_cus, hipStream_t st) {
+    if (a.n == 0) return 0;
+    const uint64_t cap = static_cast<uint64_t>(num_cus) * 8u;
+    const unsigned g_thr = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>((a.n + 255) / 256, cap)));
+    const unsigned g_wave = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>((a.n + 3) / 4, cap)));
+    hipLaunchKernelGGL(frag_claim_kernel, dim3(g_thr), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(frag_decide_kernel, dim3(g_thr), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(frag_copy_kernel, dim3(g_wave), dim3(256), 0, st, a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : -static_cast<int>(e);
+}
+
+}  // namespace enethip

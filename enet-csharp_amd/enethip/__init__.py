@@ -31,7 +31,7 @@ EXPORTED_SYMBOLS = (
     "enet_hip_crc32_gather_device", "enet_hip_crc32_batch_multi", "enet_hip_device_alloc",
     "enet_hip_device_free", "enet_hip_host_alloc", "enet_hip_host_free", "enet_hip_memcpy_h2d",
     "enet_hip_memcpy_d2h", "enet_hip_synchronize", "enet_hip_read_probe_device", "enet_hip_set_kernel_path",
-    "enet_hip_diag_ablation", "enet_hip_diag_trace",
+    "enet_hip_diag_ablation", "enet_hip_diag_trace", "enet_hip_fragment_reassemble_device",
 )
 
 
@@ -104,6 +104,9 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.enet_hip_read_probe_device.argtypes = [vp, vp, sz, vp, vp]
     L.enet_hip_synchronize.restype = i32
     L.enet_hip_synchronize.argtypes = [vp]
+    L.enet_hip_fragment_reassemble_device.restype = i32
+    L.enet_hip_fragment_reassemble_device.argtypes = [vp, vp, vp, vp, vp, sz, u32, vp, vp, vp, vp, vp, u32, vp, sz,
+                                                      vp, vp]
     if path is None:
         _lib = L
     return L
@@ -213,6 +216,15 @@ class Context:
         _check("enet_hip_crc32_gather_device", self.lib.enet_hip_crc32_gather_device(
             self.handle, _ptr(d_bytes), _ptr(d_seg_off), _ptr(d_seg_len), _ptr(d_seg_first), int(n_dgrams),
             _ptr(d_out), stream or None))
+
+    def fragment_reassemble_device(self, d_bytes, d_cmd_off, d_cmd_avail, d_slots, n: int, max_packet: int,
+                                   d_msg_bytes, d_msg_off, d_msg_len, d_msg_count, d_fragments, words: int,
+                                   d_remaining, n_slots: int, d_status, stream: int = 0) -> None:
+        """Batched fragment reassembly (c/protocol.cs:529-637): see enet_hip.h."""
+        _check("enet_hip_fragment_reassemble_device", self.lib.enet_hip_fragment_reassemble_device(
+            self.handle, _ptr(d_bytes), _ptr(d_cmd_off), _ptr(d_cmd_avail), _ptr(d_slots), int(n), int(max_packet),
+            _ptr(d_msg_bytes), _ptr(d_msg_off), _ptr(d_msg_len), _ptr(d_msg_count), _ptr(d_fragments), int(words),
+            _ptr(d_remaining), int(n_slots), _ptr(d_status), stream or None))
 
     def read_probe_device(self, d_bytes, nbytes: int, d_sink, stream: int = 0) -> None:
         _check("enet_hip_read_probe_device", self.lib.enet_hip_read_probe_device(

@@ -132,3 +132,83 @@ def cfg5(messages: int = 4096, message_bytes: int = 65536, mtu: int = 1392) -> G
     total = int(seg_len.astype(np.uint64).sum())
     return GatherBatch(payload, seg_off, seg_len, seg_first, total,
                        f"cfg5: {messages} x {message_bytes} B -> {n} DGRAMs")
+
+
+@dataclass
+class FragmentBatch:
+    """Received SEND_FRAGMENT DGRAMs ready for reassembly: DGRAM = [4 B header]
+    [4 B checksum slot][24 B ENetProtocolSendFragment, network order][data].
+    cmd_off[i] points at the command, cmd_avail[i] = data bytes after it, slots[i]
+    = the message (reassembly slot) it belongs to.  msg_len / msg_count describe
+    the slots; `messages` holds the original message bytes (the round-trip check)."""
+    payload: np.ndarray
+    cmd_off: np.ndarray     # uint64
+    cmd_avail: np.ndarray   # uint32
+    slots: np.ndarray       # int32
+    msg_len: np.ndarray     # uint32
+    msg_count: np.ndarray   # uint32
+    messages: list
+    data_bytes: int
+    name: str
+
+    @property
+    def n(self) -> int:
+        return len(self.cmd_off)
+
+
+def send_fragment_cmd(count: int, number: int, total: int, offset: int, length: int, seq: int = 1) -> bytes:
+    """include/protocol.cs:156-165 as c/peer.cs:183-193 fills it (network order)."""
+    hdr = bytes([0x80 | 8, 0]) + (seq & 0xFFFF).to_bytes(2, "big")    # SEND_FRAGMENT | ACKNOWLEDGE, channel 0
+    return (hdr + (seq & 0xFFFF).to_bytes(2, "big") + length.to_bytes(2, "big") + count.to_bytes(4, "big") +
+            number.to_bytes(4, "big") + total.to_bytes(4, "big") + offset.to_bytes(4, "big"))
+
+
+def fragments(message_lens, mtu: int = 1392, seed: int = SEED_PAYLOAD, shuffle: bool = True,
+              duplicates: float = 0.0, name: str = "fragments") -> FragmentBatch:
+    """Split messages as c/peer.cs:130-196 does (fragmentLength = mtu - 4 - 24 - 4 with
+    checksums on, the last fragment shorter), one DGRAM per fragment, in shuffled
+    arrival order, with a fraction of retransmitted duplicates."""
+    frag = mtu - 4 - 24 - 4
+    rng = np.random.default_rng(seed)
+    lens = [int(x) for x in message_lens]
+    total_data = sum(lens)
+    body = payload_bytes(total_data, seed=seed)
+    messages, pieces = [], []
+    pos = 0
+    for m, L in enumerate(lens):
+        messages.append(body[pos:pos + L])
+        cnt = (L + frag - 1) // frag
+        for k in range(cnt):
+            off = k * frag
+            pieces.append((m, cnt, k, L, off, min(frag, L - off), pos + off))
+        pos += L
+    order = rng.permutation(len(pieces)) if shuffle else np.arange(len(pieces))
+    order = list(order)
+    ndup = int(duplicates * len(pieces))
+    if ndup:
+        dup = rng.choice(len(pieces), ndup, replace=True)
+        for d in dup:
+            order.insert(int(rng.integers(0, len(order) + 1)), int(d))
+    n = len(order)
+    sizes = np.array([32 + pieces[i][5] for i in order], dtype=np.uint64)
+    starts = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+    arena = np.zeros(int(sizes.sum()) + 64, dtype=np.uint8)
+    cmd_off = starts + np.uint64(8)
+    cmd_avail = np.zeros(n, dtype=np.uint32)
+    slots = np.zeros(n, dtype=np.int32)
+    for i, pi in enumerate(order):
+        m, cnt, k, L, off, ln, src = pieces[pi]
+        a = int(starts[i])
+        arena[a + 4:a + 8] = np.frombuffer(np.uint32(CONNECT_ID).tobytes(), dtype=np.uint8)
+        arena[a + 8:a + 32] = np.frombuffer(send_fragment_cmd(cnt, k, L, off, ln), dtype=np.uint8)
+        arena[a + 32:a + 32 + ln] = body[src:src + ln]
+        cmd_avail[i] = ln
+        slots[i] = m
+    msg_count = np.array([(L + frag - 1) // frag for L in lens], dtype=np.uint32)
+    return FragmentBatch(arena, cmd_off, cmd_avail, slots, np.array(lens, dtype=np.uint32), msg_count, messages,
+                         total_data, name)
+
+
+def cfg5_fragments(messages: int = 4096, message_bytes: int = 65536) -> FragmentBatch:
+    """cfg5's 4096 x 64 KiB messages as received fragment DGRAMs (200 704 commands)."""
+    return fragments([message_bytes] * messages, shuffle=True, name=f"cfg5 receive: {messages} x {message_bytes} B")

@@ -117,6 +117,35 @@ ENET_HIP_API int enet_hip_crc32_gather_device(enet_hip_context* ctx, const uint8
                                               const uint32_t* segFirst, size_t dgramCount, uint32_t* out,
                                               void* stream);
 
+/* ---- batched fragment reassembly (receive side, c/protocol.cs:529-637) ----
+ * The data movement of enet_protocol_handle_send_fragment for a batch of
+ * SEND_FRAGMENT commands; replaces its per-command validation, bitmap update,
+ * fragmentsRemaining countdown and memcpy (protocol.cs:546-552, 566-634).  The
+ * caller keeps the channel / sequence-window search (protocol.cs:540-545,
+ * 553-617) and passes the reassembly slot it matched for each command.
+ *   command i : the 24-byte ENetProtocolSendFragment at bytes[cmdOffsets[i]]
+ *               (network byte order, include/protocol.cs:156-165), followed by its
+ *               data; cmdAvail[i] = bytes available after the command;
+ *   slots[i]  : reassembly slot of command i, or -1 to skip it (status 0);
+ *   slot s    : packet data msgBytes[msgOffsets[s] .. +msgLengths[s]) (totalLength
+ *               bytes), fragmentCount msgFragCounts[s], received-fragment bitmap
+ *               fragments[s*wordsPerMsg .. +wordsPerMsg), fragmentsRemaining
+ *               remaining[s].
+ * status[i] = -1 where the reference returns -1 (or the bitmap is shorter than
+ * fragmentCount bits), 1 when the data was copied, 0 for a skipped command or a
+ * duplicate: a fragment already in the bitmap, or one an earlier command of the
+ * same batch carries (batch order = the reference's sequential order).  A message
+ * is complete when remaining[s] reaches 0 (protocol.cs:632).  Device pointers,
+ * async on `stream`; calls on one context must not overlap (shared scratch). */
+ENET_HIP_API int enet_hip_fragment_reassemble_device(enet_hip_context* ctx, const uint8_t* bytes,
+                                                     const uint64_t* cmdOffsets, const uint32_t* cmdAvail,
+                                                     const int32_t* slots, size_t count,
+                                                     uint32_t maximumPacketSize, uint8_t* msgBytes,
+                                                     const uint64_t* msgOffsets, const uint32_t* msgLengths,
+                                                     const uint32_t* msgFragCounts, uint32_t* fragments,
+                                                     uint32_t wordsPerMsg, uint32_t* remaining,
+                                                     size_t slotCount, int8_t* status, void* stream);
+
 /* ---- multi-GPU: independent contiguous shards, no collective ----
  * Packets [i*count/k, (i+1)*count/k) go to contexts[i]; each shard's bytes are
  * copied to its device, checksummed and the CRCs copied back into out[].

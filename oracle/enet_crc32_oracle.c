@@ -152,3 +152,47 @@ void oracle_verify_batch(const uint8_t* bytes, const uint64_t* off, const uint32
         ok[i] = (c == desired) ? 1 : 0;
     }
 }
+
+/* Batched fragment reassembly, sequential, as c/protocol.cs:529-637
+ * (enet_protocol_handle_send_fragment) treats each command once the caller has
+ * matched its reassembly slot: the -1 checks of 546-552 / 571-577 / 598-601, the
+ * bitmap duplicate test (619), --fragmentsRemaining (621), the bit set (623) and
+ * the memcpy with the length clamp (625-630).  Command fields are network order
+ * (include/protocol.cs:156-165).  status: -1 rejected, 0 skipped/duplicate, 1 copied. */
+static uint32_t be16_(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
+static uint32_t be32_(const uint8_t* p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+void oracle_fragment_reassemble(const uint8_t* bytes, const uint64_t* cmd_off, const uint32_t* cmd_avail,
+                                const int32_t* slots, size_t n, uint32_t max_packet, uint8_t* msg_bytes,
+                                const uint64_t* msg_off, const uint32_t* msg_len, const uint32_t* msg_count,
+                                uint32_t* fragments, uint32_t words, uint32_t* remaining, size_t slot_count,
+                                int8_t* status) {
+    for (size_t i = 0; i < n; ++i) {
+        int32_t s = slots[i];
+        if (s < 0) { status[i] = 0; continue; }
+        if ((size_t)s >= slot_count) { status[i] = -1; continue; }
+        const uint8_t* c = bytes + cmd_off[i];
+        uint32_t fragmentLength = be16_(c + 6);
+        uint32_t fragmentCount = be32_(c + 8), fragmentNumber = be32_(c + 12);
+        uint32_t totalLength = be32_(c + 16), fragmentOffset = be32_(c + 20);
+        if (fragmentLength == 0 || fragmentLength > max_packet || fragmentLength > cmd_avail[i]) { status[i] = -1; continue; }
+        if (fragmentCount > 1024u * 1024u || fragmentNumber >= fragmentCount || totalLength > max_packet ||
+            totalLength < fragmentCount || fragmentOffset >= totalLength || fragmentLength > totalLength - fragmentOffset) {
+            status[i] = -1;
+            continue;
+        }
+        if (totalLength != msg_len[s] || fragmentCount != msg_count[s]) { status[i] = -1; continue; }
+        if (fragmentCount > 32u * words) { status[i] = -1; continue; }
+        uint32_t* fr = fragments + (size_t)s * words;
+        if ((fr[fragmentNumber / 32] & (1u << (fragmentNumber % 32))) == 0) {
+            --remaining[s];
+            fr[fragmentNumber / 32] |= 1u << (fragmentNumber % 32);
+            if (fragmentOffset + fragmentLength > msg_len[s]) fragmentLength = msg_len[s] - fragmentOffset;
+            memcpy(msg_bytes + msg_off[s] + fragmentOffset, c + 24, fragmentLength);
+            status[i] = 1;
+        } else {
+            status[i] = 0;
+        }
+    }
+}

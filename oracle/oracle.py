@@ -79,6 +79,9 @@ class OracleLib:
         L.oracle_crc32_gather.argtypes = [vp, vp, vp, vp, sz, vp]
         L.oracle_verify_batch.restype = None
         L.oracle_verify_batch.argtypes = [vp, vp, vp, vp, vp, sz, vp, vp]
+        L.oracle_fragment_reassemble.restype = None
+        L.oracle_fragment_reassemble.argtypes = [vp, vp, vp, vp, sz, ctypes.c_uint32, vp, vp, vp, vp, vp,
+                                                 ctypes.c_uint32, vp, sz, vp]
         L.oracle_crc_table.restype = None
         L.oracle_crc_table.argtypes = [vp]
 
@@ -133,3 +136,23 @@ class OracleLib:
         self.lib.oracle_verify_batch(self._p(payload), self._p(off), self._p(lens), self._p(slot_off),
                                      self._p(connect_id), n, self._p(ok), self._p(comp))
         return ok, comp
+
+
+def fragment_reassemble(lib: "OracleLib", payload, cmd_off, cmd_avail, slots, max_packet, msg_bytes, msg_off,
+                        msg_len, msg_count, fragments, words, remaining):
+    """Sequential reference (c/protocol.cs:529-637) on numpy arrays; msg_bytes,
+    fragments and remaining are updated in place; returns the int8 status array."""
+    n = len(cmd_off)
+    status = np.zeros(n, dtype=np.int8)
+    arrs = [np.ascontiguousarray(payload, dtype=np.uint8), np.ascontiguousarray(cmd_off, dtype=np.uint64),
+            np.ascontiguousarray(cmd_avail, dtype=np.uint32), np.ascontiguousarray(slots, dtype=np.int32)]
+    for a, dt in ((msg_bytes, np.uint8), (fragments, np.uint32), (remaining, np.uint32)):
+        assert a.dtype == dt and a.flags["C_CONTIGUOUS"]
+    mo = np.ascontiguousarray(msg_off, dtype=np.uint64)
+    ml = np.ascontiguousarray(msg_len, dtype=np.uint32)
+    mc = np.ascontiguousarray(msg_count, dtype=np.uint32)
+    lib.lib.oracle_fragment_reassemble(arrs[0].ctypes.data, arrs[1].ctypes.data, arrs[2].ctypes.data,
+                                       arrs[3].ctypes.data, n, int(max_packet), msg_bytes.ctypes.data,
+                                       mo.ctypes.data, ml.ctypes.data, mc.ctypes.data, fragments.ctypes.data,
+                                       int(words), remaining.ctypes.data, len(ml), status.ctypes.data)
+    return status

@@ -1,0 +1,89 @@
+"""GPU parity of enet_hip_fragment_reassemble_device (c/protocol.cs:529-637)
+against the sequential oracle: status, reassembled bytes, bitmaps and
+fragmentsRemaining bit-exact, with duplicates inside and across batches and every
+-1 path; plus the cfg5-sized round trip (200 704 fragments)."""
+import numpy as np
+import pytest
+
+import oracle
+from enethip import workloads
+from test_fragments import MAXP, run_oracle, state
+from test_gpu_parity import ctx, dev  # noqa: F401  (fixture)
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def dev_i32(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.int32)).cuda()
+
+
+def run_gpu(ctx, fb, st, sel=None, payload=None):  # noqa: F811
+    sel = np.arange(fb.n) if sel is None else sel
+    p = fb.payload if payload is None else payload
+    d = dict(msg_bytes=dev(st["msg_bytes"]), fragments=dev(st["fragments"]), remaining=dev(st["remaining"]))
+    status = torch.zeros(len(sel), dtype=torch.int8, device="cuda")
+    ctx.fragment_reassemble_device(dev(p), dev(fb.cmd_off[sel]), dev(fb.cmd_avail[sel]), dev_i32(fb.slots[sel]),
+                                   len(sel), MAXP, d["msg_bytes"], dev(st["msg_off"]), dev(fb.msg_len),
+                                   dev(fb.msg_count), d["fragments"], st["words"], d["remaining"], len(fb.msg_len),
+                                   status, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    st["msg_bytes"] = d["msg_bytes"].cpu().numpy().view(np.uint8).copy()
+    st["fragments"] = d["fragments"].cpu().numpy().view(np.uint32).copy()
+    st["remaining"] = d["remaining"].cpu().numpy().view(np.uint32).copy()
+    return status.cpu().numpy()
+
+
+def corrupt(fb, rng, k=40):
+    p = fb.payload.copy()
+    for j, i in enumerate(rng.choice(fb.n, k, replace=False)):
+        o = int(fb.cmd_off[i])
+        kind = j % 6
+        if kind == 0:
+            p[o + 6:o + 8] = 0
+        elif kind == 1:
+            p[o + 12:o + 16] = np.frombuffer((1 << 21).to_bytes(4, "big"), np.uint8)
+        elif kind == 2:
+            p[o + 20:o + 24] = np.frombuffer((10 ** 6).to_bytes(4, "big"), np.uint8)
+        elif kind == 3:
+            p[o + 16:o + 20] = np.frombuffer((10 ** 5).to_bytes(4, "big"), np.uint8)
+        elif kind == 4:
+            p[o + 6:o + 8] = np.frombuffer((4000).to_bytes(2, "big"), np.uint8)
+        else:
+            fb.slots[i] = -1
+    return p
+
+
+@pytest.mark.parametrize("dups", [0.0, 0.5])
+def test_fragments_match_oracle(ctx, oracle_lib, dups):  # noqa: F811
+    rng = np.random.default_rng(21)
+    fb = workloads.fragments(rng.integers(1, 80000, 300), seed=22, duplicates=dups)
+    p = corrupt(fb, rng)
+    so, sg = state(fb), state(fb)
+    exp = run_oracle(oracle_lib, fb, so, payload=p)
+    got = run_gpu(ctx, fb, sg, payload=p)
+    assert (got == exp).all()
+    for k in ("msg_bytes", "fragments", "remaining"):
+        assert (so[k] == sg[k]).all(), k
+
+
+def test_fragments_across_batches(ctx, oracle_lib):  # noqa: F811
+    rng = np.random.default_rng(23)
+    fb = workloads.fragments(rng.integers(1, 30000, 100), seed=24, duplicates=0.7)
+    so, sg = state(fb), state(fb)
+    cuts = [0, fb.n // 3, fb.n // 2, fb.n]
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        sel = np.arange(a, b)
+        assert (run_gpu(ctx, fb, sg, sel) == run_oracle(oracle_lib, fb, so, sel)).all()
+    for k in ("msg_bytes", "fragments", "remaining"):
+        assert (so[k] == sg[k]).all(), k
+    assert (sg["remaining"] == 0).all()
+
+
+def test_cfg5_round_trip(ctx):  # noqa: F811
+    fb = workloads.cfg5_fragments(1024)            # 1024 x 64 KiB = 50 176 fragments
+    st = state(fb)
+    status = run_gpu(ctx, fb, st)
+    assert (status == 1).all() and (st["remaining"] == 0).all()
+    body = np.concatenate(fb.messages)
+    assert (st["msg_bytes"][:len(body)] == body).all()

@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Fragment reassembly throughput (enet_hip_fragment_reassemble_device,
+c/protocol.cs:529-637) on cfg5's receive side: 4096 x 64 KiB messages = 200 704
+SEND_FRAGMENT DGRAMs in shuffled order, device-resident.  Algorithmic bytes per
+call = 2 x fragment data (read from the DGRAM arena, written to the messages).
+The bitmaps / remaining counters are reset between calls (untimed); HIP events
+bracket each call on its stream.  Result checked against the original messages.
+
+    python tools/frag_bench.py [--messages 4096] [--reps 20]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "enet-csharp_amd"))
+
+import numpy as np  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--messages", type=int, default=4096)
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    import torch
+    import enethip
+    from enethip import workloads
+    fb = workloads.cfg5_fragments(a.messages)
+    words = 2
+    ctx = enethip.Context(0)
+    t = lambda x, dt: torch.from_numpy(np.ascontiguousarray(x).view(dt)).cuda()  # noqa: E731
+    d_payload = t(fb.payload, np.uint8)
+    d_off, d_avail, d_slots = t(fb.cmd_off, np.int64), t(fb.cmd_avail, np.int32), t(fb.slots, np.int32)
+    msg_off = np.concatenate([[0], np.cumsum(fb.msg_len.astype(np.uint64))[:-1]]).astype(np.uint64)
+    d_msg = torch.zeros(int(fb.msg_len.astype(np.uint64).sum()), dtype=torch.uint8, device="cuda")
+    d_moff, d_mlen, d_mcnt = t(msg_off, np.int64), t(fb.msg_len, np.int32), t(fb.msg_count, np.int32)
+    d_frag = torch.zeros(len(fb.msg_len) * words, dtype=torch.int32, device="cuda")
+    d_rem0 = t(fb.msg_count, np.int32)
+    d_rem = d_rem0.clone()
+    d_status = torch.zeros(fb.n, dtype=torch.int8, device="cuda")
+    s = torch.cuda.Stream()
+    times = []
+    for r in range(a.reps + 2):
+        d_frag.zero_()
+        d_rem.copy_(d_rem0)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(s):
+            e0.record(s)
+            ctx.fragment_reassemble_device(d_payload, d_off, d_avail, d_slots, fb.n, 32 << 20, d_msg, d_moff, d_mlen,
+                                           d_mcnt, d_frag, words, d_rem, len(fb.msg_len), d_status,
+                                           stream=s.cuda_stream)
+            e1.record(s)
+        torch.cuda.synchronize()
+        if r >= 2:
+            times.append(e0.elapsed_time(e1) * 1e-3)
+    ok = bool((d_status.cpu().numpy() == 1).all() and (d_rem.cpu().numpy() == 0).all() and
+              (d_msg.cpu().numpy() == np.concatenate(fb.messages)).all())
+    dt = float(np.median(times))
+    moved = 2.0 * fb.data_bytes
+    print(json.dumps({"workload": fb.name, "fragments": fb.n, "data_bytes": fb.data_bytes,
+                      "us_per_call": round(dt * 1e6, 2), "GBps_moved": round(moved / dt / 1e9, 1),
+                      "hbm_frac": round(moved / dt / 8e12, 4), "ok": ok}), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
