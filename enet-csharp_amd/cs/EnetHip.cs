@@ -88,6 +88,19 @@ namespace enet
                                                               uint* segLengths, uint* segFirst, nuint dgramCount,
                                                               uint* output, IntPtr stream);
 
+        // batched range coder, c/compress.cs:69-943
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_range_compress_device(IntPtr ctx, byte* input, ulong* inOffsets,
+                                                                uint* inLengths, nuint count, byte* output,
+                                                                ulong* outOffsets, uint* outLimits,
+                                                                uint* outLengths, IntPtr stream);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_range_decompress_device(IntPtr ctx, byte* input, ulong* inOffsets,
+                                                                  uint* inLengths, nuint count, byte* output,
+                                                                  ulong* outOffsets, uint* outLimits,
+                                                                  uint* outLengths, IntPtr stream);
+
         // receive-side fragment reassembly, c/protocol.cs:529-637
         [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
         public static extern int enet_hip_fragment_reassemble_device(IntPtr ctx, byte* bytes, ulong* cmdOffsets,
@@ -194,6 +207,19 @@ namespace enet
                 EnetHipNative.enet_hip_fragment_reassemble_device(Handle, bytes, cmdOffsets, cmdAvail, slots, count,
                     maximumPacketSize, msgBytes, msgOffsets, msgLengths, msgFragCounts, fragments, wordsPerMsg,
                     remaining, slotCount, status, stream));
+
+        public void RangeCompressDevice(byte* input, ulong* inOffsets, uint* inLengths, nuint count, byte* output,
+                                        ulong* outOffsets, uint* outLimits, uint* outLengths, IntPtr stream = default)
+            => EnetHip.Check("enet_hip_range_compress_device",
+                EnetHipNative.enet_hip_range_compress_device(Handle, input, inOffsets, inLengths, count, output,
+                    outOffsets, outLimits, outLengths, stream));
+
+        public void RangeDecompressDevice(byte* input, ulong* inOffsets, uint* inLengths, nuint count, byte* output,
+                                          ulong* outOffsets, uint* outLimits, uint* outLengths,
+                                          IntPtr stream = default)
+            => EnetHip.Check("enet_hip_range_decompress_device",
+                EnetHipNative.enet_hip_range_decompress_device(Handle, input, inOffsets, inLengths, count, output,
+                    outOffsets, outLimits, outLengths, stream));
 
         public void Synchronize() => EnetHip.Check("enet_hip_synchronize", EnetHipNative.enet_hip_synchronize(Handle));
 

@@ -33,6 +33,7 @@
 #include "crc32_stream_common.hpp"
 #include "enet_hip.h"
 #include "fragment_kernels.hpp"
+#include "range_coder.hpp"
 
 namespace enethip {
 
@@ -880,6 +881,8 @@ struct enet_hip_context {
     size_t d_claim_cap = 0;     // words
     uint8_t* d_frag_desc = nullptr;   // copy descriptors, 28 B per command
     size_t d_frag_desc_cap = 0;
+    uint8_t* d_rc_scratch = nullptr;  // range coder models, kRangeModelBytes per thread
+    size_t d_rc_scratch_cap = 0;
 };
 
 namespace {
@@ -1225,6 +1228,7 @@ int enet_hip_context_destroy(enet_hip_context* ctx) {
     (void)hipFree(ctx->d_meta);
     (void)hipFree(ctx->d_claim);
     (void)hipFree(ctx->d_frag_desc);
+    (void)hipFree(ctx->d_rc_scratch);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return 0;
@@ -1241,7 +1245,7 @@ int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgro
 }
 
 int enet_hip_diag_ablation(enet_hip_context* ctx, int mode) {
-    if (!ctx || mode < 0 || mode > 31) return -static_cast<int>(hipErrorInvalidValue);
+    if (!ctx || mode < 0 || mode > 63) return -static_cast<int>(hipErrorInvalidValue);
     ctx->ablation = mode & ~8;
     ctx->ablation_prio = (mode >> 3) & 1;
     return 0;
@@ -1346,6 +1350,43 @@ int enet_hip_fragment_reassemble_device(enet_hip_context* ctx, const uint8_t* by
                msgFragCounts, fragments, wordsPerMsg, remaining, slotCount, status, ctx->d_claim,
                d_src, d_dst, d_len, d_cl};
     return fragment_reassemble_launch(a, ctx->num_cus, st);
+}
+
+static int range_coder_call(enet_hip_context* ctx, bool decompress, const uint8_t* in, const uint64_t* inOffsets,
+                            const uint32_t* inLengths, size_t count, uint8_t* out, const uint64_t* outOffsets,
+                            const uint32_t* outLimits, uint32_t* outLengths, void* stream) {
+    if (!ctx) return -static_cast<int>(hipErrorInvalidValue);
+    if (count == 0) return 0;
+    if (!in || !inOffsets || !inLengths || !out || !outOffsets || !outLimits || !outLengths)
+        return -static_cast<int>(hipErrorInvalidValue);
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ENH_CHECK(hipSetDevice(ctx->device));
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    // one lane per DGRAM, at most 4 waves per CU in flight (the models are HBM scratch)
+    const uint64_t threads = std::min<uint64_t>(count, static_cast<uint64_t>(ctx->num_cus) * 256u);
+    const size_t need = ((threads + 63) / 64) * 64 * kRangeModelBytes;
+    if (need > ctx->d_rc_scratch_cap) {
+        ENH_CHECK(hipStreamSynchronize(st));
+        int rc;
+        if ((rc = ensure(&ctx->d_rc_scratch, &ctx->d_rc_scratch_cap, need))) return rc;
+    }
+    RangeArgs a{in, inOffsets, inLengths, count, out, outOffsets, outLimits, outLengths, ctx->d_rc_scratch};
+    return range_coder_launch(decompress, a, threads, st);
+}
+
+int enet_hip_range_compress_device(enet_hip_context* ctx, const uint8_t* in, const uint64_t* inOffsets,
+                                   const uint32_t* inLengths, size_t count, uint8_t* out, const uint64_t* outOffsets,
+                                   const uint32_t* outLimits, uint32_t* outLengths, void* stream) {
+    return range_coder_call(ctx, false, in, inOffsets, inLengths, count, out, outOffsets, outLimits, outLengths,
+                            stream);
+}
+
+int enet_hip_range_decompress_device(enet_hip_context* ctx, const uint8_t* in, const uint64_t* inOffsets,
+                                     const uint32_t* inLengths, size_t count, uint8_t* out,
+                                     const uint64_t* outOffsets, const uint32_t* outLimits, uint32_t* outLengths,
+                                     void* stream) {
+    return range_coder_call(ctx, true, in, inOffsets, inLengths, count, out, outOffsets, outLimits, outLengths,
+                            stream);
 }
 
 int enet_hip_crc32_batch_host(enet_hip_context* ctx, const uint8_t* bytes, size_t byteCount,

@@ -136,7 +136,8 @@ __device__ __forceinline__ void wait_vm_sel(uint32_t c) {
 // ABL (diagnostics, wrong checksums by design): 1 = no table lookups (the fold is
 // an XOR of the data), 2 = packet DMA from an L2-resident 2 KiB slice of the table
 // images per wave (no HBM traffic), 4 = no table image load (with 1 only),
-// 16 = synthetic metadata (1200-byte packets packed from offset 0, nothing read).
+// 16 = synthetic metadata (1200-byte packets packed from offset 0, nothing read);
+// 32 (tuning, correct checksums) = each wave takes a contiguous range of groups.
 template <int MODE, int LG, int W, int NB, int ABL = 0>
 __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, KernelTables tb) {
     using G = LeanGeom<MODE, LG, W, NB>;
@@ -146,7 +147,14 @@ __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, Kerne
     const uint64_t ngroups = (pa.n + kPk - 1u) >> (6 - LG);
     const uint64_t wv = static_cast<uint64_t>(blockIdx.x) * W + wave;
     const uint64_t wt = static_cast<uint64_t>(gridDim.x) * W;
-    const uint32_t J = wv < ngroups ? static_cast<uint32_t>((ngroups - 1u - wv) / wt) + 1u : 0u;
+    // groups of this wave: wv, wv + wt, ... (default) or, with ABL & 32, a contiguous range
+    constexpr bool kContig = (ABL & 32) != 0;
+    const uint64_t g0 = kContig ? wv * ngroups / wt : wv;
+    const uint32_t J = kContig ? static_cast<uint32_t>((wv + 1u) * ngroups / wt - g0)
+                               : (wv < ngroups ? static_cast<uint32_t>((ngroups - 1u - wv) / wt) + 1u : 0u);
+    auto group_of = [&](uint32_t j) __attribute__((always_inline)) -> uint64_t {
+        return kContig ? g0 + j : wv + static_cast<uint64_t>(j) * wt;
+    };
     const uint32_t ring = kLdsTableBytes + wave * (G::kRing + 2u * G::kHalf);
     const uint32_t meta0 = ring + G::kRing;
     const uint64_t zero = reinterpret_cast<uint64_t>(tb.zero);
@@ -178,7 +186,7 @@ __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, Kerne
             const uint32_t x = 64u * o + lane;
             const uint32_t q = x / G::kGroupMeta, f = (x / kPk) % G::kF, p = x % kPk;
             const uint32_t j = min(c * JM + q, J - 1u);
-            const uint64_t pk = min((wv + static_cast<uint64_t>(j) * wt) * kPk + p, pa.n - 1u);
+            const uint64_t pk = min(group_of(j) * kPk + p, pa.n - 1u);
             const uint32_t* src = pa.len + pk;
             if (f == 1u || f == 2u) src = reinterpret_cast<const uint32_t*>(pa.off) + 2u * pk + (f - 1u);
             if (MODE && f == 3u) src = pa.slot_off + pk;
@@ -191,7 +199,7 @@ __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, Kerne
     };
     auto window_of = [&](uint32_t j) __attribute__((always_inline)) -> Window {
         Window w;
-        const uint64_t pkw = (wv + static_cast<uint64_t>(j) * wt) * kPk + pj_lane;
+        const uint64_t pkw = group_of(j) * kPk + pj_lane;
         w.active = pkw < pa.n;
         w.L = w.active ? ((ABL & 16) ? 1200u : meta_at(j, 0)) : 0u;
         const uint64_t off = (ABL & 16) ? 1200u * pkw
@@ -343,7 +351,7 @@ __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, Kerne
     Task t{};
     auto consumer_setup = [&](uint32_t j) __attribute__((always_inline)) {
         const Window w = window_of(j);
-        t.pk = (wv + static_cast<uint64_t>(j) * wt) * kPk + pj_lane;
+        t.pk = group_of(j) * kPk + pj_lane;
         t.active = w.active;
         t.k = k;
         t.w0 = (k - w.r) & (P - 1u);
@@ -500,6 +508,7 @@ struct LeanVariant {
                 case 17: go_abl<3, 17>(num_cus, st, pa, tb); break;
                 case 21: go_abl<3, 21>(num_cus, st, pa, tb); break;
                 case 16: go_abl<3, 16>(num_cus, st, pa, tb); break;
+                case 32: go_abl<3, 32>(num_cus, st, pa, tb); break;
                 default: break;
             }
             return;

@@ -32,6 +32,7 @@ EXPORTED_SYMBOLS = (
     "enet_hip_device_free", "enet_hip_host_alloc", "enet_hip_host_free", "enet_hip_memcpy_h2d",
     "enet_hip_memcpy_d2h", "enet_hip_synchronize", "enet_hip_read_probe_device", "enet_hip_set_kernel_path",
     "enet_hip_diag_ablation", "enet_hip_diag_trace", "enet_hip_fragment_reassemble_device",
+    "enet_hip_range_compress_device", "enet_hip_range_decompress_device",
 )
 
 
@@ -104,6 +105,9 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.enet_hip_read_probe_device.argtypes = [vp, vp, sz, vp, vp]
     L.enet_hip_synchronize.restype = i32
     L.enet_hip_synchronize.argtypes = [vp]
+    for f in ("enet_hip_range_compress_device", "enet_hip_range_decompress_device"):
+        getattr(L, f).restype = i32
+        getattr(L, f).argtypes = [vp, vp, vp, vp, sz, vp, vp, vp, vp, vp]
     L.enet_hip_fragment_reassemble_device.restype = i32
     L.enet_hip_fragment_reassemble_device.argtypes = [vp, vp, vp, vp, vp, sz, u32, vp, vp, vp, vp, vp, u32, vp, sz,
                                                       vp, vp]
@@ -225,6 +229,14 @@ class Context:
             self.handle, _ptr(d_bytes), _ptr(d_cmd_off), _ptr(d_cmd_avail), _ptr(d_slots), int(n), int(max_packet),
             _ptr(d_msg_bytes), _ptr(d_msg_off), _ptr(d_msg_len), _ptr(d_msg_count), _ptr(d_fragments), int(words),
             _ptr(d_remaining), int(n_slots), _ptr(d_status), stream or None))
+
+    def range_coder_device(self, decompress: bool, d_in, d_in_off, d_in_len, n: int, d_out, d_out_off,
+                           d_out_limit, d_out_len, stream: int = 0) -> None:
+        """Batched ENet range coder (c/compress.cs:69-943): see enet_hip.h."""
+        name = "enet_hip_range_decompress_device" if decompress else "enet_hip_range_compress_device"
+        _check(name, getattr(self.lib, name)(
+            self.handle, _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len), int(n), _ptr(d_out), _ptr(d_out_off),
+            _ptr(d_out_limit), _ptr(d_out_len), stream or None))
 
     def read_probe_device(self, d_bytes, nbytes: int, d_sink, stream: int = 0) -> None:
         _check("enet_hip_read_probe_device", self.lib.enet_hip_read_probe_device(

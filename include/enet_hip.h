@@ -146,6 +146,24 @@ ENET_HIP_API int enet_hip_fragment_reassemble_device(enet_hip_context* ctx, cons
                                                      uint32_t wordsPerMsg, uint32_t* remaining,
                                                      size_t slotCount, int8_t* status, void* stream);
 
+/* ---- batched range coder (c/compress.cs:69-943) ----
+ * ENet's adaptive order-2 range coder (enet_host_compress_with_range_coder) over
+ * a batch of DGRAMs, one independent model per DGRAM exactly as one
+ * enet_range_coder_compress / _decompress call each.  DGRAM i is
+ * in[inOffsets[i] .. +inLengths[i]) (the send path's buffer list, concatenated);
+ * its result goes to out[outOffsets[i] .. +outLimits[i]) and outLengths[i]
+ * receives the byte count, 0 where the reference returns 0 (empty input, output
+ * over outLimit, or a corrupt compressed stream).  Device pointers, async on
+ * `stream`; calls on one context must not overlap (shared model scratch). */
+ENET_HIP_API int enet_hip_range_compress_device(enet_hip_context* ctx, const uint8_t* in, const uint64_t* inOffsets,
+                                                const uint32_t* inLengths, size_t count, uint8_t* out,
+                                                const uint64_t* outOffsets, const uint32_t* outLimits,
+                                                uint32_t* outLengths, void* stream);
+ENET_HIP_API int enet_hip_range_decompress_device(enet_hip_context* ctx, const uint8_t* in,
+                                                  const uint64_t* inOffsets, const uint32_t* inLengths, size_t count,
+                                                  uint8_t* out, const uint64_t* outOffsets, const uint32_t* outLimits,
+                                                  uint32_t* outLengths, void* stream);
+
 /* ---- multi-GPU: independent contiguous shards, no collective ----
  * Packets [i*count/k, (i+1)*count/k) go to contexts[i]; each shard's bytes are
  * copied to its device, checksummed and the CRCs copied back into out[].

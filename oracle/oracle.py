@@ -79,6 +79,9 @@ class OracleLib:
         L.oracle_crc32_gather.argtypes = [vp, vp, vp, vp, sz, vp]
         L.oracle_verify_batch.restype = None
         L.oracle_verify_batch.argtypes = [vp, vp, vp, vp, vp, sz, vp, vp]
+        for f in ("oracle_range_compress_batch", "oracle_range_decompress_batch"):
+            getattr(L, f).restype = None
+            getattr(L, f).argtypes = [vp, vp, vp, sz, vp, vp, vp, vp]
         L.oracle_fragment_reassemble.restype = None
         L.oracle_fragment_reassemble.argtypes = [vp, vp, vp, vp, sz, ctypes.c_uint32, vp, vp, vp, vp, vp,
                                                  ctypes.c_uint32, vp, sz, vp]
@@ -156,3 +159,20 @@ def fragment_reassemble(lib: "OracleLib", payload, cmd_off, cmd_avail, slots, ma
                                        mo.ctypes.data, ml.ctypes.data, mc.ctypes.data, fragments.ctypes.data,
                                        int(words), remaining.ctypes.data, len(ml), status.ctypes.data)
     return status
+
+
+def range_coder_batch(lib: "OracleLib", decompress: bool, data, in_off, in_len, out_limit):
+    """Batched adaptive range coder (c/compress.cs:69-943), sequential: DGRAM i =
+    data[in_off[i] .. +in_len[i]); returns (out bytes, out offsets, out lengths),
+    length 0 = output over out_limit[i] (or a corrupt stream)."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    in_off = np.ascontiguousarray(in_off, dtype=np.uint64)
+    in_len = np.ascontiguousarray(in_len, dtype=np.uint32)
+    out_limit = np.ascontiguousarray(out_limit, dtype=np.uint32)
+    out_off = np.concatenate([[0], np.cumsum(out_limit.astype(np.uint64))[:-1]]).astype(np.uint64)
+    out = np.zeros(int(out_limit.astype(np.uint64).sum()) + 16, dtype=np.uint8)
+    out_len = np.zeros(len(in_off), dtype=np.uint32)
+    fn = lib.lib.oracle_range_decompress_batch if decompress else lib.lib.oracle_range_compress_batch
+    fn(data.ctypes.data, in_off.ctypes.data, in_len.ctypes.data, len(in_off), out.ctypes.data, out_off.ctypes.data,
+       out_limit.ctypes.data, out_len.ctypes.data)
+    return out, out_off, out_len
