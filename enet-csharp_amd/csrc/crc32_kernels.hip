@@ -1245,7 +1245,7 @@ int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgro
 }
 
 int enet_hip_diag_ablation(enet_hip_context* ctx, int mode) {
-    if (!ctx || mode < 0 || mode > 63) return -static_cast<int>(hipErrorInvalidValue);
+    if (!ctx || mode < 0 || mode > 127) return -static_cast<int>(hipErrorInvalidValue);
     ctx->ablation = mode & ~8;
     ctx->ablation_prio = (mode >> 3) & 1;
     return 0;

@@ -137,7 +137,8 @@ __device__ __forceinline__ void wait_vm_sel(uint32_t c) {
 // an XOR of the data), 2 = packet DMA from an L2-resident 2 KiB slice of the table
 // images per wave (no HBM traffic), 4 = no table image load (with 1 only),
 // 16 = synthetic metadata (1200-byte packets packed from offset 0, nothing read);
-// 32 (tuning, correct checksums) = each wave takes a contiguous range of groups.
+// 32 (tuning, correct checksums) = each wave takes a contiguous range of groups;
+// 64 (tuning, correct checksums) = s_setprio 1 for the later-dispatched half of the waves.
 template <int MODE, int LG, int W, int NB, int ABL = 0>
 __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, KernelTables tb) {
     using G = LeanGeom<MODE, LG, W, NB>;
@@ -165,6 +166,9 @@ __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, Kerne
         if (pa.trace) tmark[i] = __builtin_amdgcn_s_memrealtime();
     };
     mark(0);
+    if constexpr ((ABL & 64) != 0) {
+        if (wave >= W / 2) __builtin_amdgcn_s_setprio(1);   // tuning: the later-dispatched half first
+    }
     auto trace_end = [&]() __attribute__((always_inline)) {
         if (pa.trace && lane == 0u) {
             uint64_t* tr = pa.trace + 8u * wv;
@@ -509,6 +513,7 @@ struct LeanVariant {
                 case 21: go_abl<3, 21>(num_cus, st, pa, tb); break;
                 case 16: go_abl<3, 16>(num_cus, st, pa, tb); break;
                 case 32: go_abl<3, 32>(num_cus, st, pa, tb); break;
+                case 64: go_abl<3, 64>(num_cus, st, pa, tb); break;
                 default: break;
             }
             return;
