@@ -37,6 +37,9 @@ class FakeEngine:
     def kernel_ms(self, fn, steps):
         return 0.02, 0.022
 
+    def region_ms(self, fn, steps):
+        return 0.019
+
     def outputs(self, j):
         b = self.batches[j]
         return self.lib.batch(b.payload, b.off, b.lens, threads=2)
