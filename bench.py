@@ -46,6 +46,8 @@ def parse(argv=None):
                          "launch's prologue overlaps the previous launch's tail (1 = serial)")
     ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "small"],
                     help="cfg2 = the metric's workload; cfg3 = mixed lengths; small = harness tests only")
+    ap.add_argument("--binned", action="store_true",
+                    help="length-binned entry (enet_hip_crc32_batch_device_binned): for mixed lengths (cfg3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget per CPU-baseline leg")
     return ap.parse_args(argv)
@@ -132,15 +134,28 @@ class GpuEngine:
                 n=b.n, nbytes=b.payload_bytes))
         self.sink = torch.zeros(4, dtype=torch.int32, device="cuda")
         self.graph = None
+        self.binned = False
+        self.ws = {}                               # binned: one workspace per stream
         torch.cuda.synchronize()
 
     def set_streams(self, n: int):
         self.streams = [self.stream] + [self.torch.cuda.Stream() for _ in range(max(1, n) - 1)]
 
+    def set_binned(self, on: bool):
+        self.binned = on
+        if on:
+            nb = self.ctx.binned_workspace_size(max(b["n"] for b in self.bufs))
+            for s in self.streams:
+                self.ws[s.cuda_stream] = self.torch.zeros(nb, dtype=self.torch.uint8, device="cuda")
+
     def step(self, i: int, stream=None):
         b = self.bufs[i % len(self.bufs)]
         h = self.h if stream is None else stream.cuda_stream
-        self.ctx.crc32_batch_device(b["payload"], b["off"], b["lens"], b["n"], b["out"], h)
+        if self.binned:
+            w = self.ws[h]
+            self.ctx.crc32_batch_device_binned(b["payload"], b["off"], b["lens"], b["n"], b["out"], w, w.numel(), h)
+        else:
+            self.ctx.crc32_batch_device(b["payload"], b["off"], b["lens"], b["n"], b["out"], h)
 
     def probe(self, i: int):
         b = self.bufs[i % len(self.bufs)]
@@ -279,6 +294,8 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
     eng = (engine_factory or GpuEngine)(local, batches, args.lanes, args.wgs)
     if hasattr(eng, "set_streams"):
         eng.set_streams(args.streams)
+    if args.binned:
+        eng.set_binned(True)
 
     # correctness gate (untimed): first resident batch vs the oracle
     eng.step(0)
@@ -351,6 +368,7 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
                 "parallelism": f"{ws} independent shards (no collective)",
                 "lanes_per_packet": args.lanes or "default",
                 "streams": args.streams,
+                "entry": "enet_hip_crc32_batch_device_binned" if args.binned else "enet_hip_crc32_batch_device",
             },
             "hbm_read_frac": round(value * GIB / 1e9 / (HBM_PEAK_GBPS * ws), 4),
             "roofline": {

@@ -193,6 +193,7 @@ __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, Kerne
             const uint64_t pk = min(group_of(j) * kPk + p, pa.n - 1u);
             const uint32_t* src = pa.len + pk;
             if (f == 1u || f == 2u) src = reinterpret_cast<const uint32_t*>(pa.off) + 2u * pk + (f - 1u);
+            if (!MODE && pa.meta4) src = pa.meta4 + 4u * pk + f;       // binned: the record in field order
             if (MODE && f == 3u) src = pa.slot_off + pk;
             if (MODE && f == 4u) src = pa.connect + pk;
             dma4(src, half + 256u * o);
@@ -356,6 +357,7 @@ __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, Kerne
     auto consumer_setup = [&](uint32_t j) __attribute__((always_inline)) {
         const Window w = window_of(j);
         t.pk = group_of(j) * kPk + pj_lane;
+        if (!MODE && pa.meta4 && w.active) t.pk = meta_at(j, 3);   // binned: the packet's caller index
         t.active = w.active;
         t.k = k;
         t.w0 = (k - w.r) & (P - 1u);
@@ -538,6 +540,74 @@ int lean_launch(int mode, int lg, int geom, int abl, int num_cus, hipStream_t st
     if (lg != 2 && lg != 3) return -static_cast<int>(hipErrorInvalidValue);
     if (geom == 1) LeanVariant<12, 3>::launch(mode, lg, 0, num_cus, st, pa, tb);
     else LeanVariant<16, 2>::launch(mode, lg, abl, num_cus, st, pa, tb);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : -static_cast<int>(e);
+}
+
+// ---------------------------------------------------------------- length bins
+// Mixed-length batches (cfg3): a group's stage count is the longest of its
+// packets, so a group of short and long packets idles most of its lanes.
+// enet_hip_crc32_batch_device_binned first orders the packet records inside each
+// tile of 1024 packets by length bin (32-byte bins, longest first): one launch,
+// one workgroup per tile, a counting sort in LDS, no global atomics and nothing
+// carried between calls.  A group of 64/P consecutive records then holds
+// packets of about one length.  The lean kernel reads the ordered records
+// (PacketArgs::meta4) and writes each CRC to its caller index.  The order inside
+// a tile's bin is scheduling-dependent; the CRCs are not (each is its own
+// packet's), and tile t's records stay in [1024 t, 1024 (t + 1)).
+
+constexpr uint32_t kBins = 256, kBinThreads = 256, kBinItems = 4, kBinTile = kBinThreads * kBinItems;
+
+__device__ __forceinline__ uint32_t bin_of(uint32_t len) { return kBins - 1u - min(len >> 5, kBins - 1u); }
+
+__global__ void __launch_bounds__(kBinThreads) bin_tile_kernel(const uint32_t* len, const uint64_t* off, uint64_t n,
+                                                               uint4* rec) {
+    __shared__ uint32_t h[kBins], sc[kBins];
+    const uint32_t tid = threadIdx.x;
+    h[tid] = 0;
+    __syncthreads();
+    const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kBinTile;
+    uint32_t L[kBinItems], slot[kBinItems];
+    uint64_t o[kBinItems];
+#pragma unroll
+    for (uint32_t r = 0; r < kBinItems; ++r) {
+        const uint64_t i = base + r * kBinThreads + tid;
+        L[r] = i < n ? len[i] : 0u;
+        o[r] = i < n ? off[i] : 0u;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kBinItems; ++r)
+        slot[r] = base + r * kBinThreads + tid < n ? atomicAdd(&h[bin_of(L[r])], 1u) : 0u;
+    __syncthreads();
+    const uint32_t mine = h[tid];
+    sc[tid] = mine;
+    __syncthreads();
+    for (uint32_t s = 1; s < kBins; s <<= 1) {               // inclusive scan over the bins
+        const uint32_t v = tid >= s ? sc[tid - s] : 0u;
+        __syncthreads();
+        sc[tid] += v;
+        __syncthreads();
+    }
+    h[tid] = sc[tid] - mine;                                 // first slot of bin tid in the tile
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < kBinItems; ++r) {
+        const uint64_t i = base + r * kBinThreads + tid;
+        if (i < n)
+            rec[base + h[bin_of(L[r])] + slot[r]] = make_uint4(L[r], static_cast<uint32_t>(o[r]),
+                                                               static_cast<uint32_t>(o[r] >> 32),
+                                                               static_cast<uint32_t>(i));
+    }
+}
+
+size_t length_bin_workspace(uint64_t n) { return 16u * n; }
+
+int length_bin(const uint32_t* len, const uint64_t* off, uint64_t n, void* workspace, hipStream_t st) {
+    if (n == 0) return 0;
+    if (n > 0xFFFFFFFFull || !workspace) return -static_cast<int>(hipErrorInvalidValue);
+    const unsigned tiles = static_cast<unsigned>((n + kBinTile - 1) / kBinTile);
+    hipLaunchKernelGGL(bin_tile_kernel, dim3(tiles), dim3(kBinThreads), 0, st, len, off, n,
+                       static_cast<uint4*>(workspace));
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : -static_cast<int>(e);
 }

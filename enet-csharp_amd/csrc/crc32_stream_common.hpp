@@ -29,6 +29,10 @@ struct PacketArgs {
     uint8_t* ok;
     uint64_t* trace;  // diagnostics: per-wave timeline (enet_hip_diag_trace) or null
     uint32_t prio;    // lean kernel: raise the issue priority of lagging waves (tuning)
+    // lean kernel, MODE 0: packet metadata pre-ordered by length bin, one record
+    // {len, off_lo, off_hi, index} per packet (enet_hip_crc32_batch_device_binned);
+    // out[index] receives the CRC.  Null = read len/off directly.
+    const uint32_t* meta4;
 };
 
 __device__ __forceinline__ uint32_t lds_load(uint32_t addr) { return *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(addr)); }

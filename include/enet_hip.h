@@ -90,6 +90,21 @@ ENET_HIP_API int enet_hip_crc32_batch_device(enet_hip_context* ctx, const uint8_
                                              const uint64_t* offsets, const uint32_t* lengths,
                                              size_t count, uint32_t* out, void* stream);
 
+/* Same results as enet_hip_crc32_batch_device (enet_crc32, c/packet.cs:142-160,
+ * per packet), for batches of mixed lengths (SURVEY cfg3): inside each tile of
+ * 1024 packets the packet records are first ordered by length (32-byte bins,
+ * longest first) on the GPU, so the packets the kernel runs together have about
+ * the same length; out[] stays in caller order.  `workspace` is caller-owned
+ * device memory of at least enet_hip_binned_workspace_size(count) bytes (16 per
+ * packet: the ordered {len, off_lo, off_hi, index} records), 16-byte aligned, not
+ * shared with a call in flight on another stream; count < 2^32.  No state is
+ * kept between calls; graph-capturable. */
+ENET_HIP_API size_t enet_hip_binned_workspace_size(size_t count);
+ENET_HIP_API int enet_hip_crc32_batch_device_binned(enet_hip_context* ctx, const uint8_t* bytes,
+                                                    const uint64_t* offsets, const uint32_t* lengths,
+                                                    size_t count, uint32_t* out, void* workspace,
+                                                    size_t workspaceBytes, void* stream);
+
 /* ---- batched checksum from/to host memory ----
  * bytes[0 .. byteCount) is copied H2D, the batch is checksummed on the GPU and
  * out[] is copied back; synchronous.  Host buffers allocated with

@@ -96,6 +96,90 @@ def test_cfg3_full(ctx, oracle_lib):
         assert (run_batch(ctx, b.payload, b.off, b.lens, lanes) == exp).all(), lanes
 
 
+def run_binned(ctx, payload, off, lens, lanes=0, path=0):
+    ctx.set_tuning(lanes, 0)
+    ctx.set_kernel_path(path)
+    try:
+        n = len(off)
+        d_p, d_o, d_l = dev(payload if len(payload) else np.zeros(16, np.uint8)), dev(off), dev(lens)
+        out = torch.zeros(n, dtype=torch.int32, device="cuda")
+        ws_bytes = ctx.binned_workspace_size(n)
+        ws = torch.zeros(ws_bytes, dtype=torch.uint8, device="cuda")
+        ctx.crc32_batch_device_binned(d_p, d_o, d_l, n, out, ws, ws_bytes,
+                                      stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        return out.cpu().numpy().view(np.uint32)
+    finally:
+        ctx.set_kernel_path(0)
+
+
+def test_binned_cfg3_full(ctx, oracle_lib):
+    """Length-binned entry (records reordered on the GPU): same CRCs, caller order."""
+    b = workloads.cfg3()
+    exp = oracle_lib.batch(b.payload, b.off, b.lens, threads=16)
+    for lanes in (4, 8):
+        assert (run_binned(ctx, b.payload, b.off, b.lens, lanes) == exp).all(), lanes
+
+
+@pytest.mark.parametrize("lanes", [1, 4, 8])
+def test_binned_golden_and_edges(ctx, golden, oracle_lib, lanes):
+    payload, off, lens, exp = golden_batch(golden)
+    assert (run_binned(ctx, payload, off, lens, lanes) == exp).all()
+    # lengths over every bin incl. the clamped last one (>= 8160 B), empties, one-packet batches
+    rng = np.random.default_rng(7 + lanes)
+    n = 20000
+    lens = rng.integers(0, 9000, size=n).astype(np.uint32)
+    lens[:64] = 0
+    lens[64:128] = np.arange(64) * 32
+    off = rng.integers(0, 1 << 20, size=n).astype(np.uint64)
+    payload = rng.integers(0, 256, size=(1 << 20) + 9000, dtype=np.uint8)
+    exp = oracle_lib.batch(payload, off, lens, threads=8)
+    assert (run_binned(ctx, payload, off, lens, lanes) == exp).all()
+    assert (run_binned(ctx, payload, off[:1], lens[:1], lanes) == exp[:1]).all()
+
+
+def test_binned_records_are_a_length_ordered_permutation(ctx, oracle_lib):
+    """The workspace's records (documented layout: n x {len, off_lo, off_hi, index}
+    first) are a permutation of the batch that keeps every 1024-packet tile in place
+    and orders it by non-increasing 32-byte length bin; 600 K packets, ragged last tile."""
+    rng = np.random.default_rng(11)
+    n = 600_000
+    lens = rng.integers(0, 1500, size=n).astype(np.uint32)
+    lens[rng.integers(0, n, size=50)] = rng.integers(8160, 20000, size=50).astype(np.uint32)   # clamped bin
+    off = rng.integers(0, 1 << 22, size=n).astype(np.uint64)
+    payload = rng.integers(0, 256, size=(1 << 22) + 20000, dtype=np.uint8)
+    ctx.set_tuning(8, 0)
+    d_p, d_o, d_l = dev(payload), dev(off), dev(lens)
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    ws_bytes = ctx.binned_workspace_size(n)
+    ws = torch.zeros(ws_bytes, dtype=torch.uint8, device="cuda")
+    ctx.crc32_batch_device_binned(d_p, d_o, d_l, n, out, ws, ws_bytes, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    rec = ws[:16 * n].cpu().numpy().view(np.uint32).reshape(n, 4)
+    idx = rec[:, 3].astype(np.int64)
+    assert (np.sort(idx) == np.arange(n)).all()
+    assert (rec[:, 0] == lens[idx]).all()
+    assert ((rec[:, 1].astype(np.uint64) | (rec[:, 2].astype(np.uint64) << np.uint64(32))) == off[idx]).all()
+    tiles = np.arange(n) // 1024
+    assert (idx // 1024 == tiles).all()                       # records stay in their 1024-packet tile
+    bins = np.minimum(rec[:, 0] >> 5, 255).astype(np.int64)
+    d = np.diff(bins)
+    assert (d[np.diff(tiles) == 0] <= 0).all()                # longest bin first inside a tile
+    exp = oracle_lib.batch(payload, off, lens, threads=16)
+    assert (out.cpu().numpy().view(np.uint32) == exp).all()
+
+
+def test_binned_rejects_small_workspace(ctx):
+    d = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    o = torch.zeros(4, dtype=torch.int64, device="cuda")
+    ln = torch.zeros(4, dtype=torch.int32, device="cuda")
+    out = torch.zeros(4, dtype=torch.int32, device="cuda")
+    need = ctx.binned_workspace_size(4)
+    ws = torch.zeros(need, dtype=torch.uint8, device="cuda")
+    with pytest.raises(enethip.ENetHipError):
+        ctx.crc32_batch_device_binned(d, o, ln, 4, out, ws, need - 1)
+
+
 def test_cfg4_shard_full(ctx, oracle_lib):
     b = workloads.cfg4(1, 8)
     exp = oracle_lib.batch(b.payload, b.off, b.lens, threads=16)
