@@ -75,6 +75,14 @@ namespace enet
                                                              nuint count, uint* output, IntPtr stream);
 
         [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern nuint enet_hip_binned_workspace_size(nuint count);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_crc32_batch_device_binned(IntPtr ctx, byte* bytes, ulong* offsets, uint* lengths,
+                                                                    nuint count, uint* output, void* workspace,
+                                                                    nuint workspaceBytes, IntPtr stream);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
         public static extern int enet_hip_crc32_batch_host(IntPtr ctx, byte* bytes, nuint byteCount, ulong* offsets,
                                                            uint* lengths, nuint count, uint* output);
 
@@ -190,6 +198,15 @@ namespace enet
         public void BatchDevice(byte* bytes, ulong* offsets, uint* lengths, nuint count, uint* output, IntPtr stream = default)
             => EnetHip.Check("enet_hip_crc32_batch_device",
                 EnetHipNative.enet_hip_crc32_batch_device(Handle, bytes, offsets, lengths, count, output, stream));
+
+        /// <summary>Device-resident batch of mixed lengths: records ordered by length per 1024-packet
+        /// tile in <paramref name="workspace" /> (EnetHipNative.enet_hip_binned_workspace_size bytes),
+        /// CRCs in caller order.</summary>
+        public void BatchDeviceBinned(byte* bytes, ulong* offsets, uint* lengths, nuint count, uint* output,
+                                      void* workspace, nuint workspaceBytes, IntPtr stream = default)
+            => EnetHip.Check("enet_hip_crc32_batch_device_binned",
+                EnetHipNative.enet_hip_crc32_batch_device_binned(Handle, bytes, offsets, lengths, count, output,
+                                                                 workspace, workspaceBytes, stream));
 
         /// <summary>Batched receive verify (c/protocol.cs:1052-1068); ok[i] = 1 keeps DGRAM i.</summary>
         public void VerifyDevice(byte* bytes, ulong* offsets, uint* lengths, uint* slotOffsets, uint* connectIds,
