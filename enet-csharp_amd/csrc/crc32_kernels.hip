@@ -1303,7 +1303,7 @@ int enet_hip_crc32_batch_device_binned(enet_hip_context* ctx, const uint8_t* byt
                       (ctx->path >= kLeanPath0 || (ctx->path == 0 && ctx->ablation == 0));
     if (lean) {
         int rc;
-        if ((rc = length_bin(lengths, offsets, count, workspace, st))) return rc;
+        if ((rc = length_bin(lengths, offsets, count, 64u >> pa.lg, workspace, st))) return rc;
         pa.meta4 = static_cast<const uint32_t*>(workspace);
     }
     return launch_packets(ctx, 0, pa, st);

@@ -547,21 +547,24 @@ int lean_launch(int mode, int lg, int geom, int abl, int num_cus, hipStream_t st
 // ---------------------------------------------------------------- length bins
 // Mixed-length batches (cfg3): a group's stage count is the longest of its
 // packets, so a group of short and long packets idles most of its lanes.
-// enet_hip_crc32_batch_device_binned first orders the packet records inside each
+// enet_hip_crc32_batch_device_binned first orders the packet records of each
 // tile of 1024 packets by length bin (32-byte bins, longest first): one launch,
 // one workgroup per tile, a counting sort in LDS, no global atomics and nothing
-// carried between calls.  A group of 64/P consecutive records then holds
-// packets of about one length.  The lean kernel reads the ordered records
-// (PacketArgs::meta4) and writes each CRC to its caller index.  The order inside
-// a tile's bin is scheduling-dependent; the CRCs are not (each is its own
-// packet's), and tile t's records stay in [1024 t, 1024 (t + 1)).
+// carried between calls.  Sorted group q of full tile t (kpk records) is written
+// as global group q * T + t (T = full tiles): the groups of rank q from every
+// tile sit side by side, so the lean kernel's rounds (consecutive groups across
+// all waves) see about one length each and run longest first, close to a
+// global sort at the cost of a local one.  A ragged last tile stays in place.
+// The lean kernel reads the ordered records (PacketArgs::meta4) and writes each
+// CRC to its caller index.  The order inside a tile's bin is
+// scheduling-dependent; the CRCs are not (each is its own packet's).
 
 constexpr uint32_t kBins = 256, kBinThreads = 256, kBinItems = 4, kBinTile = kBinThreads * kBinItems;
 
 __device__ __forceinline__ uint32_t bin_of(uint32_t len) { return kBins - 1u - min(len >> 5, kBins - 1u); }
 
 __global__ void __launch_bounds__(kBinThreads) bin_tile_kernel(const uint32_t* len, const uint64_t* off, uint64_t n,
-                                                               uint4* rec) {
+                                                               uint32_t kpk, uint4* rec) {
     __shared__ uint32_t h[kBins], sc[kBins];
     const uint32_t tid = threadIdx.x;
     h[tid] = 0;
@@ -590,11 +593,15 @@ __global__ void __launch_bounds__(kBinThreads) bin_tile_kernel(const uint32_t* l
     }
     h[tid] = sc[tid] - mine;                                 // first slot of bin tid in the tile
     __syncthreads();
+    const uint64_t full = n / kBinTile;                      // T
+    const bool interleave = blockIdx.x < full;
 #pragma unroll
     for (uint32_t r = 0; r < kBinItems; ++r) {
         const uint64_t i = base + r * kBinThreads + tid;
+        const uint32_t srt = h[bin_of(L[r])] + slot[r];      // rank inside the tile
+        const uint64_t dst = interleave ? ((srt / kpk) * full + blockIdx.x) * kpk + srt % kpk : base + srt;
         if (i < n)
-            rec[base + h[bin_of(L[r])] + slot[r]] = make_uint4(L[r], static_cast<uint32_t>(o[r]),
+            rec[dst] = make_uint4(L[r], static_cast<uint32_t>(o[r]),
                                                                static_cast<uint32_t>(o[r] >> 32),
                                                                static_cast<uint32_t>(i));
     }
@@ -602,11 +609,11 @@ __global__ void __launch_bounds__(kBinThreads) bin_tile_kernel(const uint32_t* l
 
 size_t length_bin_workspace(uint64_t n) { return 16u * n; }
 
-int length_bin(const uint32_t* len, const uint64_t* off, uint64_t n, void* workspace, hipStream_t st) {
+int length_bin(const uint32_t* len, const uint64_t* off, uint64_t n, uint32_t kpk, void* workspace, hipStream_t st) {
     if (n == 0) return 0;
-    if (n > 0xFFFFFFFFull || !workspace) return -static_cast<int>(hipErrorInvalidValue);
+    if (n > 0xFFFFFFFFull || !workspace || kpk == 0 || kBinTile % kpk) return -static_cast<int>(hipErrorInvalidValue);
     const unsigned tiles = static_cast<unsigned>((n + kBinTile - 1) / kBinTile);
-    hipLaunchKernelGGL(bin_tile_kernel, dim3(tiles), dim3(kBinThreads), 0, st, len, off, n,
+    hipLaunchKernelGGL(bin_tile_kernel, dim3(tiles), dim3(kBinThreads), 0, st, len, off, n, kpk,
                        static_cast<uint4*>(workspace));
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : -static_cast<int>(e);

@@ -18,11 +18,12 @@ int lean_setup();
 int lean_launch(int mode, int lg, int geom, int abl, int num_cus, hipStream_t st, const PacketArgs& pa,
                 const KernelTables& tb);
 
-// Order the packet records of each 1024-packet tile by length bin, longest first
-// (see crc32_lean.hip).  workspace (length_bin_workspace(n) bytes, 16-B aligned)
-// = n x uint4 {len, off_lo, off_hi, index} records.
+// Order the packet records of each 1024-packet tile by length bin, longest first,
+// and interleave the tiles' groups of kpk records rank by rank (see
+// crc32_lean.hip).  workspace (length_bin_workspace(n) bytes, 16-B aligned) =
+// n x uint4 {len, off_lo, off_hi, index} records.
 // Stream-ordered; n < 2^32.  Returns 0 or -hipError_t.
 size_t length_bin_workspace(uint64_t n);
-int length_bin(const uint32_t* len, const uint64_t* off, uint64_t n, void* workspace, hipStream_t st);
+int length_bin(const uint32_t* len, const uint64_t* off, uint64_t n, uint32_t kpk, void* workspace, hipStream_t st);
 
 }  // namespace enethip

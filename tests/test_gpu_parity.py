@@ -140,8 +140,8 @@ def test_binned_golden_and_edges(ctx, golden, oracle_lib, lanes):
 
 def test_binned_records_are_a_length_ordered_permutation(ctx, oracle_lib):
     """The workspace's records (documented layout: n x {len, off_lo, off_hi, index}
-    first) are a permutation of the batch that keeps every 1024-packet tile in place
-    and orders it by non-increasing 32-byte length bin; 600 K packets, ragged last tile."""
+    first) are a permutation of the batch: each 1024-packet tile ordered by non-increasing
+    32-byte length bin, full tiles interleaved group by group; 600 K packets, ragged last tile."""
     rng = np.random.default_rng(11)
     n = 600_000
     lens = rng.integers(0, 1500, size=n).astype(np.uint32)
@@ -160,11 +160,19 @@ def test_binned_records_are_a_length_ordered_permutation(ctx, oracle_lib):
     assert (np.sort(idx) == np.arange(n)).all()
     assert (rec[:, 0] == lens[idx]).all()
     assert ((rec[:, 1].astype(np.uint64) | (rec[:, 2].astype(np.uint64) << np.uint64(32))) == off[idx]).all()
-    tiles = np.arange(n) // 1024
-    assert (idx // 1024 == tiles).all()                       # records stay in their 1024-packet tile
+    # full tiles: sorted group q of tile t sits at global group q * T + t (8 records at 8 lanes);
+    # the ragged last tile stays in place
+    T, kpk = n // 1024, 8
+    pos = np.arange(n)
+    t_of = idx // 1024
+    full = pos < T * 1024
+    grp = pos[full] // kpk
+    assert (t_of[full] == grp % T).all()
+    assert (t_of[~full] == T).all()
     bins = np.minimum(rec[:, 0] >> 5, 255).astype(np.int64)
-    d = np.diff(bins)
-    assert (d[np.diff(tiles) == 0] <= 0).all()                # longest bin first inside a tile
+    order = np.lexsort((pos, t_of))                           # each tile's records in position order
+    same = np.diff(t_of[order]) == 0
+    assert (np.diff(bins[order])[same] <= 0).all()            # longest bin first inside a tile
     exp = oracle_lib.batch(payload, off, lens, threads=16)
     assert (out.cpu().numpy().view(np.uint32) == exp).all()
 
