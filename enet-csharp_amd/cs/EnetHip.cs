@@ -83,6 +83,15 @@ namespace enet
                                                                     nuint workspaceBytes, IntPtr stream);
 
         [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern nuint enet_hip_verify_binned_workspace_size(nuint count);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_verify_batch_device_binned(IntPtr ctx, byte* bytes, ulong* offsets, uint* lengths,
+                                                                     uint* slotOffsets, uint* connectIds, nuint count,
+                                                                     byte* ok, uint* computed, void* workspace,
+                                                                     nuint workspaceBytes, IntPtr stream);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
         public static extern int enet_hip_crc32_batch_host(IntPtr ctx, byte* bytes, nuint byteCount, ulong* offsets,
                                                            uint* lengths, nuint count, uint* output);
 

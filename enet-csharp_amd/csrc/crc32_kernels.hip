@@ -1279,7 +1279,9 @@ int enet_hip_crc32_batch_device(enet_hip_context* ctx, const uint8_t* bytes, con
     return launch_packets(ctx, 0, pa, stream ? static_cast<hipStream_t>(stream) : ctx->stream);
 }
 
-size_t enet_hip_binned_workspace_size(size_t count) { return length_bin_workspace(count); }
+size_t enet_hip_binned_workspace_size(size_t count) { return length_bin_workspace(count, false); }
+
+size_t enet_hip_verify_binned_workspace_size(size_t count) { return length_bin_workspace(count, true); }
 
 int enet_hip_crc32_batch_device_binned(enet_hip_context* ctx, const uint8_t* bytes, const uint64_t* offsets,
                                        const uint32_t* lengths, size_t count, uint32_t* out, void* workspace,
@@ -1303,7 +1305,7 @@ int enet_hip_crc32_batch_device_binned(enet_hip_context* ctx, const uint8_t* byt
                       (ctx->path >= kLeanPath0 || (ctx->path == 0 && ctx->ablation == 0));
     if (lean) {
         int rc;
-        if ((rc = length_bin(lengths, offsets, count, 64u >> pa.lg, workspace, st))) return rc;
+        if ((rc = length_bin(lengths, offsets, nullptr, nullptr, count, 64u >> pa.lg, workspace, st))) return rc;
         pa.meta4 = static_cast<const uint32_t*>(workspace);
     }
     return launch_packets(ctx, 0, pa, st);
@@ -1328,6 +1330,38 @@ int enet_hip_verify_batch_device(enet_hip_context* ctx, const uint8_t* bytes, co
     pa.connect = connectIds;
     pa.ok = ok;
     return launch_packets(ctx, 1, pa, stream ? static_cast<hipStream_t>(stream) : ctx->stream);
+}
+
+int enet_hip_verify_batch_device_binned(enet_hip_context* ctx, const uint8_t* bytes, const uint64_t* offsets,
+                                        const uint32_t* lengths, const uint32_t* slotOffsets,
+                                        const uint32_t* connectIds, size_t count, uint8_t* ok, uint32_t* computed,
+                                        void* workspace, size_t workspaceBytes, void* stream) {
+    if (!ctx) return -static_cast<int>(hipErrorInvalidValue);
+    if (count == 0) return 0;
+    if (!bytes || !offsets || !lengths || !slotOffsets || !connectIds || !ok || !workspace ||
+        count > 0xFFFFFFFFull || workspaceBytes < enet_hip_verify_binned_workspace_size(count) ||
+        (reinterpret_cast<uintptr_t>(workspace) & 15u))
+        return -static_cast<int>(hipErrorInvalidValue);
+    ENH_CHECK(hipSetDevice(ctx->device));
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    PacketArgs pa{};
+    pa.bytes = bytes;
+    pa.off = offsets;
+    pa.len = lengths;
+    pa.n = count;
+    pa.lg = static_cast<uint32_t>(log2i(auto_lanes(ctx)));
+    pa.out = computed;
+    pa.slot_off = slotOffsets;
+    pa.connect = connectIds;
+    pa.ok = ok;
+    const bool lean = ctx->path != 1 && (pa.lg == 2 || pa.lg == 3) &&
+                      (ctx->path >= kLeanPath0 || (ctx->path == 0 && ctx->ablation == 0));
+    if (lean) {
+        int rc;
+        if ((rc = length_bin(lengths, offsets, slotOffsets, connectIds, count, 64u >> pa.lg, workspace, st))) return rc;
+        pa.meta4 = static_cast<const uint32_t*>(workspace);
+    }
+    return launch_packets(ctx, 1, pa, st);
 }
 
 int enet_hip_crc32_gather_device(enet_hip_context* ctx, const uint8_t* bytes, const uint64_t* segOffsets,

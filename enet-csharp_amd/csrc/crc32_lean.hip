@@ -138,7 +138,10 @@ __device__ __forceinline__ void wait_vm_sel(uint32_t c) {
 // images per wave (no HBM traffic), 4 = no table image load (with 1 only),
 // 16 = synthetic metadata (1200-byte packets packed from offset 0, nothing read);
 // 32 (tuning, correct checksums) = each wave takes a contiguous range of groups;
-// 64 (tuning, correct checksums) = s_setprio 1 for the later-dispatched half of the waves.
+// 64 (tuning, correct checksums) = s_setprio 1 for the later-dispatched half of the waves;
+// 128 (product, correct checksums) = metadata from the length-ordered records of the
+// *_binned entry points (PacketArgs::meta4): a separate instance, so the plain path
+// carries no per-op test for it.
 template <int MODE, int LG, int W, int NB, int ABL = 0>
 __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, KernelTables tb) {
     using G = LeanGeom<MODE, LG, W, NB>;
@@ -150,6 +153,7 @@ __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, Kerne
     const uint64_t wt = static_cast<uint64_t>(gridDim.x) * W;
     // groups of this wave: wv, wv + wt, ... (default) or, with ABL & 32, a contiguous range
     constexpr bool kContig = (ABL & 32) != 0;
+    constexpr bool kBin = (ABL & 128) != 0;
     const uint64_t g0 = kContig ? wv * ngroups / wt : wv;
     const uint32_t J = kContig ? static_cast<uint32_t>((wv + 1u) * ngroups / wt - g0)
                                : (wv < ngroups ? static_cast<uint32_t>((ngroups - 1u - wv) / wt) + 1u : 0u);
@@ -193,9 +197,9 @@ __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, Kerne
             const uint64_t pk = min(group_of(j) * kPk + p, pa.n - 1u);
             const uint32_t* src = pa.len + pk;
             if (f == 1u || f == 2u) src = reinterpret_cast<const uint32_t*>(pa.off) + 2u * pk + (f - 1u);
-            if (!MODE && pa.meta4) src = pa.meta4 + 4u * pk + f;       // binned: the record in field order
             if (MODE && f == 3u) src = pa.slot_off + pk;
             if (MODE && f == 4u) src = pa.connect + pk;
+            if constexpr (kBin) src = pa.meta4 + G::kF * pk + f;    // binned: the record in field order
             dma4(src, half + 256u * o);
         }
     };
@@ -357,7 +361,7 @@ __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, Kerne
     auto consumer_setup = [&](uint32_t j) __attribute__((always_inline)) {
         const Window w = window_of(j);
         t.pk = group_of(j) * kPk + pj_lane;
-        if (!MODE && pa.meta4 && w.active) t.pk = meta_at(j, 3);   // binned: the packet's caller index
+        if constexpr (kBin) if (w.active) t.pk = meta_at(j, MODE ? 5u : 3u);   // binned: the packet's caller index
         t.active = w.active;
         t.k = k;
         t.w0 = (k - w.r) & (P - 1u);
@@ -466,15 +470,17 @@ __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, Kerne
 
 template <int W, int NB>
 struct LeanVariant {
-    template <int MODE, int LG>
+    template <int MODE, int LG, int ABL = 0>
     static const void* fn() {
-        return reinterpret_cast<const void*>(crc32_lean_kernel<MODE, LG, W, NB>);
+        return reinterpret_cast<const void*>(crc32_lean_kernel<MODE, LG, W, NB, ABL>);
     }
     static int setup() {
-        const void* fns[4] = {fn<0, 2>(), fn<0, 3>(), fn<1, 2>(), fn<1, 3>()};
-        const int lds[4] = {LeanGeom<0, 2, W, NB>::kLds, LeanGeom<0, 3, W, NB>::kLds, LeanGeom<1, 2, W, NB>::kLds,
-                            LeanGeom<1, 3, W, NB>::kLds};
-        for (int i = 0; i < 4; ++i) {
+        const void* fns[8] = {fn<0, 2>(), fn<0, 3>(), fn<1, 2>(), fn<1, 3>(),
+                              fn<0, 2, 128>(), fn<0, 3, 128>(), fn<1, 2, 128>(), fn<1, 3, 128>()};
+        const int lds[8] = {LeanGeom<0, 2, W, NB>::kLds, LeanGeom<0, 3, W, NB>::kLds, LeanGeom<1, 2, W, NB>::kLds,
+                            LeanGeom<1, 3, W, NB>::kLds, LeanGeom<0, 2, W, NB>::kLds, LeanGeom<0, 3, W, NB>::kLds,
+                            LeanGeom<1, 2, W, NB>::kLds, LeanGeom<1, 3, W, NB>::kLds};
+        for (int i = 0; i < 8; ++i) {
             const hipError_t e = hipFuncSetAttribute(fns[i], hipFuncAttributeMaxDynamicSharedMemorySize, lds[i]);
             if (e != hipSuccess) return -static_cast<int>(e);
         }
@@ -486,7 +492,12 @@ struct LeanVariant {
         const uint64_t groups = (pa.n + G::kPk - 1u) / G::kPk;
         const unsigned grid = static_cast<unsigned>(
             std::max<uint64_t>(1, std::min<uint64_t>((groups + W - 1) / W, static_cast<uint64_t>(num_cus))));
-        hipLaunchKernelGGL((crc32_lean_kernel<MODE, LG, W, NB>), dim3(grid), dim3(G::kThreads), G::kLds, st, pa, tb);
+        if (pa.meta4)
+            hipLaunchKernelGGL((crc32_lean_kernel<MODE, LG, W, NB, 128>), dim3(grid), dim3(G::kThreads), G::kLds, st,
+                               pa, tb);
+        else
+            hipLaunchKernelGGL((crc32_lean_kernel<MODE, LG, W, NB>), dim3(grid), dim3(G::kThreads), G::kLds, st, pa,
+                               tb);
     }
     template <int LG, int ABL>
     static void go_abl(int num_cus, hipStream_t st, const PacketArgs& pa, const KernelTables& tb) {
@@ -563,8 +574,12 @@ constexpr uint32_t kBins = 256, kBinThreads = 256, kBinItems = 4, kBinTile = kBi
 
 __device__ __forceinline__ uint32_t bin_of(uint32_t len) { return kBins - 1u - min(len >> 5, kBins - 1u); }
 
+// VERIFY: 32-byte records {len, off_lo, off_hi, slot_off, connect, index, 0, 0}
+// (the lean kernel's MODE 1 metadata fields), else 16-byte {len, off_lo, off_hi, index}
+template <bool VERIFY>
 __global__ void __launch_bounds__(kBinThreads) bin_tile_kernel(const uint32_t* len, const uint64_t* off, uint64_t n,
-                                                               uint32_t kpk, uint4* rec) {
+                                                               uint32_t kpk, const uint32_t* slot_off,
+                                                               const uint32_t* connect, uint4* rec) {
     __shared__ uint32_t h[kBins], sc[kBins];
     const uint32_t tid = threadIdx.x;
     h[tid] = 0;
@@ -600,21 +615,31 @@ __global__ void __launch_bounds__(kBinThreads) bin_tile_kernel(const uint32_t* l
         const uint64_t i = base + r * kBinThreads + tid;
         const uint32_t srt = h[bin_of(L[r])] + slot[r];      // rank inside the tile
         const uint64_t dst = interleave ? ((srt / kpk) * full + blockIdx.x) * kpk + srt % kpk : base + srt;
-        if (i < n)
-            rec[dst] = make_uint4(L[r], static_cast<uint32_t>(o[r]),
-                                                               static_cast<uint32_t>(o[r] >> 32),
-                                                               static_cast<uint32_t>(i));
+        if (i < n) {
+            if constexpr (VERIFY) {
+                rec[2 * dst] = make_uint4(L[r], static_cast<uint32_t>(o[r]), static_cast<uint32_t>(o[r] >> 32), slot_off[i]);
+                rec[2 * dst + 1] = make_uint4(connect[i], static_cast<uint32_t>(i), 0u, 0u);
+            } else {
+                rec[dst] = make_uint4(L[r], static_cast<uint32_t>(o[r]), static_cast<uint32_t>(o[r] >> 32),
+                                      static_cast<uint32_t>(i));
+            }
+        }
     }
 }
 
-size_t length_bin_workspace(uint64_t n) { return 16u * n; }
+size_t length_bin_workspace(uint64_t n, bool verify) { return (verify ? 32u : 16u) * n; }
 
-int length_bin(const uint32_t* len, const uint64_t* off, uint64_t n, uint32_t kpk, void* workspace, hipStream_t st) {
+int length_bin(const uint32_t* len, const uint64_t* off, const uint32_t* slot_off, const uint32_t* connect, uint64_t n,
+               uint32_t kpk, void* workspace, hipStream_t st) {
     if (n == 0) return 0;
     if (n > 0xFFFFFFFFull || !workspace || kpk == 0 || kBinTile % kpk) return -static_cast<int>(hipErrorInvalidValue);
     const unsigned tiles = static_cast<unsigned>((n + kBinTile - 1) / kBinTile);
-    hipLaunchKernelGGL(bin_tile_kernel, dim3(tiles), dim3(kBinThreads), 0, st, len, off, n, kpk,
-                       static_cast<uint4*>(workspace));
+    if (slot_off && connect)
+        hipLaunchKernelGGL(bin_tile_kernel<true>, dim3(tiles), dim3(kBinThreads), 0, st, len, off, n, kpk, slot_off,
+                           connect, static_cast<uint4*>(workspace));
+    else
+        hipLaunchKernelGGL(bin_tile_kernel<false>, dim3(tiles), dim3(kBinThreads), 0, st, len, off, n, kpk, nullptr,
+                           nullptr, static_cast<uint4*>(workspace));
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : -static_cast<int>(e);
 }

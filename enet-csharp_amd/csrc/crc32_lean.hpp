@@ -20,10 +20,12 @@ int lean_launch(int mode, int lg, int geom, int abl, int num_cus, hipStream_t st
 
 // Order the packet records of each 1024-packet tile by length bin, longest first,
 // and interleave the tiles' groups of kpk records rank by rank (see
-// crc32_lean.hip).  workspace (length_bin_workspace(n) bytes, 16-B aligned) =
-// n x uint4 {len, off_lo, off_hi, index} records.
+// crc32_lean.hip).  workspace (length_bin_workspace(n, verify) bytes, 16-B
+// aligned) = n x {len, off_lo, off_hi, index} records, or with slot_off and
+// connect (receive verify) n x {len, off_lo, off_hi, slot_off, connect, index, 0, 0}.
 // Stream-ordered; n < 2^32.  Returns 0 or -hipError_t.
-size_t length_bin_workspace(uint64_t n);
-int length_bin(const uint32_t* len, const uint64_t* off, uint64_t n, uint32_t kpk, void* workspace, hipStream_t st);
+size_t length_bin_workspace(uint64_t n, bool verify);
+int length_bin(const uint32_t* len, const uint64_t* off, const uint32_t* slot_off, const uint32_t* connect, uint64_t n,
+               uint32_t kpk, void* workspace, hipStream_t st);
 
 }  // namespace enethip

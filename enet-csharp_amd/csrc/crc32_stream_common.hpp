@@ -29,9 +29,10 @@ struct PacketArgs {
     uint8_t* ok;
     uint64_t* trace;  // diagnostics: per-wave timeline (enet_hip_diag_trace) or null
     uint32_t prio;    // lean kernel: raise the issue priority of lagging waves (tuning)
-    // lean kernel, MODE 0: packet metadata pre-ordered by length bin, one record
-    // {len, off_lo, off_hi, index} per packet (enet_hip_crc32_batch_device_binned);
-    // out[index] receives the CRC.  Null = read len/off directly.
+    // lean kernel: packet metadata pre-ordered by length bin, one record per packet
+    // in the kernel's metadata field order -- MODE 0 {len, off_lo, off_hi, index},
+    // MODE 1 {len, off_lo, off_hi, slot_off, connect, index, 0, 0} (the *_binned
+    // entry points); out/ok[index] receive the results.  Null = read the arrays.
     const uint32_t* meta4;
 };
 

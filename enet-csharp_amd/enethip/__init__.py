@@ -28,6 +28,7 @@ EXPORTED_SYMBOLS = (
     "enet_hip_crc32", "enet_hip_crc32_update", "enet_hip_device_count", "enet_hip_context_create",
     "enet_hip_context_destroy", "enet_hip_error_string", "enet_hip_set_tuning",
     "enet_hip_crc32_batch_device", "enet_hip_binned_workspace_size", "enet_hip_crc32_batch_device_binned",
+    "enet_hip_verify_binned_workspace_size", "enet_hip_verify_batch_device_binned",
     "enet_hip_crc32_batch_host", "enet_hip_verify_batch_device",
     "enet_hip_crc32_gather_device", "enet_hip_crc32_batch_multi", "enet_hip_device_alloc",
     "enet_hip_device_free", "enet_hip_host_alloc", "enet_hip_host_free", "enet_hip_memcpy_h2d",
@@ -86,6 +87,10 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.enet_hip_binned_workspace_size.argtypes = [sz]
     L.enet_hip_crc32_batch_device_binned.restype = i32
     L.enet_hip_crc32_batch_device_binned.argtypes = [vp, vp, vp, vp, sz, vp, vp, sz, vp]
+    L.enet_hip_verify_binned_workspace_size.restype = sz
+    L.enet_hip_verify_binned_workspace_size.argtypes = [sz]
+    L.enet_hip_verify_batch_device_binned.restype = i32
+    L.enet_hip_verify_batch_device_binned.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, sz, vp]
     L.enet_hip_crc32_batch_host.restype = i32
     L.enet_hip_crc32_batch_host.argtypes = [vp, vp, sz, vp, vp, sz, vp]
     L.enet_hip_verify_batch_device.restype = i32
@@ -222,6 +227,15 @@ class Context:
         _check("enet_hip_crc32_batch_device_binned", self.lib.enet_hip_crc32_batch_device_binned(
             self.handle, _ptr(d_bytes), _ptr(d_off), _ptr(d_len), int(n), _ptr(d_out), _ptr(d_workspace),
             int(workspace_bytes), stream or None))
+
+    def verify_binned_workspace_size(self, n: int) -> int:
+        return int(self.lib.enet_hip_verify_binned_workspace_size(int(n)))
+
+    def verify_batch_device_binned(self, d_bytes, d_off, d_len, d_slot, d_connect, n: int, d_ok, d_workspace,
+                                   workspace_bytes: int, d_computed=None, stream: int = 0) -> None:
+        _check("enet_hip_verify_batch_device_binned", self.lib.enet_hip_verify_batch_device_binned(
+            self.handle, _ptr(d_bytes), _ptr(d_off), _ptr(d_len), _ptr(d_slot), _ptr(d_connect), int(n),
+            _ptr(d_ok), _ptr(d_computed) or None, _ptr(d_workspace), int(workspace_bytes), stream or None))
 
     def verify_batch_device(self, d_bytes, d_off, d_len, d_slot, d_connect, n: int, d_ok, d_computed=None,
                             stream: int = 0) -> None:

@@ -123,6 +123,19 @@ ENET_HIP_API int enet_hip_verify_batch_device(enet_hip_context* ctx, const uint8
                                               const uint32_t* slotOffsets, const uint32_t* connectIds,
                                               size_t count, uint8_t* ok, uint32_t* computed, void* stream);
 
+/* enet_hip_verify_batch_device for batches of mixed lengths: the same per-tile
+ * length ordering as enet_hip_crc32_batch_device_binned, with 32-byte records
+ * {len, off_lo, off_hi, slotOffset, connectId, index, 0, 0} in `workspace`
+ * (enet_hip_verify_binned_workspace_size(count) bytes, 16-byte aligned, not
+ * shared with a call in flight on another stream); ok[] / computed[] stay in
+ * caller order (c/protocol.cs:1012-1014, 1052-1068 per DGRAM). */
+ENET_HIP_API size_t enet_hip_verify_binned_workspace_size(size_t count);
+ENET_HIP_API int enet_hip_verify_batch_device_binned(enet_hip_context* ctx, const uint8_t* bytes,
+                                                     const uint64_t* offsets, const uint32_t* lengths,
+                                                     const uint32_t* slotOffsets, const uint32_t* connectIds,
+                                                     size_t count, uint8_t* ok, uint32_t* computed,
+                                                     void* workspace, size_t workspaceBytes, void* stream);
+
 /* ---- batched gather-list checksum (send path, c/protocol.cs:1690-1698) ----
  * DGRAM d is the concatenation of segments segFirst[d] .. segFirst[d+1]-1;
  * segment s is bytes[segOffsets[s] .. +segLengths[s]).  segFirst has

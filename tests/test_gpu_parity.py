@@ -326,6 +326,33 @@ def test_verify_batch(ctx, oracle_lib):
         assert (d_comp.cpu().numpy().view(np.uint32) == exp_comp).all()
 
 
+@pytest.mark.parametrize("n", [1, 3000, 70_000])
+def test_verify_binned(ctx, oracle_lib, n):
+    """Binned receive verify: mixed-length DGRAMs (6..1400 B, 2- and 4-byte headers),
+    half correctly stamped, the rest corrupted or unstamped; ok/computed in caller order."""
+    rng = np.random.default_rng(31 + n)
+    payload, off, lens, slot, conn = _verify_inputs(rng, n)
+    stamped = oracle_lib.batch(payload, off, lens, threads=8)
+    good = rng.integers(0, 2, size=n) == 1
+    for i in np.nonzero(good)[0]:
+        o, s = int(off[i]), int(slot[i])
+        payload[o + s:o + s + 4] = np.frombuffer(np.uint32(stamped[i]).tobytes(), np.uint8)
+    exp_ok, exp_comp = oracle_lib.verify(payload, off, lens, slot, conn)
+    for lanes in (1, 4, 8):
+        ctx.set_tuning(lanes, 0)
+        d_ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        d_comp = torch.zeros(n, dtype=torch.int32, device="cuda")
+        wsb = ctx.verify_binned_workspace_size(n)
+        ws = torch.zeros(wsb, dtype=torch.uint8, device="cuda")
+        ctx.verify_batch_device_binned(dev(payload), dev(off), dev(lens), dev(slot), dev(conn), n, d_ok, ws, wsb,
+                                       d_comp, stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert (d_ok.cpu().numpy() == exp_ok).all(), lanes
+        assert (d_comp.cpu().numpy().view(np.uint32) == exp_comp).all(), lanes
+    if n > 1:
+        assert 0 < exp_ok.sum() < n
+
+
 def test_verify_golden(ctx, golden):
     vecs, blob = golden
     vv = [v for v in vecs if v["kind"] == "verify"]
