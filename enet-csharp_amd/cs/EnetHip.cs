@@ -217,6 +217,17 @@ namespace enet
                 EnetHipNative.enet_hip_crc32_batch_device_binned(Handle, bytes, offsets, lengths, count, output,
                                                                  workspace, workspaceBytes, stream));
 
+        /// <summary>Batched receive verify for DGRAMs of mixed lengths (records ordered by length per
+        /// 1024-DGRAM tile in <paramref name="workspace" />, EnetHipNative.enet_hip_verify_binned_workspace_size
+        /// bytes); ok[i] / computed[i] in caller order.</summary>
+        public void VerifyDeviceBinned(byte* bytes, ulong* offsets, uint* lengths, uint* slotOffsets, uint* connectIds,
+                                       nuint count, byte* ok, void* workspace, nuint workspaceBytes,
+                                       uint* computed = null, IntPtr stream = default)
+            => EnetHip.Check("enet_hip_verify_batch_device_binned",
+                EnetHipNative.enet_hip_verify_batch_device_binned(Handle, bytes, offsets, lengths, slotOffsets,
+                                                                  connectIds, count, ok, computed, workspace,
+                                                                  workspaceBytes, stream));
+
         /// <summary>Batched receive verify (c/protocol.cs:1052-1068); ok[i] = 1 keeps DGRAM i.</summary>
         public void VerifyDevice(byte* bytes, ulong* offsets, uint* lengths, uint* slotOffsets, uint* connectIds,
                                  nuint count, byte* ok, uint* computed = null, IntPtr stream = default)
