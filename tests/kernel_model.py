@@ -493,3 +493,39 @@ def lean_group(arena: bytes, offs: list[int], lens: list[int], P: int, check_ban
             total = mulmod(total, img[cinv_addr(tz) // 4])
         out.append(finalize(total))
     return out
+
+
+# ---------------------------------------------------------------- length bins
+# bin_tile_kernel (crc32_lean.hip): placement of the ordered records.
+
+BIN_TILE = 1024
+
+
+def bin_of(length: int) -> int:
+    """32-byte bins, longest first (bin 0 holds lengths >= 8160)."""
+    return 255 - min(length >> 5, 255)
+
+
+def binned_order(lens, kpk: int):
+    """Caller index held by each record position: every 1024-packet tile sorted by
+    bin (ties in index order here; on the GPU the order inside a bin is free), sorted
+    group q of full tile t placed as global group q * T + t, a ragged last tile in place."""
+    n = len(lens)
+    full = n // BIN_TILE
+    order = [0] * n
+    for t in range((n + BIN_TILE - 1) // BIN_TILE):
+        ids = range(t * BIN_TILE, min(n, (t + 1) * BIN_TILE))
+        srt = sorted(ids, key=lambda i: (bin_of(int(lens[i])), i))
+        for s, i in enumerate(srt):
+            dst = ((s // kpk) * full + t) * kpk + s % kpk if t < full else t * BIN_TILE + s
+            order[dst] = i
+    return order
+
+
+def group_stage_cost(lens, order, kpk: int, lanes: int) -> int:
+    """Sum over groups of the group's stage count (its longest packet, P*32-byte stages):
+    the lean kernel's work in stages, whatever the packets' own lengths."""
+    total = 0
+    for g in range(0, len(order), kpk):
+        total += max((int(lens[i]) + 31) // 32 // lanes + 1 for i in order[g:g + kpk])
+    return total
