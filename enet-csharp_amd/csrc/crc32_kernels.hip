@@ -1298,7 +1298,9 @@ int enet_hip_crc32_batch_device_binned(enet_hip_context* ctx, const uint8_t* byt
     pa.off = offsets;
     pa.len = lengths;
     pa.n = count;
-    pa.lg = static_cast<uint32_t>(log2i(auto_lanes(ctx)));
+    // mixed lengths (mean well under the 1200-B MTU payload): 4 lanes per packet unless set
+    // (cfg3: 3160-3217 GiB/s at 4 lanes against 2495 at 8, profiles/r01e_*, r01f_*)
+    pa.lg = static_cast<uint32_t>(log2i(ctx->lanes_per_packet > 0 ? ctx->lanes_per_packet : 4));
     pa.out = out;
     // the ordered records only pay on the lean kernel; every other path reads len/off itself
     const bool lean = ctx->path != 1 && (pa.lg == 2 || pa.lg == 3) &&

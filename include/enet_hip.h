@@ -98,7 +98,8 @@ ENET_HIP_API int enet_hip_crc32_batch_device(enet_hip_context* ctx, const uint8_
  * device memory of at least enet_hip_binned_workspace_size(count) bytes (16 per
  * packet: the ordered {len, off_lo, off_hi, index} records), 16-byte aligned, not
  * shared with a call in flight on another stream; count < 2^32.  No state is
- * kept between calls; graph-capturable. */
+ * kept between calls; graph-capturable.  Runs 4 lanes per packet unless
+ * enet_hip_set_tuning chose a count. */
 ENET_HIP_API size_t enet_hip_binned_workspace_size(size_t count);
 ENET_HIP_API int enet_hip_crc32_batch_device_binned(enet_hip_context* ctx, const uint8_t* bytes,
                                                     const uint64_t* offsets, const uint32_t* lengths,
