@@ -131,34 +131,49 @@ __device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint
     }
 }
 
+// One wave copies kCopyCmds commands at a time as one flat space of 16-byte chunks
+// (chunk k of the wave belongs to the command whose prefix range holds it), so a
+// 1360-byte fragment no longer leaves a third of the lanes idle in its second pass.
+// Every write stays inside [dst, dst + len) of its own command.
+constexpr uint32_t kCopyCmds = 4;
+
 __global__ void __launch_bounds__(256) frag_copy_kernel(FragArgs a) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t wstride = static_cast<uint64_t>(gridDim.x) * (blockDim.x >> 6);
-    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6); i < a.n;
-         i += 2 * wstride) {
-        const uint64_t j = i + wstride;
-        const bool hj = j < a.n;
-        const uint32_t Li = a.copy_len[i], Lj = hj ? a.copy_len[j] : 0u;
-        const uint64_t ci = a.copy_claim[i], cj = hj ? a.copy_claim[j] : ~0ull;
-        const uint8_t* si = a.bytes + a.copy_src[i];
-        const uint8_t* sj = a.bytes + (hj ? a.copy_src[j] : 0u);
-        uint8_t* di = a.msg_bytes + a.copy_dst[i];
-        uint8_t* dj = a.msg_bytes + (hj ? a.copy_dst[j] : 0u);
-        if (lane == 0) {
-            if (ci != ~0ull) a.claim[ci] = ~0u;
-            if (cj != ~0ull) a.claim[cj] = ~0u;
+    const uint64_t waves = static_cast<uint64_t>(gridDim.x) * (blockDim.x >> 6);
+    const uint64_t w = static_cast<uint64_t>(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    for (uint64_t base = w * kCopyCmds; base < a.n; base += waves * kCopyCmds) {
+        uint32_t L[kCopyCmds], pre[kCopyCmds + 1];
+        uint64_t src[kCopyCmds], dst[kCopyCmds];
+        pre[0] = 0;
+#pragma unroll
+        for (uint32_t c = 0; c < kCopyCmds; ++c) {
+            const uint64_t i = base + c;
+            const bool h = i < a.n;
+            L[c] = h ? a.copy_len[i] : 0u;
+            src[c] = h ? a.copy_src[i] : 0u;
+            dst[c] = h ? a.copy_dst[i] : 0u;
+            pre[c + 1] = pre[c] + ((L[c] + 15u) >> 4);
+            if (h && lane == c) {
+                const uint64_t ci = a.copy_claim[i];
+                if (ci != ~0ull) a.claim[ci] = ~0u;                // claim words back to ~0 for the next batch
+            }
         }
-        const uint32_t L = max(Li, Lj);
-        for (uint32_t x = 16u * lane; x < L; x += 1024u) {
-            // loads of both commands first, then the stores
-            const bool fi = x + 16u <= Li, fj = x + 16u <= Lj;
-            u32x4v vi = {0, 0, 0, 0}, vj = {0, 0, 0, 0};
-            if (fi) __builtin_memcpy(&vi, si + x, 16);
-            if (fj) __builtin_memcpy(&vj, sj + x, 16);
-            if (fi) __builtin_memcpy(di + x, &vi, 16);
-            else if (x < Li) copy_span(si, di, Li, x);
-            if (fj) __builtin_memcpy(dj + x, &vj, 16);
-            else if (x < Lj) copy_span(sj, dj, Lj, x);
+        for (uint32_t k = lane; k < pre[kCopyCmds]; k += 64u) {
+            uint32_t c = 0;
+#pragma unroll
+            for (uint32_t q = 1; q < kCopyCmds; ++q) c += k >= pre[q] ? 1u : 0u;
+            uint32_t Lc = L[0], pc = pre[0];
+            uint64_t sc = src[0], dc = dst[0];
+#pragma unroll
+            for (uint32_t q = 1; q < kCopyCmds; ++q)
+                if (c == q) {
+                    Lc = L[q];
+                    pc = pre[q];
+                    sc = src[q];
+                    dc = dst[q];
+                }
+            const uint32_t x = (k - pc) << 4;
+            copy_span(a.bytes + sc, a.msg_bytes + dc, Lc, x);
         }
     }
 }
@@ -169,7 +184,8 @@ int fragment_reassemble_launch(const FragArgs& a, int num_cus, hipStream_t st) {
     if (a.n == 0) return 0;
     const uint64_t cap = static_cast<uint64_t>(num_cus) * 8u;
     const unsigned g_thr = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>((a.n + 255) / 256, cap)));
-    const unsigned g_wave = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>((a.n + 3) / 4, cap)));
+    const unsigned g_wave = static_cast<unsigned>(
+        std::max<uint64_t>(1, std::min<uint64_t>((a.n + 4 * kCopyCmds - 1) / (4 * kCopyCmds), cap)));
     hipLaunchKernelGGL(frag_claim_kernel, dim3(g_thr), dim3(256), 0, st, a);
     hipLaunchKernelGGL(frag_decide_kernel, dim3(g_thr), dim3(256), 0, st, a);
     hipLaunchKernelGGL(frag_copy_kernel, dim3(g_wave), dim3(256), 0, st, a);
