@@ -81,46 +81,83 @@ __global__ void __launch_bounds__(256) frag_claim_kernel(FragArgs a) {
     const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
     for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < a.n; i += stride) {
         const Frag f = parse(a, i);
-        if (f.valid) atomicMin(a.claim + claim_index(a, f), static_cast<uint32_t>(i));
+        const uint64_t cidx = f.valid ? claim_index(a, f) : ~0ull;
+        if (f.valid) atomicMin(a.claim + cidx, static_cast<uint32_t>(i));
         a.status[i] = f.valid ? 0 : (f.slot < 0 ? 0 : -1);
+        // the parsed command for the decide kernel (its copy descriptor slots, overwritten there)
+        a.copy_claim[i] = cidx;
+        a.copy_src[i] = f.len;
+        a.copy_dst[i] = static_cast<uint64_t>(f.offset) | (static_cast<uint64_t>(static_cast<uint32_t>(f.slot)) << 32);
+        a.copy_len[i] = 0;                                   // nothing to copy unless a decide kernel says so
     }
 }
 
 // Thread per command: the claim winner tests-and-sets the bitmap bit (a bit set
 // by an earlier batch = duplicate) and decrements remaining; every command gets a
 // copy descriptor (len 0 = nothing to copy) for the copy kernel.
+// Reads the command as the claim kernel parsed it (no second parse of the arena).
 __global__ void __launch_bounds__(256) frag_decide_kernel(FragArgs a) {
     const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
     for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < a.n; i += stride) {
-        const Frag f = parse(a, i);
+        const uint64_t cidx = a.copy_claim[i];
         uint32_t len = 0;
-        uint64_t src = 0, dst = 0, cidx = ~0ull;
-        if (f.valid) {
-            cidx = claim_index(a, f);
-            if (a.claim[cidx] == static_cast<uint32_t>(i)) {             // first command of the batch for it
-                const uint32_t bit = 1u << (f.number & 31u);
-                const uint32_t old =
-                    atomicOr(a.fragments + static_cast<uint64_t>(f.slot) * a.words + (f.number >> 5), bit);   // 619, 623
-                if (!(old & bit)) {
-                    atomicSub(a.remaining + f.slot, 1u);                 // --fragmentsRemaining (621)
-                    a.status[i] = 1;
-                    len = min(f.len, a.msg_len[f.slot] - f.offset);      // clamp (625-626)
-                    src = a.cmd_off[i] + kCmdBytes;
-                    dst = a.msg_off[f.slot] + f.offset;
-                }
+        uint64_t src = 0, dst = 0;
+        if (cidx != ~0ull && a.claim[cidx] == static_cast<uint32_t>(i)) {   // first command of the batch for it
+            const uint64_t packed = a.copy_dst[i];
+            const uint32_t slot = static_cast<uint32_t>(packed >> 32), offset = static_cast<uint32_t>(packed);
+            const uint32_t number = static_cast<uint32_t>(cidx - (static_cast<uint64_t>(slot) * a.words << 5));
+            const uint32_t bit = 1u << (number & 31u);
+            const uint32_t old =
+                atomicOr(a.fragments + static_cast<uint64_t>(slot) * a.words + (number >> 5), bit);   // 619, 623
+            if (!(old & bit)) {
+                atomicSub(a.remaining + slot, 1u);                       // --fragmentsRemaining (621)
+                a.status[i] = 1;
+                len = min(static_cast<uint32_t>(a.copy_src[i]), a.msg_len[slot] - offset);   // clamp (625-626)
+                src = a.cmd_off[i] + kCmdBytes;
+                dst = a.msg_off[slot] + offset;
             }
         }
         a.copy_src[i] = src;
         a.copy_dst[i] = dst;
         a.copy_len[i] = len;
-        a.copy_claim[i] = cidx;
     }
 }
 
-// Wave per two commands (i, i + wstride, their copies overlapped):
-// memcpy(packet->data + fragmentOffset, command + 24, length) (protocol.cs:628-630)
-// with 16-byte lanes; lane 0 also returns each command's claim word to ~0 (every
-// decide read is done).
+// Same decisions without atomics: one wave owns a slot and walks its claim words
+// 64 fragment numbers at a time; the winner (first command of the batch) of a
+// fragment whose bitmap bit is clear sets it, counts it off fragmentsRemaining and
+// gets its copy descriptor.  Used when the claim space (slots x bitmap bits) is
+// not much larger than the batch.
+__global__ void __launch_bounds__(256) frag_decide_slots_kernel(FragArgs a) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t waves = static_cast<uint64_t>(gridDim.x) * (blockDim.x >> 6);
+    const uint32_t bits = a.words << 5;
+    for (uint64_t sl = static_cast<uint64_t>(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6); sl < a.slot_count;
+         sl += waves) {
+        uint32_t* bm = a.fragments + sl * a.words;
+        uint32_t removed = 0;
+        for (uint32_t f0 = 0; f0 < bits; f0 += 64u) {
+            const uint32_t f = f0 + lane;
+            const uint32_t w = f < bits ? a.claim[sl * bits + f] : ~0u;
+            bool take = false;
+            if (w != ~0u) take = ((bm[f >> 5] >> (f & 31u)) & 1u) == 0u;               // 619-620
+            const uint64_t m = __ballot(take);
+            if (lane == 0u && static_cast<uint32_t>(m)) bm[f0 >> 5] |= static_cast<uint32_t>(m);        // 623
+            if (lane == 32u && (m >> 32) && (f0 >> 5) + 1u < a.words) bm[(f0 >> 5) + 1u] |= static_cast<uint32_t>(m >> 32);
+            removed += static_cast<uint32_t>(__builtin_popcountll(m));
+            if (take) {
+                const uint64_t packed = a.copy_dst[w];
+                const uint32_t offset = static_cast<uint32_t>(packed);
+                a.status[w] = 1;
+                a.copy_len[w] = min(static_cast<uint32_t>(a.copy_src[w]), a.msg_len[sl] - offset);   // 625-626
+                a.copy_src[w] = a.cmd_off[w] + kCmdBytes;
+                a.copy_dst[w] = a.msg_off[sl] + offset;
+            }
+        }
+        if (lane == 0u && removed) a.remaining[sl] -= removed;                     // 621
+    }
+}
+
 __device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint32_t L, uint32_t x) {
     if (x + 16u <= L) {
         u32x4v v;
@@ -187,7 +224,13 @@ int fragment_reassemble_launch(const FragArgs& a, int num_cus, hipStream_t st) {
     const unsigned g_wave = static_cast<unsigned>(
         std::max<uint64_t>(1, std::min<uint64_t>((a.n + 4 * kCopyCmds - 1) / (4 * kCopyCmds), cap)));
     hipLaunchKernelGGL(frag_claim_kernel, dim3(g_thr), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(frag_decide_kernel, dim3(g_thr), dim3(256), 0, st, a);
+    const uint64_t claim_space = a.slot_count * (static_cast<uint64_t>(a.words) << 5);
+    if (claim_space <= 8u * a.n + 65536u) {
+        const unsigned g_slot = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>((a.slot_count + 3) / 4, cap)));
+        hipLaunchKernelGGL(frag_decide_slots_kernel, dim3(g_slot), dim3(256), 0, st, a);
+    } else {
+        hipLaunchKernelGGL(frag_decide_kernel, dim3(g_thr), dim3(256), 0, st, a);
+    }
     hipLaunchKernelGGL(frag_copy_kernel, dim3(g_wave), dim3(256), 0, st, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : -static_cast<int>(e);

@@ -87,3 +87,18 @@ def test_cfg5_round_trip(ctx):  # noqa: F811
     assert (status == 1).all() and (st["remaining"] == 0).all()
     body = np.concatenate(fb.messages)
     assert (st["msg_bytes"][:len(body)] == body).all()
+
+
+@pytest.mark.parametrize("words", [None, 64])
+def test_fragments_both_decide_paths(ctx, oracle_lib, words):  # noqa: F811
+    """Small batches against a large claim space (slots x bitmap bits > 8 n + 65536) take
+    the atomic decide kernel; dense ones the slot-owned, atomic-free one.  Both must equal
+    the sequential reference, duplicates and earlier batches included."""
+    rng = np.random.default_rng(29)
+    fb = workloads.fragments(rng.integers(1, 60000, 400), seed=30, duplicates=0.5)
+    so, sg = state(fb, words), state(fb, words)
+    order = rng.permutation(fb.n)
+    for sel in (order[:300], order[300:900], order[900:]):    # 400 x 32 x words claim words
+        assert (run_gpu(ctx, fb, sg, np.sort(sel)) == run_oracle(oracle_lib, fb, so, np.sort(sel))).all()
+    for k in ("msg_bytes", "fragments", "remaining"):
+        assert (so[k] == sg[k]).all(), k
