@@ -275,6 +275,17 @@ def make_batches(cfg: str, rotate: int, rank: int):
     return out
 
 
+def kernel_name(args) -> str:
+    """The dominant kernel of the measured entry point (as rocprofv3 names it)."""
+    lanes = args.lanes or 4
+    lg = {4: 2, 8: 3}.get(lanes)
+    if args.binned:
+        return f"crc32_lean_kernel<0, {lg}, 16, 2, 128>"
+    if lg is None:
+        return "crc32_stream_kernel / crc32_direct_kernel"
+    return f"crc32_vring_kernel<{lg}, 4, 0>"
+
+
 def load_traffic(cfg: str):
     """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/), or None."""
     p = os.path.join(ROOT, "profiles", f"traffic_{cfg}.json")
@@ -378,7 +389,7 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": (traffic or {}).get("hbm_bytes_per_launch"),
-                "kernel": "crc32_lean_kernel<0, 3, 16, 2>",
+                "kernel": kernel_name(args),
                 "kernel_ms": round(r_ms, 5),
                 "kernel_ms_timing": f"HIP events around {nk} serial launches on the launch stream",
                 "kernel_ms_bracketed_median": round(k_ms, 5),

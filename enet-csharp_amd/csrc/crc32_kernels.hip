@@ -30,6 +30,7 @@
 #include "crc32_device.hpp"
 #include "crc32_math.hpp"
 #include "crc32_lean.hpp"
+#include "crc32_vring.hpp"
 #include "crc32_stream_common.hpp"
 #include "enet_hip.h"
 #include "fragment_kernels.hpp"
@@ -864,6 +865,7 @@ struct enet_hip_context {
     uint32_t* d_init = nullptr;  // 32
     uint8_t* d_zero = nullptr;   // 256 zero bytes
     uint32_t* d_basis = nullptr; // lean-kernel table basis, kBasisDwords per image
+    uint32_t* d_basis2 = nullptr; // vring-kernel table basis, kVrBasisDwords per image
     int lanes_per_packet = 0;    // 0 = auto
     int wgs_per_cu = 0;          // 0 = auto (direct / gather kernels)
     int path = 0;                // 0 = stream (default geometry), 1 = direct, 2+k = stream geometry k
@@ -908,13 +910,13 @@ constexpr int kImages = 4;                             // P = 1, 4, 8, 16
 constexpr int kImageP[kImages] = {1, 4, 8, 16};
 
 struct HostTables {
-    std::vector<uint32_t> image, xn, init, basis;
-    bool basis_ok = true;   // the basis rebuilds every image dword the lean kernel reads
+    std::vector<uint32_t> image, xn, init, basis, basis2;
+    bool basis_ok = true;   // the bases rebuild every image dword the lean / vring kernels read
     HostTables()
-        : image(static_cast<size_t>(kImages) * kImageDwords), xn(2 * kXnEntries), init(32),
-          basis(static_cast<size_t>(kImages) * kBasisDwords) {
+        : image(static_cast<size_t>(kImages) * kImageDwords), xn(2 * kXnEntries), init(64),
+          basis(static_cast<size_t>(kImages) * kBasisDwords), basis2(static_cast<size_t>(kImages) * kVrBasisDwords) {
         init[0] = 0xFFFFFFFFu;
-        for (int r = 1; r < 32; ++r) init[r] = unstep_zero(init[r - 1]);
+        for (int r = 1; r < 64; ++r) init[r] = unstep_zero(init[r - 1]);
         std::vector<uint32_t> cinv(kCinvEntries);
         uint32_t xinv8 = kOneReflected;
         for (int i = 0; i < 8; ++i) xinv8 = gf2_mulmod(xinv8, x_inverse());
@@ -938,7 +940,7 @@ struct HostTables {
                 for (uint32_t b = 0; b < 4; ++b)
                     for (uint32_t v = 0; v < 256; ++v)
                         img[(256u * v + corr_col(k, b)) / 4] = gf2_mulmod(v << (8 * b), cinv[32 * k]);
-            for (uint32_t r = 0; r < 32; ++r) img[init_addr(r) / 4] = init[r];
+            for (uint32_t r = 0; r < 64; ++r) img[init_addr(r) / 4] = init[r];
             for (uint32_t i = 0; i < static_cast<uint32_t>(kCinvEntries); ++i) img[cinv_addr(i) / 4] = cinv[i];
             // lean-kernel basis: image rows 2^b of the linear columns, then INIT | CINV
             uint32_t* bs = basis.data() + static_cast<size_t>(im) * kBasisDwords;
@@ -949,8 +951,16 @@ struct HostTables {
                 bs[512 + r] = init[r];
                 bs[544 + r] = cinv[r];
             }
+            // vring-kernel basis: the same linear rows, then INIT[0..63], CINV[0..63]
+            uint32_t* b2 = basis2.data() + static_cast<size_t>(im) * kVrBasisDwords;
+            for (uint32_t d = 0; d < 512; ++d) b2[d] = bs[d];
+            for (uint32_t r = 0; r < 64; ++r) {
+                b2[512 + r] = init[r];
+                b2[576 + r] = cinv[r];
+            }
             // what crc32_lean.hip rebuilds must equal the image wherever that kernel
-            // looks (INIT rows < 32, CINV rows < 16; CINV n >= 256 never)
+            // looks (INIT rows < 32, CINV rows < 16; CINV n >= 256 never); the same
+            // for crc32_vring.hip with INIT / CINV rows < 64
             for (uint32_t j = 0; j < 256; ++j)
                 for (uint32_t d = 0; d < 64; ++d) {
                     if (d == kCinvDword + 2u || ((d == kInitDword || d == kCinvDword) && j >= 32)) continue;
@@ -959,6 +969,16 @@ struct HostTables {
                         if ((j >> b) & 1u) v ^= bs[64 * b + d];
                     if (d == kInitDword) v = bs[512 + j];
                     if (d == kCinvDword) v = bs[544 + j];
+                    if (v != img[64 * j + d]) basis_ok = false;
+                }
+            for (uint32_t j = 0; j < 256; ++j)
+                for (uint32_t d = 0; d < 64; ++d) {
+                    if (d == kCinvDword + 2u || ((d == kInitDword || d == kCinvDword) && j >= 64)) continue;
+                    uint32_t v = 0;
+                    for (uint32_t b = 0; b < 8; ++b)
+                        if ((j >> b) & 1u) v ^= b2[64 * b + d];
+                    if (d == kInitDword) v = b2[512 + j];
+                    if (d == kCinvDword) v = b2[576 + j];
                     if (v != img[64 * j + d]) basis_ok = false;
                 }
         }
@@ -976,7 +996,12 @@ const HostTables& host_tables() {
     return t;
 }
 
-int auto_lanes(const enet_hip_context* ctx) { return ctx->lanes_per_packet > 0 ? ctx->lanes_per_packet : 8; }
+// Default lanes per packet: 4 for checksum batches (vring kernel: 5650 vs 5369 GB/s
+// at 8 on cfg2 with overlapped launches, profiles/r02_*), 8 for receive verify
+// (lean kernel).
+int auto_lanes(const enet_hip_context* ctx, int mode = 0) {
+    return ctx->lanes_per_packet > 0 ? ctx->lanes_per_packet : (mode == 0 ? 4 : 8);
+}
 
 int log2i(int v) {
     int l = 0;
@@ -1061,6 +1086,7 @@ using VStreamGeoms = std::tuple<VGeom<16, 3, 3>, VGeom<16, 2, 3>, VGeom<16, 4, 4
 constexpr int kNumVStreamGeoms = std::tuple_size<VStreamGeoms>::value;
 // lean kernel geometries (crc32_lean.hip): paths kLeanPath0 + geom; path 0 runs geom 0
 constexpr int kLeanPath0 = 2 + kNumStreamGeoms + kNumVStreamGeoms;
+constexpr int kVringPath = kLeanPath0 + kLeanGeoms;     // crc32_vring.hip (path 0 for checksum batches)
 
 template <size_t I = 0>
 void launch_stream(int geom, int mode, int abl, int num_cus, uint64_t groups, hipStream_t st,
@@ -1116,8 +1142,12 @@ int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStr
     const_cast<PacketArgs&>(pa).trace = ctx->trace;
     const_cast<PacketArgs&>(pa).prio = static_cast<uint32_t>(ctx->ablation_prio);
     // the stream kernel takes 4, 8 or 16 lanes per packet; anything else runs direct
+    // default (path 0) checksum batches at 4 or 8 lanes: the VGPR-ring kernel
+    if (mode == 0 && !pa.meta4 && (pa.lg == 2 || pa.lg == 3) && ctx->ablation == 0 &&
+        (ctx->path == 0 || ctx->path == kVringPath))
+        return vring_launch(pa.lg, ctx->num_cus, st, pa, tb, ctx->d_basis2);
     if (ctx->path != 1 && pa.lg >= 2 && pa.lg <= 4) {
-        const bool lean_path = ctx->path >= kLeanPath0 || (ctx->path == 0 && ctx->ablation == 0);
+        const bool lean_path = (ctx->path >= kLeanPath0 && ctx->path < kVringPath) || (ctx->path == 0 && ctx->ablation == 0);
         if (lean_path && pa.lg <= 3)
             return lean_launch(mode, pa.lg, ctx->path == 0 ? 0 : ctx->path - kLeanPath0, ctx->ablation,
                                ctx->num_cus, st, pa, tb);
@@ -1185,18 +1215,21 @@ int enet_hip_context_create(int device, enet_hip_context** out) {
         if ((rc = herr(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)))) break;
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_image), ht.image.size() * 4)))) break;
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_xn), ht.xn.size() * 4)))) break;
-        if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_init), 32 * 4)))) break;
+        if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_init), ht.init.size() * 4)))) break;
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_zero), 256)))) break;
         if ((rc = herr(hipMemset(ctx->d_zero, 0, 256)))) break;
         if ((rc = herr(hipMemcpy(ctx->d_image, ht.image.data(), ht.image.size() * 4, hipMemcpyHostToDevice)))) break;
         if ((rc = herr(hipMemcpy(ctx->d_xn, ht.xn.data(), ht.xn.size() * 4, hipMemcpyHostToDevice)))) break;
-        if ((rc = herr(hipMemcpy(ctx->d_init, ht.init.data(), 32 * 4, hipMemcpyHostToDevice)))) break;
+        if ((rc = herr(hipMemcpy(ctx->d_init, ht.init.data(), ht.init.size() * 4, hipMemcpyHostToDevice)))) break;
         if (!ht.basis_ok) {
             rc = -static_cast<int>(hipErrorInvalidImage);
             break;
         }
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_basis), ht.basis.size() * 4)))) break;
         if ((rc = herr(hipMemcpy(ctx->d_basis, ht.basis.data(), ht.basis.size() * 4, hipMemcpyHostToDevice)))) break;
+        if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_basis2), ht.basis2.size() * 4)))) break;
+        if ((rc = herr(hipMemcpy(ctx->d_basis2, ht.basis2.data(), ht.basis2.size() * 4, hipMemcpyHostToDevice)))) break;
+        if ((rc = vring_setup())) break;
         if ((rc = setup_stream())) break;
         if ((rc = setup_vstream())) break;
         if ((rc = lean_setup())) break;
@@ -1224,6 +1257,7 @@ int enet_hip_context_destroy(enet_hip_context* ctx) {
     (void)hipFree(ctx->d_init);
     (void)hipFree(ctx->d_zero);
     (void)hipFree(ctx->d_basis);
+    (void)hipFree(ctx->d_basis2);
     (void)hipFree(ctx->d_bytes);
     (void)hipFree(ctx->d_meta);
     (void)hipFree(ctx->d_claim);
@@ -1245,7 +1279,9 @@ int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgro
 }
 
 int enet_hip_diag_ablation(enet_hip_context* ctx, int mode) {
-    if (!ctx || mode < 0 || mode > 127) return -static_cast<int>(hipErrorInvalidValue);
+    if (!ctx || mode < 0 || mode > 1023) return -static_cast<int>(hipErrorInvalidValue);
+    vring_set_wpe((mode & 512) ? 8 : 4);                      // tuning: two vring workgroups per CU
+    mode &= 511;
     ctx->ablation = mode & ~8;
     ctx->ablation_prio = (mode >> 3) & 1;
     return 0;
@@ -1258,7 +1294,7 @@ int enet_hip_diag_trace(enet_hip_context* ctx, uint64_t* deviceBuffer) {
 }
 
 int enet_hip_set_kernel_path(enet_hip_context* ctx, int path) {
-    if (!ctx || path < 0 || path >= kLeanPath0 + kLeanGeoms) return -static_cast<int>(hipErrorInvalidValue);
+    if (!ctx || path < 0 || path > kVringPath) return -static_cast<int>(hipErrorInvalidValue);
     ctx->path = path;
     return 0;
 }
@@ -1304,7 +1340,7 @@ int enet_hip_crc32_batch_device_binned(enet_hip_context* ctx, const uint8_t* byt
     pa.out = out;
     // the ordered records only pay on the lean kernel; every other path reads len/off itself
     const bool lean = ctx->path != 1 && (pa.lg == 2 || pa.lg == 3) &&
-                      (ctx->path >= kLeanPath0 || (ctx->path == 0 && ctx->ablation == 0));
+                      ((ctx->path >= kLeanPath0 && ctx->path < kVringPath) || (ctx->path == 0 && ctx->ablation == 0));
     if (lean) {
         int rc;
         if ((rc = length_bin(lengths, offsets, nullptr, nullptr, count, 64u >> pa.lg, workspace, st))) return rc;
@@ -1326,7 +1362,7 @@ int enet_hip_verify_batch_device(enet_hip_context* ctx, const uint8_t* bytes, co
     pa.off = offsets;
     pa.len = lengths;
     pa.n = count;
-    pa.lg = static_cast<uint32_t>(log2i(auto_lanes(ctx)));
+    pa.lg = static_cast<uint32_t>(log2i(auto_lanes(ctx, 1)));
     pa.out = computed;
     pa.slot_off = slotOffsets;
     pa.connect = connectIds;
@@ -1351,13 +1387,13 @@ int enet_hip_verify_batch_device_binned(enet_hip_context* ctx, const uint8_t* by
     pa.off = offsets;
     pa.len = lengths;
     pa.n = count;
-    pa.lg = static_cast<uint32_t>(log2i(auto_lanes(ctx)));
+    pa.lg = static_cast<uint32_t>(log2i(auto_lanes(ctx, 1)));
     pa.out = computed;
     pa.slot_off = slotOffsets;
     pa.connect = connectIds;
     pa.ok = ok;
     const bool lean = ctx->path != 1 && (pa.lg == 2 || pa.lg == 3) &&
-                      (ctx->path >= kLeanPath0 || (ctx->path == 0 && ctx->ablation == 0));
+                      ((ctx->path >= kLeanPath0 && ctx->path < kVringPath) || (ctx->path == 0 && ctx->ablation == 0));
     if (lean) {
         int rc;
         if ((rc = length_bin(lengths, offsets, slotOffsets, connectIds, count, 64u >> pa.lg, workspace, st))) return rc;

@@ -99,6 +99,8 @@ __device__ __forceinline__ uint32_t fold_perm(uint32_t reg, const uint32_t (&x)[
     return acc ^ v[31];
 }
 
+constexpr uint32_t floor_pow2(uint32_t v) { return v < 2u ? v : 2u * floor_pow2(v / 2u); }
+
 template <int MODE, int LG, int W, int NB>
 struct LeanGeom {
     static constexpr uint32_t P = 1u << LG, kPk = 64u >> LG;           // lanes / packets per group
@@ -107,7 +109,7 @@ struct LeanGeom {
     static constexpr uint32_t kRing = NB * 2048u;                       // NB stages of 64 lanes x 32 B
     static constexpr uint32_t kWaveLds = (160u * 1024u - kLdsTableBytes) / W / 256u * 256u;
     static constexpr uint32_t kHalf = (kWaveLds - kRing) / 2u / 256u * 256u;
-    static constexpr uint32_t JM = kHalf / (4u * kGroupMeta);          // groups per metadata chunk
+    static constexpr uint32_t JM = floor_pow2(kHalf / (4u * kGroupMeta));   // groups per metadata chunk
     static constexpr uint32_t kMetaOps = JM * kGroupMeta / 64u;
     static constexpr int kThreads = 64 * W;
     static constexpr int kLds = kLdsTableBytes + W * static_cast<int>(kRing + 2u * kHalf);
@@ -139,6 +141,7 @@ __device__ __forceinline__ void wait_vm_sel(uint32_t c) {
 // 16 = synthetic metadata (1200-byte packets packed from offset 0, nothing read);
 // 32 (tuning, correct checksums) = each wave takes a contiguous range of groups;
 // 64 (tuning, correct checksums) = s_setprio 1 for the later-dispatched half of the waves;
+// 256 (tuning, correct checksums) = nt cache policy on the packet-data DMAs;
 // 128 (product, correct checksums) = metadata from the length-ordered records of the
 // *_binned entry points (PacketArgs::meta4): a separate instance, so the plain path
 // carries no per-op test for it.
@@ -284,8 +287,9 @@ __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, Kerne
             a0 = l2;
             a1 = l2 + 1024u;
         }
-        dma16(reinterpret_cast<const void*>(a0), ring + 2048u * slot);
-        dma16(reinterpret_cast<const void*>(a1), ring + 2048u * slot + 1024u);
+        constexpr int kAux = (ABL & 256) ? 2 : 0;           // 256 (tuning): nt data loads
+        dma16_pol<kAux>(reinterpret_cast<const void*>(a0), ring + 2048u * slot);
+        dma16_pol<kAux>(reinterpret_cast<const void*>(a1), ring + 2048u * slot + 1024u);
         pcur += 32u * P;
         ++pst;
     };
@@ -527,6 +531,7 @@ struct LeanVariant {
                 case 16: go_abl<3, 16>(num_cus, st, pa, tb); break;
                 case 32: go_abl<3, 32>(num_cus, st, pa, tb); break;
                 case 64: go_abl<3, 64>(num_cus, st, pa, tb); break;
+                case 256: go_abl<3, 256>(num_cus, st, pa, tb); break;
                 default: break;
             }
             return;
@@ -549,7 +554,10 @@ int lean_setup() {
 int lean_launch(int mode, int lg, int geom, int abl, int num_cus, hipStream_t st, const PacketArgs& pa,
                 const KernelTables& tb) {
     if (lg != 2 && lg != 3) return -static_cast<int>(hipErrorInvalidValue);
-    if (geom == 1) LeanVariant<12, 3>::launch(mode, lg, 0, num_cus, st, pa, tb);
+    // geoms 2, 3 (tuning sweeps): checksum mode, 8 lanes per packet only
+    if (geom == 2 && mode == 0 && lg == 3) LeanVariant<14, 3>::go_abl<3, 0>(num_cus, st, pa, tb);
+    else if (geom == 3 && mode == 0 && lg == 3) LeanVariant<10, 4>::go_abl<3, 0>(num_cus, st, pa, tb);
+    else if (geom == 1) LeanVariant<12, 3>::launch(mode, lg, 0, num_cus, st, pa, tb);
     else LeanVariant<16, 2>::launch(mode, lg, abl, num_cus, st, pa, tb);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : -static_cast<int>(e);

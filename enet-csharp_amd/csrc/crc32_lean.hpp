@@ -7,7 +7,7 @@
 
 namespace enethip {
 
-constexpr int kLeanGeoms = 2;   // 0: 16 waves x 2 stages, 1: 12 waves x 3 stages
+constexpr int kLeanGeoms = 4;   // 0: 16 waves x 2 stages, 1: 12 waves x 3 stages; sweeps: 2: 14 x 3, 3: 10 x 4
 
 // Set the dynamic-LDS attribute of every lean kernel instance (once per context).
 int lean_setup();

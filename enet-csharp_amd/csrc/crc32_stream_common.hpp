@@ -60,6 +60,12 @@ __device__ __forceinline__ void dma16(const void* g, uint32_t lds_addr) {
     __builtin_amdgcn_global_load_lds(g, reinterpret_cast<__attribute__((address_space(3))) void*>(
                                             static_cast<uintptr_t>(lds_addr)), 16, 0, 0);
 }
+// cache-policy variant (AUX = the instruction's cpol immediate: 2 = nt)
+template <int AUX>
+__device__ __forceinline__ void dma16_pol(const void* g, uint32_t lds_addr) {
+    __builtin_amdgcn_global_load_lds(g, reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                            static_cast<uintptr_t>(lds_addr)), 16, 0, AUX);
+}
 __device__ __forceinline__ void dma4(const void* g, uint32_t lds_addr) {
     __builtin_amdgcn_global_load_lds(g, reinterpret_cast<__attribute__((address_space(3))) void*>(
                                             static_cast<uintptr_t>(lds_addr)), 4, 0, 0);

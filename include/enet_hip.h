@@ -71,13 +71,17 @@ ENET_HIP_API int enet_hip_context_destroy(enet_hip_context* ctx);
 ENET_HIP_API const char* enet_hip_error_string(int code);
 
 /* Tuning knobs (0 = automatic).  lanes_per_packet: 1,2,4,...,64 lanes share one
- * packet (a power of two; default 8); workgroups_per_cu: resident workgroups per
- * CU the direct / gather grids are sized for. */
+ * packet (a power of two; default 4 for checksum batches, 8 for receive verify);
+ * workgroups_per_cu: resident workgroups per CU the direct / gather grids are
+ * sized for. */
 ENET_HIP_API int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgroups_per_cu);
 
-/* Kernel path for the packet batch entry points: 0 = LDS-DMA stream kernel
- * (default; needs 4, 8 or 16 lanes per packet, other values run direct),
- * 1 = direct loads only, 2 + k = stream kernel with tuning geometry k (sweeps). */
+/* Kernel path for the packet batch entry points (0 = default): checksum batches
+ * at 4 or 8 lanes per packet run the VGPR-ring kernel (crc32_vring.hip), receive
+ * verify and the length-binned entries the lean LDS-DMA kernel (crc32_lean.hip),
+ * 16 lanes the LDS-ring stream kernel, other lane counts the direct kernel.
+ * Tuning sweeps: 1 = direct loads only, 2 + k = stream kernel geometry k (k < 11),
+ * 13 + g = lean kernel geometry g (g < 4), 17 = the vring kernel. */
 ENET_HIP_API int enet_hip_set_kernel_path(enet_hip_context* ctx, int path);
 
 /* ---- batched checksum, device-resident ----

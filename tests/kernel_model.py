@@ -112,7 +112,7 @@ def unstep_zero(reg_next: int) -> int:
 
 
 INIT = [0xFFFFFFFF]
-for _ in range(31):
+for _ in range(63):                                 # INIT[r], r < 64 (vring windows: lz < 64)
     INIT.append(unstep_zero(INIT[-1]))
 
 
@@ -158,7 +158,7 @@ def lds_image(P: int = 1) -> list[int]:
         for b in range(4):                         # by four byte-indexed lookups
             for v in range(256):
                 img[corr_addr(k, b, v) // 4] = mulmod(v << (8 * b), CINV[32 * k])
-    for r in range(32):
+    for r in range(64):
         img[init_addr(r) // 4] = INIT[r]
     for n in range(512):
         img[cinv_addr(n) // 4] = CINV[n]
@@ -529,3 +529,92 @@ def group_stage_cost(lens, order, kpk: int, lanes: int) -> int:
     for g in range(0, len(order), kpk):
         total += max((int(lens[i]) + 31) // 32 // lanes + 1 for i in order[g:g + kpk])
     return total
+
+
+# ---------------------------------------------------------------- vring kernel
+# crc32_vring.hip: 64-byte-aligned window starts, lane k folds blocks k, k+P, ...
+# loaded straight into registers (halves swapped by the load address when the
+# lane's hs bit is set), lane k ends o = (k - nb) mod P blocks past the window end.
+VR_BASIS_ROWS = 10
+
+
+def vring_basis(P: int) -> list[int]:
+    """HostTables::basis2: rows 0..7 as the lean basis, row 8 = INIT[0..63],
+    row 9 = CINV[0..63]."""
+    return table_basis(P)[:512] + INIT[:64] + CINV[:64]
+
+
+def vring_image_from_basis(B: list[int]) -> list[int]:
+    """crc32_vring.hip's in-LDS rebuild (INIT / CINV rows < 64 from rows 8, 9)."""
+    img = [0] * (256 * 64)
+    for j in range(256):
+        row = [0] * 64
+        for b in range(8):
+            if (j >> b) & 1:
+                row = [x ^ y for x, y in zip(row, B[64 * b:64 * b + 64])]
+        if j < 64:
+            row[KINIT_DWORD] = B[512 + j]
+            row[KCINV_DWORD] = B[576 + j]
+        img[64 * j:64 * j + 64] = row
+    return img
+
+
+_VR_CACHE: dict[int, list[int]] = {}
+
+
+def vring_image(P: int) -> list[int]:
+    if P not in _VR_CACHE:
+        _VR_CACHE[P] = vring_image_from_basis(vring_basis(P))
+    return _VR_CACHE[P]
+
+
+def vring_window(addr: int, L: int):
+    """(ws, lz, e, nb): window start (64-byte aligned), packet bytes [lz, e) of it."""
+    lz = addr & 63
+    e = lz + L
+    nb = (e + 31) // 32 if L else 0
+    return addr - lz, lz, e, nb
+
+
+def vring_packet(arena: bytes, addr: int, L: int, P: int, lane_base: int = 0) -> int:
+    """What crc32_vring_kernel's P lanes (lanes lane_base .. lane_base+P-1) compute
+    for the packet arena[addr:addr+L]; returns the wire CRC."""
+    img = vring_image(P)
+    ws, lz, e, nb = vring_window(addr, L)
+    stages = (nb + P - 1) // P
+    total = 0
+    for k in range(P):
+        lane = lane_base + k
+        col, sel, sw1, sw2, hs = make_sched(lane)
+        reg = (img[init_addr(lz) // 4] if nb else 0xFFFFFFFF) if k == 0 else 0
+        cnt = (nb - 1 - k) // P + 1 if nb > k else 0
+        for st in range(stages):
+            q0 = 32 * (k + P * st)
+            pieces = []
+            for po in ((q0 + 16, q0) if hs else (q0, q0 + 16)):   # lane order A, B
+                valid = po < e and po + 16 > lz
+                pieces.append(arena[ws + po:ws + po + 16] if valid else bytes(16))
+            A = [int.from_bytes(pieces[0][4 * i:4 * i + 4], "little") for i in range(4)]
+            B = [int.from_bytes(pieces[1][4 * i:4 * i + 4], "little") for i in range(4)]
+            orig = (B + A) if hs else (A + B)
+            blk = bytearray(b"".join(v.to_bytes(4, "little") for v in orig))
+            for t in range(32):                    # edge mask: keep [lz, e) only
+                if not (lz <= q0 + t < e):
+                    blk[t] = 0
+            if st >= cnt:
+                continue
+            w = [int.from_bytes(blk[4 * q:4 * q + 4], "little") for q in range(8)]
+            w[0] ^= reg
+            acc = 0
+            for a in lookup_addresses(lane, w):
+                acc ^= img[a // 4]
+            reg = acc
+        o = (k - nb) % P
+        if o:
+            reg = (img[corr_addr(o, 0, reg & 0xFF) // 4] ^ img[corr_addr(o, 1, (reg >> 8) & 0xFF) // 4] ^
+                   img[corr_addr(o, 2, (reg >> 16) & 0xFF) // 4] ^ img[corr_addr(o, 3, reg >> 24) // 4])
+        total ^= reg
+    tz = 32 * nb - e if nb else 0
+    if tz:
+        total = mulmod(total, img[cinv_addr(tz) // 4])
+    return finalize(total)

@@ -1,0 +1,56 @@
+"""Static ISA checks of the VGPR-ring kernel (crc32_vring.hip), CPU only.
+
+The kernel issues its global loads as inline asm and waits for them by hand
+(counted vmcnt), so correctness depends on properties of the generated code,
+checked here on the gfx950 ISA hipcc emits with the Makefile's flags:
+  * no scratch (private) memory: scratch ops are VMEM and would need vmcnt(0);
+  * no instruction reads or overwrites a loaded register before its wait
+    (tools/isa_inflight_check.py);
+  * at most 64 VGPRs, so two 16-wave workgroups fit a CU.
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "enet-csharp_amd")
+HIPCC = "/opt/rocm/bin/hipcc"
+
+
+@pytest.fixture(scope="module")
+def vring_isa(tmp_path_factory):
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not available")
+    out = tmp_path_factory.mktemp("isa") / "vring.s"
+    cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-mllvm", "-simplifycfg-sink-common=false",
+           "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(PKG, "csrc"), "--cuda-device-only", "-S",
+           os.path.join(PKG, "csrc", "crc32_vring.hip"), "-o", str(out)]
+    subprocess.run(cmd, check=True, capture_output=True)
+    return str(out)
+
+
+def test_vring_makefile_flags_match():
+    mk = open(os.path.join(PKG, "Makefile")).read()
+    assert "build/crc32_vring.o:" in mk and "-simplifycfg-sink-common=false" in mk
+
+
+def test_vring_no_scratch_and_vgpr_budget(vring_isa):
+    text = open(vring_isa).read()
+    assert "scratch_" not in text
+    sizes = [int(l.split(":")[1]) for l in text.splitlines() if l.strip().startswith(".private_segment_fixed_size:")]
+    assert sizes and all(v == 0 for v in sizes), sizes
+    names = [l.split(":", 1)[1].strip() for l in text.splitlines() if l.strip().startswith(".name:")]
+    vgprs = [int(l.split(":")[1]) for l in text.splitlines() if l.strip().startswith(".vgpr_count:")]
+    for name, v in zip(names, vgprs):
+        if "ELi1EEEv" in name:            # the trace instance (diagnostics) may use more
+            continue
+        assert v <= 64, (name, v)
+
+
+def test_vring_loads_not_touched_before_wait(vring_isa):
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import isa_inflight_check as chk
+    assert chk.main(vring_isa) == 0

@@ -216,3 +216,34 @@ def test_binned_order_is_a_permutation_and_balances_groups():
         plain = km.group_stage_cost(lens, list(range(n)), kpk, lanes)
         binned = km.group_stage_cost(lens, order, kpk, lanes)
         assert binned < 0.7 * plain, (lanes, binned, plain)
+
+
+@pytest.mark.parametrize("P", [4, 8])
+def test_vring_image_from_basis(P):
+    """crc32_vring.hip rebuilds its LDS image from the 10-row basis2: equal to the
+    host image wherever that kernel reads (INIT / CINV rows < 64, CINV n < 256)."""
+    img, rb = km.image(P), km.vring_image(P)
+    for j in range(256):
+        for d in range(64):
+            if d == km.KCINV_DWORD + 2 or (d in (km.KINIT_DWORD, km.KCINV_DWORD) and j >= 64):
+                continue
+            assert rb[64 * j + d] == img[64 * j + d], (j, d)
+
+
+@pytest.mark.parametrize("P", [4, 8])
+def test_vring_model_matches_oracle(P):
+    """The vring kernel's arithmetic (64-byte-aligned window starts, zero-line
+    pieces, edge masks, strided advancing folds, lane overshoot corrections
+    x^(-256 o), tz correction) equals packet.cs:142-160 for every start alignment
+    mod 64 and lengths across block / stage boundaries, empty packets included."""
+    rng = random.Random(0x5652 + P)
+    arena = bytes(rng.getrandbits(8) for _ in range(16384))
+    ol = oracle.OracleLib()
+    cases = [(a, L) for a in range(0, 64, 5) for L in (0, 1, 15, 16, 17, 31, 32, 33, 63, 64, 65)]
+    cases += [(rng.randrange(0, 2048), rng.randrange(0, 1500)) for _ in range(40)]
+    cases += [(1200 * i, 1200) for i in range(8)]          # cfg2 shapes
+    for a, L in cases:
+        lane_base = P * rng.randrange(0, 64 // P)
+        got = km.vring_packet(arena, 128 + a, L, P, lane_base)
+        exp = ol.crc32(arena[128 + a:128 + a + L])
+        assert got == exp, (a, L, P, hex(got), hex(exp))

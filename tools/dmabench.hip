@@ -15,20 +15,41 @@ template <int N>
 __device__ __forceinline__ void waitvm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
 template <int W, int NB, int PAT, int AUX>
-__global__ void __launch_bounds__(64 * W) k_dma(const uint8_t* buf, uint64_t units, uint32_t* sink, uint64_t* trace) {
+__global__ void __launch_bounds__(64 * W) k_dma(const uint8_t* buf, uint64_t units, uint32_t* sink, uint64_t* trace,
+                                                const uint8_t* zero) {
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t wv = (uint64_t)blockIdx.x * W + wave, wt = (uint64_t)gridDim.x * W;
-    const uint64_t J = wv < units ? (units - 1 - wv) / wt + 1 : 0;
+    // PAT >= 2: units = groups, J = stages
+    constexpr uint64_t kStg = PAT == 4 ? 3u : PAT >= 2 ? 5u : 1u;
+    const uint64_t J = (wv < units ? (units - 1 - wv) / wt + 1 : 0) * kStg;
     const uint32_t ring = wave * NB * 2048u;
     auto issue = [&](uint64_t j, uint32_t slot) __attribute__((always_inline)) {
-        const uint64_t u = wv + min(j, J - 1) * wt;      // clamped: constant op count
+        const uint64_t jj = min(j, J - 1);
+        const uint64_t u = wv + jj * wt;      // clamped: constant op count
         const uint8_t* base = buf + u * 2048u;
+        // PAT >= 2: lean-kernel-like packet chunks.  Groups of 64/PL packets of
+        // 1200 B packed; a group takes STG stages; stage s of packet p reads the
+        // PL*32-byte chunk s of its window (window = lean's 16-B-aligned end, or for
+        // PAT 3 a 128-B-aligned start); pieces wholly outside read a zero line.
+        constexpr uint32_t PL = PAT == 4 ? 16u : 8u, NPK = 64u / PL;
+        constexpr uint32_t NBW = PAT == 3 ? 40u : PAT == 5 ? 39u : 38u;   // window blocks of a 1200-B packet
+        constexpr uint32_t STG = (NBW + PL - 1) / PL;
+        const uint64_t grp = wv + (jj / STG) * wt, s = jj % STG;
+        const uint32_t p = lane / PL, k = lane % PL;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            const uint8_t* g = PAT == 0 ? base + 1024u * i + 16u * lane : base + 32u * lane + 16u * i;
+            const uint8_t* g;
+            if constexpr (PAT >= 2) {
+                const uint64_t start = (grp * NPK + p) * 1200u;
+                const uint64_t ws = PAT == 3 ? (start & ~127ull) : PAT == 5 ? (start & ~63ull) : (start >= 16u ? start - 16u : 0u);
+                const uint32_t piece = (uint32_t)s * 2u * PL + i * PL + k;
+                g = piece < 2u * NBW ? buf + ws + 16u * piece : zero;
+            } else {
+                g = PAT == 0 ? base + 1024u * i + 16u * lane : base + 32u * lane + 16u * i;
+            }
             __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(uintptr_t)(ring + slot * 2048u + 1024u * i),
                                              16, 0, AUX);
         }
@@ -92,8 +113,14 @@ static int launch_dma(const void* buf, uint64_t bytes, int grid, uint32_t* sink,
         hipFuncSetAttribute((const void*)k_dma<W, NB, PAT, AUX>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         set = true;
     }
-    hipLaunchKernelGGL((k_dma<W, NB, PAT, AUX>), dim3(grid), dim3(64 * W), lds, s, (const uint8_t*)buf, bytes / 2048,
-                       sink, g_trace);
+    static uint8_t* zero = nullptr;
+    if (!zero) {
+        hipMalloc(&zero, 4096);
+        hipMemset(zero, 0, 4096);
+    }
+    const uint64_t units = PAT == 4 ? bytes / 4800 : PAT >= 2 ? bytes / 9600 : bytes / 2048;
+    hipLaunchKernelGGL((k_dma<W, NB, PAT, AUX>), dim3(grid), dim3(64 * W), lds, s, (const uint8_t*)buf, units,
+                       sink, g_trace, zero);
     return (int)hipGetLastError();
 }
 
@@ -117,15 +144,30 @@ extern "C" int db_dma(int cfg, const void* buf, uint64_t bytes, int grid, uint32
         CASE(11, 12, 4, 1, 0)
         CASE(12, 4, 8, 0, 0)
         CASE(13, 8, 8, 0, 0)
+        CASE(14, 16, 2, 2, 0)
+        CASE(15, 16, 2, 3, 0)
+        CASE(16, 16, 2, 4, 0)
+        CASE(17, 16, 2, 0, 2)
+        CASE(18, 16, 2, 2, 2)
+        CASE(19, 16, 2, 3, 2)
+        CASE(20, 16, 3, 2, 0)
+        CASE(21, 16, 3, 3, 0)
+        CASE(22, 16, 2, 5, 0)
+        CASE(23, 16, 3, 5, 0)
+        CASE(24, 14, 3, 2, 0)
+        CASE(25, 10, 4, 2, 0)
         default: return -1;
     }
 }
-extern "C" int db_ncfg() { return 14; }
+extern "C" int db_ncfg() { return 26; }
 extern "C" const char* db_name(int cfg) {
     static const char* n[] = {"W16 NB2 dense", "W16 NB3 dense", "W16 NB4 dense", "W8 NB4 dense", "W8 NB6 dense",
                               "W16 NB2 half", "W16 NB3 half", "W16 NB4 half", "W16 NB3 dense nt", "W16 NB3 half nt",
-                              "W12 NB4 dense", "W12 NB4 half", "W4 NB8 dense", "W8 NB8 dense"};
-    return cfg < 14 ? n[cfg] : "?";
+                              "W12 NB4 dense", "W12 NB4 half", "W4 NB8 dense", "W8 NB8 dense",
+                              "W16 NB2 lean8", "W16 NB2 lean8 a128", "W16 NB2 lean16", "W16 NB2 dense nt",
+                              "W16 NB2 lean8 nt", "W16 NB2 lean8 a128 nt", "W16 NB3 lean8", "W16 NB3 lean8 a128",
+                              "W16 NB2 lean8 a64", "W16 NB3 lean8 a64", "W14 NB3 lean8", "W10 NB4 lean8"};
+    return cfg < 26 ? n[cfg] : "?";
 }
 
 extern "C" int db_probe(int cfg, const void* buf, uint64_t bytes, int grid, uint32_t* sink, void* st) {

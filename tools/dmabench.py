@@ -27,7 +27,7 @@ def main():
     lib = ctypes.CDLL(SO)
     lib.db_name.restype = ctypes.c_char_p
     nbytes = 78643200
-    bufs = [torch.randint(0, 255, (nbytes,), dtype=torch.uint8, device="cuda") for _ in range(5)]
+    bufs = [torch.randint(0, 255, (nbytes + 4096,), dtype=torch.uint8, device="cuda") for _ in range(5)]  # +4 KiB: window overrun
     sink = torch.zeros(4, dtype=torch.int32, device="cuda")
     st = torch.cuda.current_stream()
     h = ctypes.c_void_p(st.cuda_stream)
