@@ -880,7 +880,8 @@ struct enet_hip_context {
     size_t d_meta_cap = 0;
     // fragment reassembly claim words (all ~0 between calls)
     uint32_t* d_claim = nullptr;
-    size_t d_claim_cap = 0;     // words
+    size_t d_claim_cap = 0;     // words (claim words + per-slot winner counts + deferred flag)
+    size_t d_claim_words = 0;   // claim words of the current layout (slots x bitmap bits)
     uint8_t* d_frag_desc = nullptr;   // copy descriptors, 28 B per command
     size_t d_frag_desc_cap = 0;
     uint8_t* d_rc_scratch = nullptr;  // range coder models, kRangeModelBytes per thread
@@ -1279,11 +1280,11 @@ int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgro
 }
 
 int enet_hip_diag_ablation(enet_hip_context* ctx, int mode) {
-    if (!ctx || mode < 0 || mode > 1023) return -static_cast<int>(hipErrorInvalidValue);
-    vring_set_wpe((mode & 512) ? 8 : 4);                      // tuning: two vring workgroups per CU
+    if (!ctx || mode < 0 || mode > 2047) return -static_cast<int>(hipErrorInvalidValue);
+    const int prio = (mode & 1024) ? 2 : (mode >> 3) & 1;    // 8: static / 1024: progress priority
     mode &= 511;
     ctx->ablation = mode & ~8;
-    ctx->ablation_prio = (mode >> 3) & 1;
+    ctx->ablation_prio = prio;
     return 0;
 }
 
@@ -1428,19 +1429,29 @@ int enet_hip_fragment_reassemble_device(enet_hip_context* ctx, const uint8_t* by
         !msgLengths || !msgFragCounts || !fragments || !remaining || wordsPerMsg == 0)))
         return -static_cast<int>(hipErrorInvalidValue);
     if (slotCount > (static_cast<size_t>(1) << 31) || wordsPerMsg > (1u << 15)) return -static_cast<int>(hipErrorInvalidValue);
+    // claim words hold command indices as uint32 with 0xFFFFFFFF = unclaimed
+    if (count >= 0xFFFFFFFFull) return -static_cast<int>(hipErrorInvalidValue);
     std::lock_guard<std::mutex> lk(ctx->mu);
     ENH_CHECK(hipSetDevice(ctx->device));
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-    const size_t need = std::max<size_t>(1, slotCount * wordsPerMsg * 32u);
-    if (need > ctx->d_claim_cap) {
-        // a fresh claim area, ~0 everywhere; the release kernel restores that after each call
+    // scratch: claim words (~0 between calls, restored by frag_copy_kernel), then the
+    // per-slot winner counts and the deferred flag (0 between calls, restored by
+    // frag_copy_kernel / frag_serial_kernel)
+    const size_t claims = std::max<size_t>(1, slotCount * wordsPerMsg * 32u);
+    const size_t need = claims + slotCount + 1;
+    if (need > ctx->d_claim_cap || claims != ctx->d_claim_words) {
         ENH_CHECK(hipStreamSynchronize(st));
-        (void)hipFree(ctx->d_claim);
-        ctx->d_claim = nullptr;
-        ctx->d_claim_cap = 0;
-        ENH_CHECK(hipMalloc(reinterpret_cast<void**>(&ctx->d_claim), need * 4));
+        if (need > ctx->d_claim_cap) {
+            (void)hipFree(ctx->d_claim);
+            ctx->d_claim = nullptr;
+            ctx->d_claim_cap = 0;
+            ENH_CHECK(hipMalloc(reinterpret_cast<void**>(&ctx->d_claim), need * 4));
+        }
+        ctx->d_claim_cap = 0;                  // valid only once both fills are queued
+        ENH_CHECK(hipMemsetAsync(ctx->d_claim, 0xFF, claims * 4, st));
+        ENH_CHECK(hipMemsetAsync(ctx->d_claim + claims, 0, (need - claims) * 4, st));
         ctx->d_claim_cap = need;
-        ENH_CHECK(hipMemsetAsync(ctx->d_claim, 0xFF, need * 4, st));
+        ctx->d_claim_words = claims;
     }
     int rc;
     if ((rc = ensure(&ctx->d_frag_desc, &ctx->d_frag_desc_cap, count * 28 + 64))) return rc;
@@ -1450,8 +1461,11 @@ int enet_hip_fragment_reassemble_device(enet_hip_context* ctx, const uint8_t* by
     uint32_t* d_len = reinterpret_cast<uint32_t*>(d_cl + count);
     FragArgs a{bytes, cmdOffsets, cmdAvail, slots, count, maximumPacketSize, msgBytes, msgOffsets, msgLengths,
                msgFragCounts, fragments, wordsPerMsg, remaining, slotCount, status, ctx->d_claim,
-               d_src, d_dst, d_len, d_cl};
-    return fragment_reassemble_launch(a, ctx->num_cus, st);
+               ctx->d_claim + claims, ctx->d_claim + claims + slotCount, d_src, d_dst, d_len, d_cl};
+    rc = fragment_reassemble_launch(a, ctx->num_cus, st);
+    // a failed launch may leave claim words set: the next call starts from fresh fills
+    if (rc) ctx->d_claim_cap = 0;
+    return rc;
 }
 
 static int range_coder_call(enet_hip_context* ctx, bool decompress, const uint8_t* in, const uint64_t* inOffsets,

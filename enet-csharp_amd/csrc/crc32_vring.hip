@@ -49,15 +49,14 @@ __device__ __forceinline__ u32x4 vr_ld16(uint64_t addr) {
     asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(addr));
     return v;
 }
-__device__ __forceinline__ uint32_t vr_ld4(uint64_t addr) {
-    uint32_t v;
-    asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(addr));
-    return v;
+// The metadata loads overwrite the previous load's register whether or not that
+// value was used ("+v": the old value is an input, so its register is never
+// handed to anything else while a load into it may be in flight).
+__device__ __forceinline__ void vr_ld4(uint32_t& v, uint64_t addr) {
+    asm volatile("global_load_dword %0, %1, off" : "+v"(v) : "v"(addr));
 }
-__device__ __forceinline__ uint64_t vr_ld8(uint64_t addr) {
-    uint64_t v;
-    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(addr));
-    return v;
+__device__ __forceinline__ void vr_ld8(uint64_t& v, uint64_t addr) {
+    asm volatile("global_load_dwordx2 %0, %1, off" : "+v"(v) : "v"(addr));
 }
 template <int N>
 __device__ __forceinline__ void vr_wait(u32x4& a, u32x4& b) {
@@ -66,6 +65,13 @@ __device__ __forceinline__ void vr_wait(u32x4& a, u32x4& b) {
 template <int N>
 __device__ __forceinline__ void vr_wait_meta(uint32_t& L, uint64_t& off) {
     asm volatile("s_waitcnt vmcnt(%2)" : "+v"(L), "+v"(off) : "n"(N));
+}
+// vmcnt(0) tying every register a load may still land in
+template <int NB>
+__device__ __forceinline__ void vr_drain(u32x4 (&a)[NB], u32x4 (&b)[NB], uint32_t& L, uint64_t& off) {
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(L), "+v"(off) :: "memory");
+#pragma unroll
+    for (int i = 0; i < NB; ++i) asm volatile("" : "+v"(a[i]), "+v"(b[i]));
 }
 
 // Zero the bytes of a block that lie outside the packet, [lo, hi) kept (block
@@ -131,15 +137,21 @@ __device__ __forceinline__ constexpr uint32_t vr_col_const() {
 // fold_block_lane (crc32_device.hpp) with at most 8 table lookups in flight:
 // groups of 4 lookups, group g+1 issued before group g is XOR-reduced, so the
 // kernel fits 64 VGPRs (32 waves per CU hide the LDS latency instead of ILP).
-__device__ __forceinline__ uint32_t vr_fold(uint32_t reg, u32x4 A, u32x4 B, const VrSched& s) {
+__device__ __forceinline__ uint32_t vr_fold(uint32_t reg, u32x4 A, u32x4 B, const VrSched& s, uint32_t lane) {
     const uint32_t a0 = __builtin_amdgcn_bitop3_b32(A.x, reg, s.hs, 0xB4);   // A ^ (reg & ~hs)
     const uint32_t b0 = __builtin_amdgcn_bitop3_b32(B.x, reg, s.hs, 0x78);   // B ^ (reg & hs)
     const uint32_t w[8] = {a0, A.y, A.z, A.w, b0, B.y, B.z, B.w};
+    // the dword-swap masks (make_sched's m1, m2) rebuilt per block from the lane
+    // id: two VALU ops instead of two VGPRs held across the loop (asm volatile, so
+    // the compiler cannot hoist them back out)
+    uint32_t m1, m2;
+    asm volatile("v_bfe_i32 %0, %1, 2, 1" : "=v"(m1) : "v"(lane));
+    asm volatile("v_bfe_i32 %0, %1, 3, 1" : "=v"(m2) : "v"(lane));
     uint32_t x[8], d[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) x[q] = __builtin_amdgcn_bitop3_b32(w[q], w[q ^ 1], s.m1, 0xD8);
+    for (int q = 0; q < 8; ++q) x[q] = __builtin_amdgcn_bitop3_b32(w[q], w[q ^ 1], m1, 0xD8);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) d[q] = __builtin_amdgcn_bitop3_b32(x[q], x[q ^ 2], s.m2, 0xD8);
+    for (int q = 0; q < 8; ++q) d[q] = __builtin_amdgcn_bitop3_b32(x[q], x[q ^ 2], m2, 0xD8);
     uint32_t v[2][4];
     uint32_t acc = 0;
     auto issue = [&](auto gc) __attribute__((always_inline)) {
@@ -163,12 +175,14 @@ __device__ __forceinline__ uint32_t vr_fold(uint32_t reg, u32x4 A, u32x4 B, cons
     return acc;
 }
 
+// NB = ring slots (NB - 1 stages in flight while one is folded).
 // WPE = waves per SIMD the register allocation must allow: 8 = two 16-wave
 // workgroups per CU (64 VGPRs), 4 = one (no cap below 128).
 // TR = 1: the diagnostics instance that writes the per-wave trace (pa.trace).
-template <int LG, int WPE, int TR = 0>
+template <int LG, int NB, int WPE, int TR = 0>
 __global__ void __launch_bounds__(64 * kVrW) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 crc32_vring_kernel(PacketArgs pa, KernelTables tb, const uint32_t* basis) {
+    static_assert(NB >= 2 && NB <= 4, "ring slots");
     constexpr uint32_t P = 1u << LG, kPk = 64u >> LG;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -202,6 +216,15 @@ crc32_vring_kernel(PacketArgs pa, KernelTables tb, const uint32_t* basis) {
         }
     };
     mark(0);
+    // tuning (pa.prio): the SIMD arbiter favours older waves, so wave slots 12-15 of a
+    // workgroup finish ~40 % after slots 0-3 (profiles/r02_timeline_*): issue priority
+    // by slot quartile, youngest highest
+    if (pa.prio == 1u) {
+        const uint32_t q = wave >> 2;                        // wave-uniform
+        if (q == 1u) __builtin_amdgcn_s_setprio(1);
+        else if (q == 2u) __builtin_amdgcn_s_setprio(2);
+        else if (q == 3u) __builtin_amdgcn_s_setprio(3);
+    }
 
     // ---- prologue: basis row `wave` (waves < 10) and metadata of group 0
     if (wave < static_cast<uint32_t>(kVrBasisRows))
@@ -211,8 +234,8 @@ crc32_vring_kernel(PacketArgs pa, KernelTables tb, const uint32_t* basis) {
     uint64_t moff = 0;
     auto load_meta = [&](uint32_t j) __attribute__((always_inline)) {
         const uint64_t q = min(packet_of(j), pa.n - 1u);
-        mL = vr_ld4(reinterpret_cast<uint64_t>(pa.len + q));
-        moff = vr_ld8(reinterpret_cast<uint64_t>(pa.off + q));
+        vr_ld4(mL, reinterpret_cast<uint64_t>(pa.len + q));
+        vr_ld8(moff, reinterpret_cast<uint64_t>(pa.off + q));
     };
     load_meta(0);                                            // (clamped index: valid for J == 0 too)
     vr_wait_meta<0>(mL, moff);                               // basis row and metadata have landed
@@ -223,6 +246,10 @@ crc32_vring_kernel(PacketArgs pa, KernelTables tb, const uint32_t* basis) {
     uint32_t plz = 0, pe = 0;                                // packet bytes [plz, pe) of the window
     uint32_t pj = 0, pst = 0, pstages = 0;
     bool pdone = J == 0;
+    // hand-over of the windows to the consumer, which runs NB - 1 stages behind:
+    // with NB == 2 it enters a group right after the producer did and reads plz /
+    // pe; deeper rings keep a FIFO of the windows the producer entered ahead
+    uint32_t f0lz = 0, f0e = 0, f1lz = 0, f1e = 0, f2lz = 0, f2e = 0, fn = 0;
     auto producer_enter = [&](uint32_t j) __attribute__((always_inline)) {
         const uint32_t L = packet_of(j) < pa.n ? mL : 0u;
         const uint64_t a = base + moff;
@@ -232,13 +259,18 @@ crc32_vring_kernel(PacketArgs pa, KernelTables tb, const uint32_t* basis) {
         const uint32_t nb = L ? (pe + 31u) >> 5 : 0u;
         pstages = max(1u, wave_max_u((nb + P - 1u) >> LG));
         pst = 0;
+        if constexpr (NB > 2) {
+            if (fn == 0u) { f0lz = plz; f0e = pe; }
+            else if (fn == 1u) { f1lz = plz; f1e = pe; }
+            else { f2lz = plz; f2e = pe; }
+            ++fn;
+        }
     };
     const VrSched s = make_vr_sched(lane);
-    const uint32_t hs16 = s.hs & 16u;                        // this lane takes the block's halves swapped
     // Every produce issues the same four loads -- the metadata of the group after
     // the producer's (an L2 hit but at group switches) and the stage's two
     // pieces -- so every wait below has a fixed count.
-    u32x4 ra[2], rb[2];
+    u32x4 ra[NB], rb[NB];
     auto produce = [&](auto slot_c) __attribute__((always_inline)) {
         constexpr uint32_t slot = decltype(slot_c)::value;
         if (!pdone && pst == pstages) {
@@ -254,6 +286,7 @@ crc32_vring_kernel(PacketArgs pa, KernelTables tb, const uint32_t* basis) {
         }
         load_meta(min(pj + 1u, J - 1u));
         const uint32_t q0 = 32u * (k + P * pst);
+        const uint32_t hs16 = s.hs & 16u;                    // this lane takes the block's halves swapped
         const uint32_t a0 = q0 + hs16, a1 = q0 + 16u - hs16;
         const uint64_t s0 = (a0 < pe && a0 + 16u > plz) ? pws + a0 : zero;
         const uint64_t s1 = (a1 < pe && a1 + 16u > plz) ? pws + a1 : zero;
@@ -263,7 +296,7 @@ crc32_vring_kernel(PacketArgs pa, KernelTables tb, const uint32_t* basis) {
     };
     if (J) {
         producer_enter(0);
-        produce(std::integral_constant<uint32_t, 0>{});
+        unroll_slots<NB - 1>([&](auto sc) __attribute__((always_inline)) { produce(sc); });
     }
 
     // ---- the table image, rebuilt in LDS while stage 0 is in flight.  Wave w
@@ -313,11 +346,17 @@ crc32_vring_kernel(PacketArgs pa, KernelTables tb, const uint32_t* basis) {
         t = t >= from ? t : ~0u;
         return wave_min_u(min(h, t));
     };
-    // Entered right after the producer has entered the same group (the producer
-    // runs exactly one stage ahead), so plz / pe are that group's window.
     auto consumer_enter = [&]() __attribute__((always_inline)) {
-        clz = plz;
-        ce = pe;
+        if constexpr (NB == 2) {
+            clz = plz;
+            ce = pe;
+        } else {
+            clz = f0lz;
+            ce = f0e;
+            f0lz = f1lz; f0e = f1e;
+            f1lz = f2lz; f1e = f2e;
+            --fn;
+        }
         const uint32_t nb = ce != clz ? (ce + 31u) >> 5 : 0u;
         ccnt = nb > k ? ((nb - 1u - k) >> LG) + 1u : 0u;
         cstages = max(1u, wave_max_u((nb + P - 1u) >> LG));
@@ -330,16 +369,26 @@ crc32_vring_kernel(PacketArgs pa, KernelTables tb, const uint32_t* basis) {
     bool done = false;
     auto iteration = [&](auto sc) __attribute__((always_inline)) {
         constexpr uint32_t S = decltype(sc)::value;
-        if (done) return;
-        produce(std::integral_constant<uint32_t, S ^ 1u>{});
-        vr_wait<4>(ra[S], rb[S]);                            // stage S has landed (4 younger loads)
+        if (pa.prio == 2u) {
+            // equal progress: the SIMD arbiter serves high priority first, then older
+            // waves; a wave with more of its work left than its neighbours goes first,
+            // so no wave is left streaming alone at the end
+            const uint32_t left = (J - cj) * 8u - min(8u, (cs * 8u) / cstages);   // eighths of groups left
+            const uint32_t q = (left * 4u) / (J * 8u + 1u);                        // 0..3
+            if (q >= 3u) __builtin_amdgcn_s_setprio(3);
+            else if (q == 2u) __builtin_amdgcn_s_setprio(2);
+            else if (q == 1u) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+        produce(std::integral_constant<uint32_t, (S + NB - 1) % NB>{});
+        vr_wait<4 * (NB - 1)>(ra[S], rb[S]);                 // stage S has landed (4 younger loads per stage)
         u32x4 A = ra[S], B = rb[S];
         if (cs == nedge) {                                   // head / tail pieces: keep [clz, ce) only
             const uint32_t q0 = 32u * (k + P * cs);               // windows < 2 GiB: differences fit int32
             vr_edge_mask(A, B, s.hs, static_cast<int32_t>(clz - q0), static_cast<int32_t>(ce - q0));
             nedge = next_edge(cs + 1u);
         }
-        const uint32_t nr = vr_fold(reg, A, B, s);
+        const uint32_t nr = vr_fold(reg, A, B, s, lane);
         reg = cs < ccnt ? nr : reg;
         if (cj == 0u && cs == 0u) mark(4);
         if (++cs == cstages) {
@@ -365,36 +414,62 @@ crc32_vring_kernel(PacketArgs pa, KernelTables tb, const uint32_t* basis) {
             const uint64_t pk = packet_of(cj);
             if (k == 0u && pk < pa.n) pa.out[pk] = finalize(reg);   // packet.cs:159
             if (++cj == J) {
+                // the producer's last loads (zero lines past the end) are dead: drain
+                // them, so no register they land in can be reused while in flight
+                vr_drain(ra, rb, mL, moff);
                 done = true;
                 return;
             }
             consumer_enter();
         }
     };
-    while (!done) unroll_slots<2>(iteration);
+    // each slot's iteration leaves the loop at once when the wave is done, so the
+    // loop head is reached only from a completed ring turn (no path with the drained
+    // loads of the last turn in flight: tools/isa_inflight_check.py)
+    for (;;) {
+        iteration(std::integral_constant<uint32_t, 0>{});
+        if (done) break;
+        iteration(std::integral_constant<uint32_t, 1>{});
+        if (done) break;
+        if constexpr (NB > 2) {
+            iteration(std::integral_constant<uint32_t, 2>{});
+            if (done) break;
+        }
+        if constexpr (NB > 3) {
+            iteration(std::integral_constant<uint32_t, 3>{});
+            if (done) break;
+        }
+    }
     trace_end();
 }
 
 // ---------------------------------------------------------------- host side
 
-template <int LG, int WPE, int TR = 0>
+template <int LG, int NB, int WPE, int TR = 0>
 const void* vring_fn() {
-    return reinterpret_cast<const void*>(crc32_vring_kernel<LG, WPE, TR>);
+    return reinterpret_cast<const void*>(crc32_vring_kernel<LG, NB, WPE, TR>);
 }
 
-int g_vring_wpe = 4;                                           // tuning: enet_hip_diag_ablation bit 9
+// The product instance: 2 ring slots, one workgroup per CU per launch, 64 VGPRs
+// (WPE 8) so that the next launch's workgroup -- overlapping batches on other
+// streams -- can share the CU while this one drains (bench: 4831 GiB/s at 59-62
+// VGPRs against 4438 at 66, profiles/r02_*).  With a trace buffer: the same kernel
+// writing per-wave timestamps.  Measured and not kept: 3 and 4 ring slots, and two
+// workgroups of one launch per CU.
+const void* vring_pick(int lg, bool trace) {
+    if (trace) return lg == 2 ? vring_fn<2, 2, 4, 1>() : vring_fn<3, 2, 4, 1>();
+    return lg == 2 ? vring_fn<2, 2, 8>() : vring_fn<3, 2, 8>();
+}
 
 int vring_setup() {
-    const void* fns[6] = {vring_fn<2, 4>(), vring_fn<3, 4>(), vring_fn<2, 8>(), vring_fn<3, 8>(),
-                          vring_fn<2, 4, 1>(), vring_fn<3, 4, 1>()};
-    for (const void* f : fns) {
-        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kVrLds);
-        if (e != hipSuccess) return -static_cast<int>(e);
-    }
+    for (int lg = 2; lg <= 3; ++lg)
+        for (int t = 0; t < 2; ++t) {
+            const hipError_t e = hipFuncSetAttribute(vring_pick(lg, t == 1),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, kVrLds);
+            if (e != hipSuccess) return -static_cast<int>(e);
+        }
     return 0;
 }
-
-void vring_set_wpe(int wpe) { g_vring_wpe = wpe == 8 ? 8 : 4; }
 
 int vring_launch(int lg, int num_cus, hipStream_t st, const PacketArgs& pa, const KernelTables& tb,
                  const uint32_t* basis2) {
@@ -402,15 +477,11 @@ int vring_launch(int lg, int num_cus, hipStream_t st, const PacketArgs& pa, cons
     if (pa.n == 0) return 0;
     const uint64_t kpk = 64u >> lg;
     const uint64_t groups = (pa.n + kpk - 1u) / kpk;
-    const int wpe = g_vring_wpe;
-    const uint64_t per_cu = wpe == 8 ? 2u : 1u;                 // resident 16-wave workgroups per CU
     const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(
-        1, std::min<uint64_t>((groups + kVrW - 1) / kVrW, per_cu * static_cast<uint64_t>(num_cus))));
-    const void* fn = pa.trace ? (lg == 2 ? vring_fn<2, 4, 1>() : vring_fn<3, 4, 1>())
-                   : lg == 2 ? (wpe == 8 ? vring_fn<2, 8>() : vring_fn<2, 4>())
-                             : (wpe == 8 ? vring_fn<3, 8>() : vring_fn<3, 4>());
+        1, std::min<uint64_t>((groups + kVrW - 1) / kVrW, static_cast<uint64_t>(num_cus))));
     void* args[] = {const_cast<PacketArgs*>(&pa), const_cast<KernelTables*>(&tb), const_cast<const uint32_t**>(&basis2)};
-    const hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(64 * kVrW), args, kVrLds, st);
+    const hipError_t e = hipLaunchKernel(vring_pick(lg, pa.trace != nullptr), dim3(grid), dim3(64 * kVrW), args,
+                                         kVrLds, st);
     return e == hipSuccess ? 0 : -static_cast<int>(e);
 }
 

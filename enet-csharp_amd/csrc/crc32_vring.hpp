@@ -16,11 +16,9 @@ constexpr int kVrBasisDwords = kVrBasisRows * 64;
 // Set the dynamic-LDS attribute of every vring kernel instance (once per context).
 int vring_setup();
 
-// Tuning: 8 = the 64-VGPR instance, two workgroups per CU; 4 (default) = one.
-void vring_set_wpe(int wpe);
 
 // Launch the vring kernel: checksum mode, lanes per packet 2^lg (lg = 2 or 3),
-// two 16-wave workgroups per CU.  basis2 = kVrBasisDwords per image (images for
+// one 16-wave workgroup per CU.  basis2 = kVrBasisDwords per image (images for
 // P = 1, 4, 8, 16 in that order).  Returns 0 or -hipError_t.
 int vring_launch(int lg, int num_cus, hipStream_t st, const PacketArgs& pa, const KernelTables& tb,
                  const uint32_t* basis2);

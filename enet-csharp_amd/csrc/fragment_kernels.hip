@@ -17,14 +17,25 @@
 //     packet->data + fragmentOffset, length clamped as at 625-626.
 // Memory: HBM-bound byte copy, 1 byte read + 1 byte written per fragment byte.
 //
-// Three launches on one stream:
-//   1. frag_claim_kernel  (thread per command): parse, validate, atomicMin of the
-//      command index into the claim word of its (slot, fragmentNumber);
-//   2. frag_decide_kernel (thread per command): the claim winner tests-and-sets
-//      the bitmap bit (a bit set by an earlier batch = duplicate), decrements
-//      remaining and writes a copy descriptor;
-//   3. frag_copy_kernel   (wave per two commands): the copies with 16-byte lanes, and the
-//      claim words back to ~0.
+// Launches on one stream:
+//   1. frag_claim_kernel (thread per command): parse, validate, atomicMin of the
+//      command index into the claim word of its (slot, fragmentNumber), and leave
+//      the parsed command in the copy-descriptor slots;
+//   2. the decide step, one of two kernels (fragment_reassemble_launch picks
+//      frag_decide_slots_kernel when the claim space, slots x bitmap bits, is at
+//      most 8 n + 65536 words, else frag_decide_kernel): the claim winner (first
+//      command of the batch for its fragment) tests-and-sets the bitmap bit (a bit
+//      set by an earlier batch = duplicate), decrements remaining and gets a copy
+//      descriptor.  Winners whose byte ranges may overlap another winner of the
+//      same slot are DEFERRED (status 2): the slot kernel checks, per slot, that
+//      the winners' ranges are disjoint and ascending in fragment-number order;
+//      the atomic kernel defers every slot with two or more winners;
+//   3. frag_copy_kernel (4 commands per wave as one flat space of 16-byte chunks):
+//      the copies of the non-deferred winners, and the claim words back to ~0;
+//   4. frag_serial_kernel (one wave; returns at once unless something was
+//      deferred): the deferred winners in batch order, each command's stores
+//      drained before the next, so where a batch's fragments overlap the later
+//      command's bytes win as in the sequential reference (protocol.cs:628).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -111,6 +122,7 @@ __global__ void __launch_bounds__(256) frag_decide_kernel(FragArgs a) {
                 atomicOr(a.fragments + static_cast<uint64_t>(slot) * a.words + (number >> 5), bit);   // 619, 623
             if (!(old & bit)) {
                 atomicSub(a.remaining + slot, 1u);                       // --fragmentsRemaining (621)
+                atomicAdd(a.wcount + slot, 1u);                          // 2+ winners: the slot is deferred
                 a.status[i] = 1;
                 len = min(static_cast<uint32_t>(a.copy_src[i]), a.msg_len[slot] - offset);   // clamp (625-626)
                 src = a.cmd_off[i] + kCmdBytes;
@@ -136,6 +148,8 @@ __global__ void __launch_bounds__(256) frag_decide_slots_kernel(FragArgs a) {
          sl += waves) {
         uint32_t* bm = a.fragments + sl * a.words;
         uint32_t removed = 0;
+        uint32_t mx = 0;                                   // largest end of the slot's winners so far
+        bool clash = false;                                // a winner starts before an earlier one ends
         for (uint32_t f0 = 0; f0 < bits; f0 += 64u) {
             const uint32_t f = f0 + lane;
             const uint32_t w = f < bits ? a.claim[sl * bits + f] : ~0u;
@@ -145,16 +159,40 @@ __global__ void __launch_bounds__(256) frag_decide_slots_kernel(FragArgs a) {
             if (lane == 0u && static_cast<uint32_t>(m)) bm[f0 >> 5] |= static_cast<uint32_t>(m);        // 623
             if (lane == 32u && (m >> 32) && (f0 >> 5) + 1u < a.words) bm[(f0 >> 5) + 1u] |= static_cast<uint32_t>(m >> 32);
             removed += static_cast<uint32_t>(__builtin_popcountll(m));
+            uint32_t offset = 0, end = 0;
             if (take) {
                 const uint64_t packed = a.copy_dst[w];
-                const uint32_t offset = static_cast<uint32_t>(packed);
+                offset = static_cast<uint32_t>(packed);
+                const uint32_t len = min(static_cast<uint32_t>(a.copy_src[w]), a.msg_len[sl] - offset);   // 625-626
+                end = offset + len;
                 a.status[w] = 1;
-                a.copy_len[w] = min(static_cast<uint32_t>(a.copy_src[w]), a.msg_len[sl] - offset);   // 625-626
+                a.copy_len[w] = len;
                 a.copy_src[w] = a.cmd_off[w] + kCmdBytes;
                 a.copy_dst[w] = a.msg_off[sl] + offset;
             }
+            if (m) {
+                // exclusive prefix max of the winners' ends in fragment-number (lane) order
+                uint32_t pm = end;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t o = static_cast<uint32_t>(__shfl_up(static_cast<int>(pm), d));
+                    if (lane >= static_cast<uint32_t>(d)) pm = max(pm, o);
+                }
+                uint32_t before = static_cast<uint32_t>(__shfl_up(static_cast<int>(pm), 1));
+                before = lane ? max(before, mx) : mx;
+                if (__ballot(take && offset < before)) clash = true;
+                mx = max(mx, static_cast<uint32_t>(__shfl(static_cast<int>(pm), 63)));
+            }
         }
         if (lane == 0u && removed) a.remaining[sl] -= removed;                     // 621
+        if (clash) {                                       // defer the slot's winners to the serial pass
+            for (uint32_t f0 = 0; f0 < bits; f0 += 64u) {
+                const uint32_t f = f0 + lane;
+                const uint32_t w = f < bits ? a.claim[sl * bits + f] : ~0u;
+                if (w != ~0u && a.status[w] == 1) a.status[w] = 2;
+            }
+            if (lane == 0u) *a.deferred = 1u;
+        }
     }
 }
 
@@ -187,13 +225,26 @@ __global__ void __launch_bounds__(256) frag_copy_kernel(FragArgs a) {
             const uint64_t i = base + c;
             const bool h = i < a.n;
             L[c] = h ? a.copy_len[i] : 0u;
+            const uint64_t ci = h ? a.copy_claim[i] : ~0ull;
+            bool defer = false;
+            if (L[c]) {
+                const int8_t st = a.status[i];
+                const uint64_t slot = ci / (static_cast<uint64_t>(a.words) << 5);
+                const uint32_t wc = a.wcount[slot];      // winners of the slot (atomic decide path)
+                defer = st == 2 || wc >= 2u;
+                if (lane == c) {
+                    if (wc == 1u) a.wcount[slot] = 0u;     // its only winner: reset for the next batch
+                    if (defer && st != 2) {
+                        a.status[i] = 2;
+                        *a.deferred = 1u;
+                    }
+                }
+            }
+            if (defer) L[c] = 0u;                          // copied by frag_serial_kernel, in batch order
             src[c] = h ? a.copy_src[i] : 0u;
             dst[c] = h ? a.copy_dst[i] : 0u;
             pre[c + 1] = pre[c] + ((L[c] + 15u) >> 4);
-            if (h && lane == c) {
-                const uint64_t ci = a.copy_claim[i];
-                if (ci != ~0ull) a.claim[ci] = ~0u;                // claim words back to ~0 for the next batch
-            }
+            if (h && lane == c && ci != ~0ull) a.claim[ci] = ~0u;   // claim words back to ~0 for the next batch
         }
         for (uint32_t k = lane; k < pre[kCopyCmds]; k += 64u) {
             uint32_t c = 0;
@@ -215,6 +266,35 @@ __global__ void __launch_bounds__(256) frag_copy_kernel(FragArgs a) {
     }
 }
 
+// One wave: the deferred winners (status 2) in batch order.  A command's stores
+// are drained (vmcnt counts stores on gfx950) before the next command's begin, so
+// overlapping bytes end up with the later command's data (protocol.cs:628 copies
+// in arrival order).  Resets the deferred flag and the slots' winner counts.
+__global__ void __launch_bounds__(64) frag_serial_kernel(FragArgs a) {
+    if (*a.deferred == 0u) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint64_t i0 = 0; i0 < a.n; i0 += 64u) {
+        const uint64_t i = i0 + lane;
+        const bool mine = i < a.n && a.status[i] == 2;
+        uint64_t m = __ballot(mine);
+        while (m) {
+            const uint32_t c = static_cast<uint32_t>(__builtin_ctzll(m));
+            m &= m - 1u;
+            const uint64_t j = i0 + c;
+            const uint32_t L = a.copy_len[j];
+            const uint64_t src = a.copy_src[j], dst = a.copy_dst[j];
+            for (uint32_t x = lane << 4; x < L; x += 64u << 4) copy_span(a.bytes + src, a.msg_bytes + dst, L, x);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this command's stores done before the next's
+            if (lane == 0u) {
+                a.status[j] = 1;
+                const uint64_t ci = a.copy_claim[j];
+                a.wcount[ci / (static_cast<uint64_t>(a.words) << 5)] = 0u;
+            }
+        }
+    }
+    if (lane == 0u) *a.deferred = 0u;
+}
+
 }  // namespace
 
 int fragment_reassemble_launch(const FragArgs& a, int num_cus, hipStream_t st) {
@@ -232,6 +312,7 @@ int fragment_reassemble_launch(const FragArgs& a, int num_cus, hipStream_t st) {
         hipLaunchKernelGGL(frag_decide_kernel, dim3(g_thr), dim3(256), 0, st, a);
     }
     hipLaunchKernelGGL(frag_copy_kernel, dim3(g_wave), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(frag_serial_kernel, dim3(1), dim3(64), 0, st, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : -static_cast<int>(e);
 }

@@ -22,7 +22,10 @@ struct FragArgs {
     uint32_t* remaining;         //   fragmentsRemaining
     uint64_t slot_count;
     int8_t* status;              // per command: -1 rejected, 0 skipped / duplicate, 1 copied
+                                 // (2 = deferred to the serial pass, internal only)
     uint32_t* claim;             // scratch, slot_count * words * 32 words, all ~0 between calls
+    uint32_t* wcount;            // scratch, slot_count words: winners per slot (atomic decide), 0 between calls
+    uint32_t* deferred;          // scratch word: some winner was deferred, 0 between calls
     uint64_t* copy_src;          // scratch, n each: copy descriptors (decide -> copy kernel)
     uint64_t* copy_dst;
     uint32_t* copy_len;

@@ -212,3 +212,41 @@ def fragments(message_lens, mtu: int = 1392, seed: int = SEED_PAYLOAD, shuffle: 
 def cfg5_fragments(messages: int = 4096, message_bytes: int = 65536) -> FragmentBatch:
     """cfg5's 4096 x 64 KiB messages as received fragment DGRAMs (200 704 commands)."""
     return fragments([message_bytes] * messages, shuffle=True, name=f"cfg5 receive: {messages} x {message_bytes} B")
+
+
+def overlapping_fragments(messages: int, seed: int = SEED_PAYLOAD, max_count: int = 12,
+                          name: str = "overlapping fragments") -> FragmentBatch:
+    """SEND_FRAGMENT commands a non-standard peer could send: per message, fragment
+    numbers 0..count-1 (plus a few repeats) with arbitrary offsets and lengths, so
+    byte ranges overlap in any order and every command carries different bytes.  The
+    reference copies in arrival order (c/protocol.cs:619-630): where ranges overlap,
+    the later command's bytes win."""
+    rng = np.random.default_rng(seed)
+    cmds = []                      # (slot, count, number, total, offset, length)
+    lens, counts = [], []
+    for m in range(messages):
+        L = int(rng.integers(64, 6000))
+        cnt = int(rng.integers(2, max_count + 1))
+        lens.append(L)
+        counts.append(cnt)
+        numbers = list(range(cnt)) + [int(x) for x in rng.integers(0, cnt, int(rng.integers(0, 3)))]
+        for k in numbers:
+            off = int(rng.integers(0, L))
+            ln = int(rng.integers(1, min(1360, L - off) + 1))
+            cmds.append((m, cnt, k, L, off, ln))
+    order = rng.permutation(len(cmds))
+    n = len(cmds)
+    sizes = np.array([32 + cmds[i][5] for i in order], dtype=np.uint64)
+    starts = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+    arena = rng.integers(0, 256, int(sizes.sum()) + 64, dtype=np.uint8)
+    cmd_off = starts + np.uint64(8)
+    cmd_avail = np.zeros(n, dtype=np.uint32)
+    slots = np.zeros(n, dtype=np.int32)
+    for i, ci in enumerate(order):
+        m, cnt, k, L, off, ln = cmds[ci]
+        a = int(starts[i])
+        arena[a + 8:a + 32] = np.frombuffer(send_fragment_cmd(cnt, k, L, off, ln), dtype=np.uint8)
+        cmd_avail[i] = ln
+        slots[i] = m
+    return FragmentBatch(arena, cmd_off, cmd_avail, slots, np.array(lens, dtype=np.uint32),
+                         np.array(counts, dtype=np.uint32), [], 0, name)

@@ -125,3 +125,16 @@ def test_split_sizes_follow_peer_cs():
     fb = workloads.fragments([65536], shuffle=False)
     assert fb.n == 49 and int(fb.msg_count[0]) == 49
     assert int(fb.cmd_avail[0]) == 1360 and int(fb.cmd_avail[-1]) == 256
+
+
+def test_oracle_overlapping_fragments_match_python(oracle_lib):
+    """The C oracle on overlapping fragment ranges equals the pure-Python handler:
+    later commands' bytes win where ranges overlap (protocol.cs:619-630)."""
+    fb = workloads.overlapping_fragments(40, seed=41)
+    so, sp = state(fb), state(fb)
+    st = run_oracle(oracle_lib, fb, so)
+    sp_status = py_reassemble(fb.payload, fb.cmd_off, fb.cmd_avail, fb.slots, fb.msg_len, fb.msg_count,
+                              sp["msg_off"], sp["msg_bytes"], sp["fragments"], sp["words"], sp["remaining"])
+    assert list(st) == list(sp_status)
+    assert (so["msg_bytes"] == sp["msg_bytes"]).all()
+    assert (st == 1).sum() > 0

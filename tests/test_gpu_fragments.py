@@ -102,3 +102,21 @@ def test_fragments_both_decide_paths(ctx, oracle_lib, words):  # noqa: F811
         assert (run_gpu(ctx, fb, sg, np.sort(sel)) == run_oracle(oracle_lib, fb, so, np.sort(sel))).all()
     for k in ("msg_bytes", "fragments", "remaining"):
         assert (so[k] == sg[k]).all(), k
+
+
+@pytest.mark.parametrize("words", [None, 64])
+def test_fragments_overlapping_ranges(ctx, oracle_lib, words):  # noqa: F811
+    """Fragments of one slot whose byte ranges overlap (a non-standard peer): the
+    reference copies in arrival order, so the later command's bytes win.  Overlapping
+    slots are deferred to the serial pass; both decide paths (slot-owned and atomic)
+    must equal the sequential oracle bit for bit, mixed with a standard batch."""
+    ov = workloads.overlapping_fragments(300, seed=31)
+    std = workloads.fragments(np.random.default_rng(32).integers(1, 20000, 60), seed=33, duplicates=0.3)
+    for fb in (ov, std):
+        so, sg = state(fb, words), state(fb, words)
+        cuts = [0, fb.n // 2, fb.n]
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            sel = np.arange(a, b)
+            assert (run_gpu(ctx, fb, sg, sel) == run_oracle(oracle_lib, fb, so, sel)).all()
+        for k in ("msg_bytes", "fragments", "remaining"):
+            assert (so[k] == sg[k]).all(), k

@@ -4,9 +4,10 @@ The kernel issues its global loads as inline asm and waits for them by hand
 (counted vmcnt), so correctness depends on properties of the generated code,
 checked here on the gfx950 ISA hipcc emits with the Makefile's flags:
   * no scratch (private) memory: scratch ops are VMEM and would need vmcnt(0);
-  * no instruction reads or overwrites a loaded register before its wait
-    (tools/isa_inflight_check.py);
-  * at most 64 VGPRs, so two 16-wave workgroups fit a CU.
+  * no instruction reads or overwrites a register while a load into it may be in
+    flight, on any path of the control-flow graph (tools/isa_inflight_check.py);
+  * at most 64 VGPRs: a launch runs one 16-wave workgroup per CU, and the next
+    launch's workgroup (another stream) can share the CU as this one drains.
 """
 import os
 import shutil

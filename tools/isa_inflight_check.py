@@ -2,11 +2,18 @@
 """Static check of crc32_vring.hip's hand-counted loads (test infrastructure).
 
 The vring kernel issues its global loads as inline asm and waits for them with
-explicit `s_waitcnt vmcnt(N)`; the compiler sees the loaded registers as ready
-at once, so nothing may read or copy them before that wait.  This scans the
-kernel's ISA (hipcc -S) in program order: for every asm `global_load*` it
-collects the destination VGPRs and fails if any instruction before the next asm
-`s_waitcnt vmcnt` reads or overwrites one of them.
+explicit `s_waitcnt vmcnt(N)`; the compiler sees a loaded register as written at
+once, so nothing may read or overwrite it before the wait that retires the load
+(a register reused while its load is in flight is clobbered when the load lands).
+
+This is a dataflow analysis over the kernel's control-flow graph (hipcc -S
+output): the state at each point is the ordered list of VMEM operations that may
+still be in flight (the destination VGPRs of asm loads; other VMEM ops --
+compiler loads / stores, LDS-DMA, scratch -- count with no tracked registers).
+`s_waitcnt vmcnt(N)` keeps only the N youngest; at a join the lists are merged
+aligned at their youngest end (element-wise union), which over-approximates what
+may be in flight on any path.  Any instruction that names a register of an
+in-flight asm load (other than the waits that tie them) is reported.
 
     python tools/isa_inflight_check.py path/to/kernel.s
 """
@@ -14,6 +21,7 @@ import re
 import sys
 
 VREG = re.compile(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b")
+MAXQ = 64
 
 
 def regs(text):
@@ -23,41 +31,116 @@ def regs(text):
             out.add(int(m.group(3)))
         else:
             out.update(range(int(m.group(1)), int(m.group(2)) + 1))
-    return out
+    return frozenset(out)
+
+
+def parse(lines):
+    """-> list of instructions (kind, text, regs, target, lineno) and label -> index."""
+    insts, labels = [], {}
+    in_asm = False
+    for no, raw in enumerate(lines):
+        st = raw.strip()
+        if st == ";;#ASMSTART":
+            in_asm = True
+            continue
+        if st == ";;#ASMEND":
+            in_asm = False
+            continue
+        line = st.split(";")[0].strip()
+        if not line:
+            continue
+        if line.endswith(":"):
+            labels[line[:-1]] = len(insts)
+            continue
+        if line.startswith("."):
+            continue
+        op = line.split()[0]
+        kind = "other"
+        if in_asm and op.startswith("global_load") and "lds" not in op:
+            kind = "aload"
+        elif op.startswith(("global_", "buffer_", "scratch_", "flat_")):
+            kind = "vmem"
+        elif op == "s_waitcnt" and "vmcnt" in line:
+            kind = "wait"
+        elif op.startswith("s_cbranch") or op == "s_branch":
+            kind = "branch"
+        elif op == "s_endpgm":
+            kind = "end"
+        target = line.split()[1] if kind == "branch" and len(line.split()) > 1 else None
+        insts.append((kind, line, op, target, no))
+    return insts, labels
+
+
+def merge(a, b):
+    if a is None:
+        return b
+    if b is None:
+        return a
+    n = max(len(a), len(b))
+    pa = [frozenset()] * (n - len(a)) + list(a)
+    pb = [frozenset()] * (n - len(b)) + list(b)
+    return tuple(x | y for x, y in zip(pa, pb))
+
+
+def step(state, inst):
+    kind, line, op, _, _ = inst
+    if kind == "aload":
+        dst = line[len(op):].split(",", 1)[0]
+        return (state + (frozenset((r, inst[4]) for r in regs(dst)),))[-MAXQ:]
+    if kind == "vmem":
+        return (state + (frozenset(),))[-MAXQ:]
+    if kind == "wait":
+        n = int(re.search(r"vmcnt\((\d+)\)", line).group(1))
+        return state[len(state) - n:] if n < len(state) else state
+    return state
 
 
 def check(lines, name):
+    insts, labels = parse(lines)
+    n = len(insts)
+    succ = []
+    for i, (kind, line, op, target, _) in enumerate(insts):
+        s = []
+        if kind == "branch" and target in labels:
+            s.append(labels[target])
+        # s_cbranch_execnz falls through only with EXEC == 0, which no wave of this
+        # kernel reaches outside a divergent region (those are skipped with execz);
+        # hipcc emits it as the exit of uniform loops, with implicit-defs on the dead
+        # fall-through path
+        if kind not in ("end",) and op not in ("s_branch", "s_cbranch_execnz") and i + 1 < n:
+            s.append(i + 1)
+        succ.append(s)
+    state_in = [None] * n
+    state_in[0] = ()
+    work = [0]
+    while work:
+        i = work.pop()
+        out = step(state_in[i], insts[i])
+        for j in succ[i]:
+            m = merge(state_in[j], out)
+            if m != state_in[j]:
+                state_in[j] = m
+                work.append(j)
     errors = []
-    in_asm = False
-    pending = []                          # (line no, dest regs)
-    for no, raw in enumerate(lines):
-        line = raw.split(";")[0].strip() if not raw.strip().startswith(";;#") else raw.strip()
-        if raw.strip() == ";;#ASMSTART":
-            in_asm = True
+    for i, inst in enumerate(insts):
+        kind, line, op, _, no = inst
+        st = state_in[i]
+        if st is None or kind == "wait":
             continue
-        if raw.strip() == ";;#ASMEND":
-            in_asm = False
+        busy_pairs = frozenset().union(*st) if st else frozenset()
+        busy = frozenset(r for r, _ in busy_pairs)
+        if not busy:
             continue
-        if not line or line.endswith(":") or line.startswith("."):
-            continue
-        op = line.split()[0]
-        if in_asm and op.startswith("global_load"):
+        used = regs(line)
+        if kind == "aload":
             dst, rest = line[len(op):].split(",", 1)
-            busy = regs(dst)
-            for pno, preg in pending:     # a load may not reuse a pending destination
-                if preg & (regs(rest) | busy):
-                    errors.append(f"{name}:{no + 1}: load touches registers of the load at {pno + 1}")
-            pending.append((no, busy))
-            continue
-        if in_asm and op == "s_waitcnt" and "vmcnt" in line:
-            pending = []
-            continue
-        if pending:
-            used = regs(line)
-            for pno, preg in pending:
-                if preg & used:
-                    errors.append(f"{name}:{no + 1}: '{line}' touches v{sorted(preg & used)} "
-                                  f"loaded at {pno + 1} before its wait")
+            # a load may overwrite its own earlier in-flight destination (same register,
+            # loads land in order) but may not read one as its address
+            used = regs(rest)
+        hit = busy & used
+        if hit:
+            src = sorted({o + 1 for r, o in busy_pairs if r in hit})
+            errors.append(f"{name}:{no + 1}: '{line}' touches v{sorted(hit)} while the load(s) at {src} may be in flight")
     return errors
 
 
@@ -70,14 +153,16 @@ def kernels(text):
             continue
         if cur is not None:
             body.append(raw)
-            if "s_endpgm" in raw:
+            if "s_endpgm" in raw and not raw.strip().startswith(";"):
                 yield cur, body
                 cur = None
 
 
-def main(path):
+def main(path, skip_trace=True):
     errs, n = [], 0
     for name, body in kernels(open(path).read()):
+        if skip_trace and "ELi1EEEv" in name:      # the diagnostics (trace) instance
+            continue
         n += 1
         errs += check(body, name)
     for e in errs[:40]:

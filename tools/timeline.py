@@ -95,6 +95,12 @@ def analyze(traces):
                           "cu_end_max_p10_p50_p90_p100": [round(float(np.percentile(hi, q)), 2) for q in (10, 50, 90, 100)],
                           "within_cu_spread_p50": round(float(np.median(hi - lo)), 2),
                           "cu_median_end_p10_p90": [round(float(np.percentile(med, q)), 2) for q in (10, 90)]}))
+        # end time by wave slot in the workgroup (row i of the trace is wave i % W)
+        nw = len(r["end"])
+        W = 16
+        slots = np.arange(nw) % W
+        print(json.dumps({"end_p50_by_wave_slot": [round(float(np.median(r["end"][slots == w])), 2) for w in range(W)]}))
+        print(json.dumps({"first_p50_by_wave_slot": [round(float(np.nanmedian(r["first"][slots == w])), 2) for w in range(W)]}))
         st = r["end"] - r["bar"]
         for sm in range(4):
             m = r["simd"] == sm

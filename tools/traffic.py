@@ -23,7 +23,7 @@ def main():
             if row["Counter_Name"] != "FETCH_SIZE":
                 continue
             name = row["Kernel_Name"]
-            key = "probe" if "read_probe" in name else "stream" if ("stream_kernel" in name or "lean_kernel" in name) else name[:60]
+            key = "probe" if "read_probe" in name else "stream" if ("stream_kernel" in name or "lean_kernel" in name or "vring_kernel" in name) else name[:60]
             vals[key].append(float(row["Counter_Value"]))
     res = {k: sum(v) / len(v) for k, v in vals.items()}
     stream = res.get("stream")
