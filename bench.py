@@ -283,7 +283,7 @@ def kernel_name(args) -> str:
         return f"crc32_lean_kernel<0, {lg}, 16, 2, 128>"
     if lg is None:
         return "crc32_stream_kernel / crc32_direct_kernel"
-    return f"crc32_vring_kernel<{lg}, 2, 4, 0>"
+    return f"crc32_vring_kernel<{lg}, 2, 8, 0, 0>"
 
 
 def load_traffic(cfg: str):

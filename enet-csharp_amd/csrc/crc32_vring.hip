@@ -58,18 +58,23 @@ __device__ __forceinline__ void vr_ld4(uint32_t& v, uint64_t addr) {
 __device__ __forceinline__ void vr_ld8(uint64_t& v, uint64_t addr) {
     asm volatile("global_load_dwordx2 %0, %1, off" : "+v"(v) : "v"(addr));
 }
+__device__ __forceinline__ void vr_ld16_tied(u32x4& v, uint64_t addr) {
+    asm volatile("global_load_dwordx4 %0, %1, off" : "+v"(v) : "v"(addr));
+}
 template <int N>
 __device__ __forceinline__ void vr_wait(u32x4& a, u32x4& b) {
     asm volatile("s_waitcnt vmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N));
 }
-template <int N>
-__device__ __forceinline__ void vr_wait_meta(uint32_t& L, uint64_t& off) {
-    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(L), "+v"(off) : "n"(N));
+// (BIN: the record register; else the length and offset registers)
+template <int N, int BIN>
+__device__ __forceinline__ void vr_wait_meta(uint32_t& L, uint64_t& off, u32x4& rec) {
+    if constexpr (BIN) asm volatile("s_waitcnt vmcnt(%1)" : "+v"(rec) : "n"(N));
+    else asm volatile("s_waitcnt vmcnt(%2)" : "+v"(L), "+v"(off) : "n"(N));
 }
 // vmcnt(0) tying every register a load may still land in
-template <int NB>
-__device__ __forceinline__ void vr_drain(u32x4 (&a)[NB], u32x4 (&b)[NB], uint32_t& L, uint64_t& off) {
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(L), "+v"(off) :: "memory");
+template <int BIN, int NB>
+__device__ __forceinline__ void vr_drain(u32x4 (&a)[NB], u32x4 (&b)[NB], uint32_t& L, uint64_t& off, u32x4& rec) {
+    vr_wait_meta<0, BIN>(L, off, rec);
 #pragma unroll
     for (int i = 0; i < NB; ++i) asm volatile("" : "+v"(a[i]), "+v"(b[i]));
 }
@@ -179,7 +184,10 @@ __device__ __forceinline__ uint32_t vr_fold(uint32_t reg, u32x4 A, u32x4 B, cons
 // WPE = waves per SIMD the register allocation must allow: 8 = two 16-wave
 // workgroups per CU (64 VGPRs), 4 = one (no cap below 128).
 // TR = 1: the diagnostics instance that writes the per-wave trace (pa.trace).
-template <int LG, int NB, int WPE, int TR = 0>
+// BIN = 1: metadata from the length-ordered records of the *_binned entry points
+// (PacketArgs::meta4, 16 B {len, off_lo, off_hi, index} per packet, one load
+// instead of two); the CRC goes to out[index].
+template <int LG, int NB, int WPE, int TR = 0, int BIN = 0>
 __global__ void __launch_bounds__(64 * kVrW) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 crc32_vring_kernel(PacketArgs pa, KernelTables tb, const uint32_t* basis) {
     static_assert(NB >= 2 && NB <= 4, "ring slots");
@@ -232,13 +240,19 @@ crc32_vring_kernel(PacketArgs pa, KernelTables tb, const uint32_t* basis) {
              kVrStaging + 256u * wave);
     uint32_t mL = 0;                                         // metadata of the producer's next group
     uint64_t moff = 0;
+    u32x4 mrec = {0u, 0u, 0u, 0u};                           // (BIN: the record)
+    constexpr int kMetaOps = BIN ? 1 : 2;                    // metadata loads per produce
     auto load_meta = [&](uint32_t j) __attribute__((always_inline)) {
         const uint64_t q = min(packet_of(j), pa.n - 1u);
-        vr_ld4(mL, reinterpret_cast<uint64_t>(pa.len + q));
-        vr_ld8(moff, reinterpret_cast<uint64_t>(pa.off + q));
+        if constexpr (BIN) {
+            vr_ld16_tied(mrec, reinterpret_cast<uint64_t>(pa.meta4 + 4u * q));
+        } else {
+            vr_ld4(mL, reinterpret_cast<uint64_t>(pa.len + q));
+            vr_ld8(moff, reinterpret_cast<uint64_t>(pa.off + q));
+        }
     };
     load_meta(0);                                            // (clamped index: valid for J == 0 too)
-    vr_wait_meta<0>(mL, moff);                               // basis row and metadata have landed
+    vr_wait_meta<0, BIN>(mL, moff, mrec);                    // basis row and metadata have landed
     mark(1);
 
     // ---- producer: window of the group it loads, one stage ahead of the consumer
@@ -250,9 +264,11 @@ crc32_vring_kernel(PacketArgs pa, KernelTables tb, const uint32_t* basis) {
     // with NB == 2 it enters a group right after the producer did and reads plz /
     // pe; deeper rings keep a FIFO of the windows the producer entered ahead
     uint32_t f0lz = 0, f0e = 0, f1lz = 0, f1e = 0, f2lz = 0, f2e = 0, fn = 0;
+    uint32_t pidx = 0;                                       // (BIN: caller index of the lane's packet)
     auto producer_enter = [&](uint32_t j) __attribute__((always_inline)) {
-        const uint32_t L = packet_of(j) < pa.n ? mL : 0u;
-        const uint64_t a = base + moff;
+        const uint32_t L = packet_of(j) < pa.n ? (BIN ? mrec.x : mL) : 0u;
+        const uint64_t a = base + (BIN ? (static_cast<uint64_t>(mrec.y) | (static_cast<uint64_t>(mrec.z) << 32)) : moff);
+        if constexpr (BIN) pidx = mrec.w;
         plz = static_cast<uint32_t>(a) & 63u;
         pws = a - plz;
         pe = plz + L;
@@ -277,7 +293,7 @@ crc32_vring_kernel(PacketArgs pa, KernelTables tb, const uint32_t* basis) {
             if (++pj < J) {
                 // last produce's metadata loads are older than its two stage loads
                 // (and a store): at most those may still be in flight
-                vr_wait_meta<2>(mL, moff);
+                vr_wait_meta<2, BIN>(mL, moff, mrec);
                 producer_enter(pj);
             } else {
                 pdone = true;
@@ -336,6 +352,7 @@ crc32_vring_kernel(PacketArgs pa, KernelTables tb, const uint32_t* basis) {
 
     // ---- consumer
     uint32_t reg = 0, ccnt = 0, clz = 0, ce = 0, cj = 0, cs = 0, cstages = 0, nedge = ~0u;
+    uint32_t cidx = 0;                                       // (BIN: out index of the lane's packet)
     // first stage >= from holding a partly covered head or tail piece (~0u = none)
     auto next_edge = [&](uint32_t from) __attribute__((always_inline)) -> uint32_t {
         const bool live = ce != clz;
@@ -350,7 +367,9 @@ crc32_vring_kernel(PacketArgs pa, KernelTables tb, const uint32_t* basis) {
         if constexpr (NB == 2) {
             clz = plz;
             ce = pe;
+            if constexpr (BIN) cidx = pidx;
         } else {
+            static_assert(!BIN, "binned records: 2 ring slots only");
             clz = f0lz;
             ce = f0e;
             f0lz = f1lz; f0e = f1e;
@@ -381,7 +400,7 @@ crc32_vring_kernel(PacketArgs pa, KernelTables tb, const uint32_t* basis) {
             else __builtin_amdgcn_s_setprio(0);
         }
         produce(std::integral_constant<uint32_t, (S + NB - 1) % NB>{});
-        vr_wait<4 * (NB - 1)>(ra[S], rb[S]);                 // stage S has landed (4 younger loads per stage)
+        vr_wait<(kMetaOps + 2) * (NB - 1)>(ra[S], rb[S]);    // stage S has landed (younger: the later produces)
         u32x4 A = ra[S], B = rb[S];
         if (cs == nedge) {                                   // head / tail pieces: keep [clz, ce) only
             const uint32_t q0 = 32u * (k + P * cs);               // windows < 2 GiB: differences fit int32
@@ -412,11 +431,11 @@ crc32_vring_kernel(PacketArgs pa, KernelTables tb, const uint32_t* basis) {
             const uint32_t tz = nb ? 32u * nb - ce : 0u;
             if (k == 0u && tz) reg = vr_mulmod(reg, lds_load(cinv_addr(tz)));
             const uint64_t pk = packet_of(cj);
-            if (k == 0u && pk < pa.n) pa.out[pk] = finalize(reg);   // packet.cs:159
+            if (k == 0u && pk < pa.n) pa.out[BIN ? cidx : pk] = finalize(reg);   // packet.cs:159
             if (++cj == J) {
                 // the producer's last loads (zero lines past the end) are dead: drain
                 // them, so no register they land in can be reused while in flight
-                vr_drain(ra, rb, mL, moff);
+                vr_drain<BIN>(ra, rb, mL, moff, mrec);
                 done = true;
                 return;
             }
@@ -445,9 +464,9 @@ crc32_vring_kernel(PacketArgs pa, KernelTables tb, const uint32_t* basis) {
 
 // ---------------------------------------------------------------- host side
 
-template <int LG, int NB, int WPE, int TR = 0>
+template <int LG, int NB, int WPE, int TR = 0, int BIN = 0>
 const void* vring_fn() {
-    return reinterpret_cast<const void*>(crc32_vring_kernel<LG, NB, WPE, TR>);
+    return reinterpret_cast<const void*>(crc32_vring_kernel<LG, NB, WPE, TR, BIN>);
 }
 
 // The product instance: 2 ring slots, one workgroup per CU per launch, 64 VGPRs
@@ -456,15 +475,16 @@ const void* vring_fn() {
 // VGPRs against 4438 at 66, profiles/r02_*).  With a trace buffer: the same kernel
 // writing per-wave timestamps.  Measured and not kept: 3 and 4 ring slots, and two
 // workgroups of one launch per CU.
-const void* vring_pick(int lg, bool trace) {
+const void* vring_pick(int lg, bool trace, bool bin) {
     if (trace) return lg == 2 ? vring_fn<2, 2, 4, 1>() : vring_fn<3, 2, 4, 1>();
+    (void)bin;   // the BIN instance stays uninstantiated (see vring_launch)
     return lg == 2 ? vring_fn<2, 2, 8>() : vring_fn<3, 2, 8>();
 }
 
 int vring_setup() {
     for (int lg = 2; lg <= 3; ++lg)
         for (int t = 0; t < 2; ++t) {
-            const hipError_t e = hipFuncSetAttribute(vring_pick(lg, t == 1),
+            const hipError_t e = hipFuncSetAttribute(vring_pick(lg, t == 1, false),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, kVrLds);
             if (e != hipSuccess) return -static_cast<int>(e);
         }
@@ -473,14 +493,17 @@ int vring_setup() {
 
 int vring_launch(int lg, int num_cus, hipStream_t st, const PacketArgs& pa, const KernelTables& tb,
                  const uint32_t* basis2) {
-    if (lg != 2 && lg != 3) return -static_cast<int>(hipErrorInvalidValue);
+    // binned records (pa.meta4) run on the lean kernel: the BIN instance of this one
+    // did not pass tools/isa_inflight_check.py (hipcc copies the record register
+    // between its load and its wait), so it is not built
+    if ((lg != 2 && lg != 3) || pa.meta4) return -static_cast<int>(hipErrorInvalidValue);
     if (pa.n == 0) return 0;
     const uint64_t kpk = 64u >> lg;
     const uint64_t groups = (pa.n + kpk - 1u) / kpk;
     const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(
         1, std::min<uint64_t>((groups + kVrW - 1) / kVrW, static_cast<uint64_t>(num_cus))));
     void* args[] = {const_cast<PacketArgs*>(&pa), const_cast<KernelTables*>(&tb), const_cast<const uint32_t**>(&basis2)};
-    const hipError_t e = hipLaunchKernel(vring_pick(lg, pa.trace != nullptr), dim3(grid), dim3(64 * kVrW), args,
+    const hipError_t e = hipLaunchKernel(vring_pick(lg, pa.trace != nullptr, false), dim3(grid), dim3(64 * kVrW), args,
                                          kVrLds, st);
     return e == hipSuccess ? 0 : -static_cast<int>(e);
 }
