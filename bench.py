@@ -46,6 +46,10 @@ def parse(argv=None):
                          "launch's prologue overlaps the previous launch's tail (1 = serial)")
     ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "small"],
                     help="cfg2 = the metric's workload; cfg3 = mixed lengths; small = harness tests only")
+    ap.add_argument("--list", type=int, default=0,
+                    help="batches per launch through enet_hip_crc32_batch_list_device (0 = one "
+                         "enet_hip_crc32_batch_device call per batch); a step is then one launch "
+                         "over that many distinct resident batches (<= --rotate)")
     ap.add_argument("--binned", action="store_true",
                     help="length-binned entry (enet_hip_crc32_batch_device_binned): for mixed lengths (cfg3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -135,6 +139,7 @@ class GpuEngine:
         self.sink = torch.zeros(4, dtype=torch.int32, device="cuda")
         self.graph = None
         self.binned = False
+        self.list = 0                              # batches per launch (batch-list entry), 0 = off
         self.ws = {}                               # binned: one workspace per stream
         torch.cuda.synchronize()
 
@@ -148,10 +153,24 @@ class GpuEngine:
             for s in self.streams:
                 self.ws[s.cuda_stream] = self.torch.zeros(nb, dtype=self.torch.uint8, device="cuda")
 
+    def set_list(self, n: int):
+        if n > len(self.bufs):
+            raise SystemExit("bench.py: --list must not exceed --rotate (batches of one launch are distinct)")
+        self.list = n
+
+    def step_batches(self, i: int) -> list:
+        """Indices of the resident batches step i checksums."""
+        if self.list:
+            return [(i * self.list + t) % len(self.bufs) for t in range(self.list)]
+        return [i % len(self.bufs)]
+
     def step(self, i: int, stream=None):
         b = self.bufs[i % len(self.bufs)]
         h = self.h if stream is None else stream.cuda_stream
-        if self.binned:
+        if self.list:
+            bs = [self.bufs[j] for j in self.step_batches(i)]
+            self.ctx.crc32_batch_list_device([(x["payload"], x["off"], x["lens"], x["n"], x["out"]) for x in bs], h)
+        elif self.binned:
             w = self.ws[h]
             self.ctx.crc32_batch_device_binned(b["payload"], b["off"], b["lens"], b["n"], b["out"], w, w.numel(), h)
         else:
@@ -283,7 +302,7 @@ def kernel_name(args) -> str:
         return f"crc32_lean_kernel<0, {lg}, 16, 2, 128>"
     if lg is None:
         return "crc32_stream_kernel / crc32_direct_kernel"
-    return f"crc32_vring_kernel<{lg}, 2, 8, 0, 0>"
+    return f"crc32_vring_kernel<{lg}, 0>"
 
 
 def load_traffic(cfg: str):
@@ -307,6 +326,11 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
         eng.set_streams(args.streams)
     if args.binned:
         eng.set_binned(True)
+    if args.list:
+        if args.binned:
+            raise SystemExit("bench.py: --list and --binned are separate entry points")
+        eng.set_list(args.list)
+    per_step = args.list or 1                 # batches one step checksums
 
     # correctness gate (untimed): first resident batch vs the oracle
     eng.step(0)
@@ -326,7 +350,7 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
         eng.replay()
         eng.sync()
         lib = oracle.OracleLib()
-        for j in range(min(args.steps, len(batches))):
+        for j in range(min(args.steps * per_step, len(batches))):
             ref = lib.batch(batches[j].payload, batches[j].off, batches[j].lens, threads=8)
             if not (eng.outputs(j) == ref).all():
                 raise SystemExit(f"bench.py: graph replay CRCs of batch {j} differ from the oracle")
@@ -334,7 +358,7 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
     else:
         secs = timed_region(dist, eng.sync, args.steps, eng.step)
     secs_max = max_over_ranks(dist, secs)
-    bytes_rank = float(sum(batches[i % len(batches)].payload_bytes for i in range(args.steps)))
+    bytes_rank = float(sum(batches[i % len(batches)].payload_bytes for i in range(args.steps * per_step)))
     bytes_all = sum_over_ranks(dist, bytes_rank)
     value = bytes_all / secs_max / GIB
 
@@ -345,7 +369,7 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
     r_ms = eng.region_ms(eng.step, nk)
     k_ms, span_ms = eng.kernel_ms(eng.step, nk)
     p_ms = eng.region_ms(eng.probe, nk)
-    per_launch = float(batches[0].payload_bytes)
+    per_launch = float(batches[0].payload_bytes) * per_step
     probe_bytes = float((batches[0].payload.nbytes // 16) * 16)
     achieved = per_launch / (r_ms * 1e-3) / 1e9
     probe = probe_bytes / (p_ms * 1e-3) / 1e9
@@ -376,10 +400,12 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
                             f", {args.rotate} rotating resident batches per GPU",
                 "packets_per_gpu": batches[0].n,
                 "payload_bytes_per_step": int(per_launch),
+                "batches_per_step": per_step,
                 "parallelism": f"{ws} independent shards (no collective)",
                 "lanes_per_packet": args.lanes or "default",
                 "streams": args.streams,
-                "entry": "enet_hip_crc32_batch_device_binned" if args.binned else "enet_hip_crc32_batch_device",
+                "entry": ("enet_hip_crc32_batch_device_binned" if args.binned else
+                          "enet_hip_crc32_batch_list_device" if args.list else "enet_hip_crc32_batch_device"),
             },
             "hbm_read_frac": round(value * GIB / 1e9 / (HBM_PEAK_GBPS * ws), 4),
             "roofline": {

@@ -185,7 +185,7 @@ __device__ __forceinline__ void producer_setup(Producer<G>& pr, const PacketArgs
         pr.cur[i] = w.ws + 32ull * w0 + 16u * h;
         most = max(most, pr.nval[i]);
     }
-    pr.stages = wave_max_u(most);
+    pr.stages = max(1u, wave_max_u(most));        // a group of empty packets: one stage of zero lines
 }
 
 template <int MODE>
@@ -344,7 +344,7 @@ __global__ void __launch_bounds__(G::kThreads) crc32_stream_kernel(PacketArgs pa
 
     uint32_t cj = 0, cst = 0;
     Task t = consumer_setup<MODE>(pa, meta_slot(0), lg, group_pk0(0), lane);
-    uint32_t cstages = wave_max_u((t.cnt + G::kSB - 1u) >> G::kLsb);
+    uint32_t cstages = max(1u, wave_max_u((t.cnt + G::kSB - 1u) >> G::kLsb));   // (as pr.stages)
     uint32_t nedge = next_edge_stage<G>(t, 0);
     uint32_t reg = t.reg, desired = 0;
     bool done = false;
@@ -392,7 +392,7 @@ __global__ void __launch_bounds__(G::kThreads) crc32_stream_kernel(PacketArgs pa
                 return;
             }
             t = consumer_setup<MODE>(pa, meta_slot(cj), lg, group_pk0(cj), lane);
-            cstages = wave_max_u((t.cnt + G::kSB - 1u) >> G::kLsb);
+            cstages = max(1u, wave_max_u((t.cnt + G::kSB - 1u) >> G::kLsb));
             nedge = next_edge_stage<G>(t, 0);
             reg = t.reg;
             desired = 0;
@@ -1137,6 +1137,10 @@ int setup_stream() {
     return 0;
 }
 
+// vring workgroups per CU of one launch (enet_hip_set_tuning's workgroups_per_cu,
+// at most 2: the LDS and 64-VGPR budget of two 16-wave workgroups)
+int vring_wgs(const enet_hip_context* ctx) { return ctx->wgs_per_cu >= 2 ? 2 : 1; }
+
 int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStream_t st) {
     if (pa.n == 0) return 0;
     const KernelTables tb = tables_of(ctx);
@@ -1146,7 +1150,7 @@ int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStr
     // default (path 0) checksum batches at 4 or 8 lanes: the VGPR-ring kernel
     if (mode == 0 && !pa.meta4 && (pa.lg == 2 || pa.lg == 3) && ctx->ablation == 0 &&
         (ctx->path == 0 || ctx->path == kVringPath))
-        return vring_launch(pa.lg, ctx->num_cus, st, pa, tb, ctx->d_basis2);
+        return vring_launch(pa.lg, ctx->num_cus * vring_wgs(ctx), st, pa, tb, ctx->d_basis2);
     if (ctx->path != 1 && pa.lg >= 2 && pa.lg <= 4) {
         const bool lean_path = (ctx->path >= kLeanPath0 && ctx->path < kVringPath) || (ctx->path == 0 && ctx->ablation == 0);
         if (lean_path && pa.lg <= 3)
@@ -1314,6 +1318,39 @@ int enet_hip_crc32_batch_device(enet_hip_context* ctx, const uint8_t* bytes, con
     pa.lg = static_cast<uint32_t>(log2i(auto_lanes(ctx)));
     pa.out = out;
     return launch_packets(ctx, 0, pa, stream ? static_cast<hipStream_t>(stream) : ctx->stream);
+}
+
+int enet_hip_crc32_batch_list_device(enet_hip_context* ctx, const ENetHipBatch* batches, size_t batchCount,
+                                     void* stream) {
+    if (!ctx) return -static_cast<int>(hipErrorInvalidValue);
+    if (batchCount == 0) return 0;
+    if (!batches) return -static_cast<int>(hipErrorInvalidValue);
+    for (size_t b = 0; b < batchCount; ++b) {
+        const ENetHipBatch& e = batches[b];
+        if (e.count && (!e.bytes || !e.offsets || !e.lengths || !e.out)) return -static_cast<int>(hipErrorInvalidValue);
+    }
+    ENH_CHECK(hipSetDevice(ctx->device));
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    const int lg = log2i(auto_lanes(ctx));
+    if ((lg == 2 || lg == 3) && ctx->ablation == 0 && (ctx->path == 0 || ctx->path == kVringPath)) {
+        const KernelTables tb = tables_of(ctx);
+        for (size_t b0 = 0; b0 < batchCount; b0 += kVrMaxBatches) {
+            VrBatches bl{};
+            for (size_t b = b0; b < std::min(batchCount, b0 + kVrMaxBatches); ++b)
+                bl.b[bl.count++] = VrBatch{batches[b].bytes, batches[b].offsets, batches[b].lengths, batches[b].out,
+                                           static_cast<uint64_t>(batches[b].count), 0u, 0u};
+            const int rc = vring_launch_list(lg, ctx->num_cus * vring_wgs(ctx), st, bl, tb, ctx->d_basis2, ctx->trace);
+            if (rc) return rc;
+        }
+        return 0;
+    }
+    // other lane counts / paths: one launch per batch on the path they select
+    for (size_t b = 0; b < batchCount; ++b) {
+        const ENetHipBatch& e = batches[b];
+        const int rc = enet_hip_crc32_batch_device(ctx, e.bytes, e.offsets, e.lengths, e.count, e.out, st);
+        if (rc) return rc;
+    }
+    return 0;
 }
 
 size_t enet_hip_binned_workspace_size(size_t count) { return length_bin_workspace(count, false); }

@@ -39,44 +39,54 @@ constexpr int kVrW = 16;                                        // waves per wor
 constexpr uint32_t kVrStaging = kLdsTableBytes;                 // basis rows land after the image
 constexpr int kVrLds = kLdsTableBytes + kVrBasisRows * 256;
 
-// Global loads as inline asm, waited for by explicit counted vmcnt: the
-// compiler's own wait insertion loses count across the loop's group-switch
-// branches and falls back to vmcnt(0) right after the next stage is issued,
-// which empties the ring.  Every wait ties the registers it guards ("+v"), so
-// no use of them can be scheduled above it.
-__device__ __forceinline__ u32x4 vr_ld16(uint64_t addr) {
-    u32x4 v;
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(addr));
-    return v;
+// Global loads as inline asm into fixed registers, waited for by explicit
+// counted vmcnt.  The compiler's own wait insertion loses count across the loop's
+// group-switch branches and falls back to vmcnt(0) right after the next stage is
+// issued, which empties the ring; and a loaded value the compiler can see is one
+// it may copy while the load is still in flight.  So the loads write fixed
+// registers -- the ring slots v[44:51] and v[52:59], the metadata v[60:61]
+// (offset) and v62 (length) -- as asm the compiler knows only as clobbering them,
+// and a value exists for the compiler only as the output of the wait that retires
+// its load (an output pinned to that register).  Every load lists its registers
+// as clobbered, so a value is read out before its register is loaded again.  The
+// compiler does not know that a register is busy between a load and its wait:
+// the build checks, on the generated ISA, that no compiler instruction touches
+// one then (tools/isa_inflight_check.py, run by the Makefile).
+template <int SLOT>
+__device__ __forceinline__ void vr_issue_stage(uint64_t a0, uint64_t a1) {
+    if constexpr (SLOT == 0)
+        asm volatile("global_load_dwordx4 v[44:47], %0, off\n\tglobal_load_dwordx4 v[48:51], %1, off"
+                     :: "v"(a0), "v"(a1) : "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51");
+    else
+        asm volatile("global_load_dwordx4 v[52:55], %0, off\n\tglobal_load_dwordx4 v[56:59], %1, off"
+                     :: "v"(a0), "v"(a1) : "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59");
 }
-// The metadata loads overwrite the previous load's register whether or not that
-// value was used ("+v": the old value is an input, so its register is never
-// handed to anything else while a load into it may be in flight).
-__device__ __forceinline__ void vr_ld4(uint32_t& v, uint64_t addr) {
-    asm volatile("global_load_dword %0, %1, off" : "+v"(v) : "v"(addr));
+// the stage of SLOT once at most N younger loads are in flight
+template <int SLOT, int N>
+__device__ __forceinline__ void vr_wait_stage(u32x4& a, u32x4& b) {
+    if constexpr (SLOT == 0)
+        asm volatile("s_waitcnt vmcnt(%2)" : "={v[44:47]}"(a), "={v[48:51]}"(b) : "n"(N));
+    else
+        asm volatile("s_waitcnt vmcnt(%2)" : "={v[52:55]}"(a), "={v[56:59]}"(b) : "n"(N));
 }
-__device__ __forceinline__ void vr_ld8(uint64_t& v, uint64_t addr) {
-    asm volatile("global_load_dwordx2 %0, %1, off" : "+v"(v) : "v"(addr));
-}
-__device__ __forceinline__ void vr_ld16_tied(u32x4& v, uint64_t addr) {
-    asm volatile("global_load_dwordx4 %0, %1, off" : "+v"(v) : "v"(addr));
+__device__ __forceinline__ void vr_issue_meta(uint64_t len_addr, uint64_t off_addr) {
+    asm volatile("global_load_dword v62, %0, off\n\tglobal_load_dwordx2 v[60:61], %1, off"
+                 :: "v"(len_addr), "v"(off_addr) : "v60", "v61", "v62");
 }
 template <int N>
-__device__ __forceinline__ void vr_wait(u32x4& a, u32x4& b) {
-    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N));
+__device__ __forceinline__ void vr_wait_meta(uint32_t& L, uint64_t& off) {
+    asm volatile("s_waitcnt vmcnt(%2)" : "={v62}"(L), "={v[60:61]}"(off) : "n"(N));
 }
-// (BIN: the record register; else the length and offset registers)
-template <int N, int BIN>
-__device__ __forceinline__ void vr_wait_meta(uint32_t& L, uint64_t& off, u32x4& rec) {
-    if constexpr (BIN) asm volatile("s_waitcnt vmcnt(%1)" : "+v"(rec) : "n"(N));
-    else asm volatile("s_waitcnt vmcnt(%2)" : "+v"(L), "+v"(off) : "n"(N));
+// every load retired (the wave's exit: no load may land after it has ended)
+__device__ __forceinline__ void vr_drain() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
-// vmcnt(0) tying every register a load may still land in
-template <int BIN, int NB>
-__device__ __forceinline__ void vr_drain(u32x4 (&a)[NB], u32x4 (&b)[NB], uint32_t& L, uint64_t& off, u32x4& rec) {
-    vr_wait_meta<0, BIN>(L, off, rec);
-#pragma unroll
-    for (int i = 0; i < NB; ++i) asm volatile("" : "+v"(a[i]), "+v"(b[i]));
+
+// the lane id, not hoistable (see the kernel)
+__device__ __forceinline__ uint32_t vr_lane() {
+    uint32_t l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
 }
 
 // Zero the bytes of a block that lie outside the packet, [lo, hi) kept (block
@@ -99,20 +109,19 @@ __device__ __forceinline__ void vr_edge_mask(u32x4& A, u32x4& B, uint32_t hs, in
 // column of step i = 4g + h for lane l, col_byte(31 ^ i ^ l5), is the
 // compile-time bytes of col_byte(31 ^ i) XOR one per-lane byte col_byte(l5):
 // one register instead of eight, one XOR per 4 lookups.
+// The four v_perm selectors of make_sched differ by constants: sel[h] =
+// sel0 ^ (h * 0x101), one register instead of four.
 struct VrSched {
     uint32_t cl;        // col_byte(l & 31) in all four bytes
-    uint32_t sel[4];    // v_perm selectors (make_sched)
-    uint32_t m1, m2, hs;
+    uint32_t sel0;      // make_sched's sel[0]
+    uint32_t hs;
 };
 
 __device__ __forceinline__ VrSched make_vr_sched(uint32_t lane) {
     const LaneSched a = make_sched(lane);
     VrSched s;
     s.cl = col_byte(lane & 31u) * 0x01010101u;
-#pragma unroll
-    for (int h = 0; h < 4; ++h) s.sel[h] = a.sel[h];
-    s.m1 = a.m1;
-    s.m2 = a.m2;
+    s.sel0 = a.sel[0];
     s.hs = a.hs;
     return s;
 }
@@ -163,7 +172,8 @@ __device__ __forceinline__ uint32_t vr_fold(uint32_t reg, u32x4 A, u32x4 B, cons
         constexpr int g = decltype(gc)::value;
         const uint32_t col = vr_col_const<g>() ^ s.cl;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[g & 1][i] = lds_load(__builtin_amdgcn_perm(d[g], col, s.sel[i]));
+        for (int i = 0; i < 4; ++i)
+            v[g & 1][i] = lds_load(__builtin_amdgcn_perm(d[g], col, s.sel0 ^ (0x101u * static_cast<uint32_t>(i))));
     };
     auto reduce = [&](int g) __attribute__((always_inline)) {
         const uint32_t(&u)[4] = v[g & 1];
@@ -180,139 +190,151 @@ __device__ __forceinline__ uint32_t vr_fold(uint32_t reg, u32x4 A, u32x4 B, cons
     return acc;
 }
 
-// NB = ring slots (NB - 1 stages in flight while one is folded).
-// WPE = waves per SIMD the register allocation must allow: 8 = two 16-wave
-// workgroups per CU (64 VGPRs), 4 = one (no cap below 128).
-// TR = 1: the diagnostics instance that writes the per-wave trace (pa.trace).
-// BIN = 1: metadata from the length-ordered records of the *_binned entry points
-// (PacketArgs::meta4, 16 B {len, off_lo, off_hi, index} per packet, one load
-// instead of two); the CRC goes to out[index].
-template <int LG, int NB, int WPE, int TR = 0, int BIN = 0>
-__global__ void __launch_bounds__(64 * kVrW) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
-crc32_vring_kernel(PacketArgs pa, KernelTables tb, const uint32_t* basis) {
-    static_assert(NB >= 2 && NB <= 4, "ring slots");
+// Batches of one launch: a wave takes its share of batch 0's groups (groups wv,
+// wv + wt, ... of that batch), then of batch 1, and so on -- each batch spread
+// over the whole chip as if launched alone, with no barrier between batches, so a
+// wave that is done with batch b streams b + 1 while its neighbours finish b, and
+// the start (metadata, table image) and the drain are paid once per launch.
+struct VrIt {
+    uint32_t b, j, J;   // batch, the wave's group ordinal in it, the wave's share of it
+};
+
+// 64 VGPRs (8 waves per SIMD: two 16-wave workgroups per CU).
+// TR = 1: the diagnostics instance that writes the per-wave trace.
+template <int LG, int TR = 0>
+__global__ void __launch_bounds__(64 * kVrW) __attribute__((amdgpu_waves_per_eu(8, 8)))
+crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_t* trace) {
     constexpr uint32_t P = 1u << LG, kPk = 64u >> LG;
-    const uint32_t lane = threadIdx.x & 63u;
+    // The lane id and everything derived from it (k, p, the fold's lane constants)
+    // is recomputed in every ring iteration from a fresh v_mbcnt (asm volatile, so
+    // not hoisted): held across the loop, those ten values were what pushed the
+    // kernel past 64 VGPRs.
+    uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t ngroups = (pa.n + kPk - 1u) >> (6 - LG);
     const uint64_t wv = static_cast<uint64_t>(blockIdx.x) * kVrW + wave;
     const uint64_t wt = static_cast<uint64_t>(gridDim.x) * kVrW;
-    const uint32_t J = wv < ngroups ? static_cast<uint32_t>((ngroups - 1u - wv) / wt) + 1u : 0u;
-    const uint32_t k = lane & (P - 1u), p = lane >> LG;
+    auto lane_k = [&]() __attribute__((always_inline)) { return lane & (P - 1u); };   // block lane
+    auto lane_p = [&]() __attribute__((always_inline)) { return lane >> LG; };         // packet of the group
     const uint64_t zero = reinterpret_cast<uint64_t>(tb.zero);
-    const uint64_t base = reinterpret_cast<uint64_t>(pa.bytes);
-    auto packet_of = [&](uint32_t j) __attribute__((always_inline)) -> uint64_t {
-        return (wv + static_cast<uint64_t>(j) * wt) * kPk + p;
+
+    // ---- the wave's group sequence over the batches (wave-uniform)
+    auto share = [&](uint32_t b) __attribute__((always_inline)) -> uint32_t {   // (no division in the kernel)
+        return bl.b[b].jq + (wv < bl.b[b].jr ? 1u : 0u);
     };
+    // the batches this wave has groups in (bit b), so that moving to the next one
+    // is a bit scan: no loop inside the streaming loop
+    uint64_t live = 0;
+    for (uint32_t b = 0; b < bl.count; ++b) live |= share(b) ? 1ull << b : 0ull;
+    // the next group after `it`, false (it unchanged) past the wave's last group
+    auto advance = [&](VrIt& it) __attribute__((always_inline)) -> bool {
+        const bool in_batch = it.j + 1u < it.J;
+        const uint64_t rest = live & (~1ull << it.b);        // batches after it.b (it.b < 48)
+        if (!in_batch && !rest) return false;
+        const uint32_t nbt = static_cast<uint32_t>(__builtin_ctzll(rest | (1ull << 63)));
+        it.j = in_batch ? it.j + 1u : 0u;
+        it.J = in_batch ? it.J : share(nbt);
+        it.b = in_batch ? it.b : nbt;
+        return true;
+    };
+    auto group_base = [&](const VrIt& it) __attribute__((always_inline)) -> uint64_t {   // its first packet
+        return (wv + static_cast<uint64_t>(it.j) * wt) * kPk;
+    };
+    const bool any = live != 0u;
+    VrIt pit{0u, 0u, 0u};                                    // the producer's group
+    if (any) {
+        pit.b = static_cast<uint32_t>(__builtin_ctzll(live));
+        pit.J = share(pit.b);
+    }
+    VrIt qit = pit;                                          // the group whose metadata is loaded
+    bool qlive = any && advance(qit);
 
     // diagnostics (enet_hip_diag_trace): per-wave timestamps, tools/timeline.py's
-    // 8 x u64 layout [start, metadata, table, barrier B, first stage, end, HW_ID, groups]
-    uint64_t tmark[5] = {0, 0, 0, 0, 0};
+    // 8 x u64 layout [start, metadata, table, barrier B, loop entry, end, HW_ID, groups]
+    // (each mark is stored at once: held in registers, the marks cost SGPR spills)
+    uint32_t ngroups = 0;
     auto mark = [&](int i) __attribute__((always_inline)) {
-        if (TR) tmark[i] = __builtin_amdgcn_s_memrealtime();
+        if (TR && (threadIdx.x & 63u) == 0u) trace[8u * wv + i] = __builtin_amdgcn_s_memrealtime();
     };
     auto trace_end = [&]() __attribute__((always_inline)) {
-        if (TR && lane == 0u) {
-            uint64_t* tr = pa.trace + 8u * wv;
+        if (TR && (threadIdx.x & 63u) == 0u) {
+            uint64_t* tr = trace + 8u * wv;
             tr[5] = __builtin_amdgcn_s_memrealtime();
-#pragma unroll
-            for (int i = 0; i < 5; ++i) tr[i] = tmark[i];
             const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);      // HW_ID
             const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);    // XCC_ID
             tr[6] = hw | (static_cast<uint64_t>(xcc) << 32);
-            tr[7] = J;
+            tr[7] = ngroups;
         }
     };
     mark(0);
-    // tuning (pa.prio): the SIMD arbiter favours older waves, so wave slots 12-15 of a
-    // workgroup finish ~40 % after slots 0-3 (profiles/r02_timeline_*): issue priority
-    // by slot quartile, youngest highest
-    if (pa.prio == 1u) {
-        const uint32_t q = wave >> 2;                        // wave-uniform
-        if (q == 1u) __builtin_amdgcn_s_setprio(1);
-        else if (q == 2u) __builtin_amdgcn_s_setprio(2);
-        else if (q == 3u) __builtin_amdgcn_s_setprio(3);
-    }
 
-    // ---- prologue: basis row `wave` (waves < 10) and metadata of group 0
+    // ---- prologue: basis row `wave` (waves < 10) and metadata of the first group
     if (wave < static_cast<uint32_t>(kVrBasisRows))
         dma4(basis + static_cast<size_t>(LG == 2 ? 1 : 2) * kVrBasisDwords + 64u * wave + lane,
              kVrStaging + 256u * wave);
-    uint32_t mL = 0;                                         // metadata of the producer's next group
+    uint32_t mL = 0;                                         // metadata (read out at group switches)
     uint64_t moff = 0;
-    u32x4 mrec = {0u, 0u, 0u, 0u};                           // (BIN: the record)
-    constexpr int kMetaOps = BIN ? 1 : 2;                    // metadata loads per produce
-    auto load_meta = [&](uint32_t j) __attribute__((always_inline)) {
-        const uint64_t q = min(packet_of(j), pa.n - 1u);
-        if constexpr (BIN) {
-            vr_ld16_tied(mrec, reinterpret_cast<uint64_t>(pa.meta4 + 4u * q));
-        } else {
-            vr_ld4(mL, reinterpret_cast<uint64_t>(pa.len + q));
-            vr_ld8(moff, reinterpret_cast<uint64_t>(pa.off + q));
-        }
+    auto load_meta = [&](const VrIt& it) __attribute__((always_inline)) {
+        const VrBatch& B = bl.b[it.b];
+        // the lane's packet, clamped to the batch's last (always a valid address; the
+        // prologue of a wave with no group at all loads batch 0's last packet)
+        const uint64_t base = min<uint64_t>(group_base(it), B.n - 1u);
+        const uint64_t left = B.n - 1u - base;               // (uniform: scalar select, no VALU)
+        const uint32_t q = min(lane_p(), left < 63u ? static_cast<uint32_t>(left) : 63u);
+        vr_issue_meta(reinterpret_cast<uint64_t>(B.len + base) + 4u * q,
+                      reinterpret_cast<uint64_t>(B.off + base) + 8u * q);
     };
-    load_meta(0);                                            // (clamped index: valid for J == 0 too)
-    vr_wait_meta<0, BIN>(mL, moff, mrec);                    // basis row and metadata have landed
+    load_meta(any ? pit : VrIt{0u, 0u, 0u});                 // (batch 0 exists: count >= 1)
+    vr_wait_meta<0>(mL, moff);                               // basis row and metadata have landed
     mark(1);
 
     // ---- producer: window of the group it loads, one stage ahead of the consumer
     uint64_t pws = 0;                                        // window start (64-byte aligned)
     uint32_t plz = 0, pe = 0;                                // packet bytes [plz, pe) of the window
-    uint32_t pj = 0, pst = 0, pstages = 0;
-    bool pdone = J == 0;
-    // hand-over of the windows to the consumer, which runs NB - 1 stages behind:
-    // with NB == 2 it enters a group right after the producer did and reads plz /
-    // pe; deeper rings keep a FIFO of the windows the producer entered ahead
-    uint32_t f0lz = 0, f0e = 0, f1lz = 0, f1e = 0, f2lz = 0, f2e = 0, fn = 0;
-    uint32_t pidx = 0;                                       // (BIN: caller index of the lane's packet)
-    auto producer_enter = [&](uint32_t j) __attribute__((always_inline)) {
-        const uint32_t L = packet_of(j) < pa.n ? (BIN ? mrec.x : mL) : 0u;
-        const uint64_t a = base + (BIN ? (static_cast<uint64_t>(mrec.y) | (static_cast<uint64_t>(mrec.z) << 32)) : moff);
-        if constexpr (BIN) pidx = mrec.w;
-        plz = static_cast<uint32_t>(a) & 63u;
-        pws = a - plz;
+    uint32_t pst = 0, pstages = 0;
+    bool pdone = !any;
+    auto producer_enter = [&]() __attribute__((always_inline)) {   // group pit; metadata in mL / moff
+        const VrBatch& B = bl.b[pit.b];
+        const uint64_t rem = B.n - group_base(pit);          // packets of the batch from the group's first
+        const uint32_t L = lane_p() < rem ? mL : 0u;
+        const uint64_t a = reinterpret_cast<uint64_t>(B.bytes) + moff;
+        const uint32_t lz = static_cast<uint32_t>(a) & 63u;
+        pws = a - lz;
+        plz = L ? lz : 0u;                                   // an empty packet: [0, 0)
         pe = plz + L;
-        const uint32_t nb = L ? (pe + 31u) >> 5 : 0u;
+        const uint32_t nb = (pe + 31u) >> 5;
         pstages = max(1u, wave_max_u((nb + P - 1u) >> LG));
         pst = 0;
-        if constexpr (NB > 2) {
-            if (fn == 0u) { f0lz = plz; f0e = pe; }
-            else if (fn == 1u) { f1lz = plz; f1e = pe; }
-            else { f2lz = plz; f2e = pe; }
-            ++fn;
-        }
     };
-    const VrSched s = make_vr_sched(lane);
-    // Every produce issues the same four loads -- the metadata of the group after
-    // the producer's (an L2 hit but at group switches) and the stage's two
-    // pieces -- so every wait below has a fixed count.
-    u32x4 ra[NB], rb[NB];
+    // Every produce issues the same four loads -- the metadata of group qit (an L2
+    // hit but at group switches) and the stage's two pieces -- so every wait below
+    // has a fixed count.
     auto produce = [&](auto slot_c) __attribute__((always_inline)) {
         constexpr uint32_t slot = decltype(slot_c)::value;
         if (!pdone && pst == pstages) {
-            if (++pj < J) {
+            if (qlive) {
                 // last produce's metadata loads are older than its two stage loads
                 // (and a store): at most those may still be in flight
-                vr_wait_meta<2, BIN>(mL, moff, mrec);
-                producer_enter(pj);
+                vr_wait_meta<2>(mL, moff);
+                pit = qit;
+                qlive = advance(qit);
+                producer_enter();
             } else {
                 pdone = true;
                 plz = pe = 0;                                // every piece reads the zero line
             }
         }
-        load_meta(min(pj + 1u, J - 1u));
-        const uint32_t q0 = 32u * (k + P * pst);
-        const uint32_t hs16 = s.hs & 16u;                    // this lane takes the block's halves swapped
+        load_meta(qit);                                      // (past the end: qit is the last group)
+        const uint32_t q0 = 32u * (lane_k() + P * pst);
+        const uint32_t hs16 = lane & 16u;                    // this lane takes the block's halves swapped
         const uint32_t a0 = q0 + hs16, a1 = q0 + 16u - hs16;
         const uint64_t s0 = (a0 < pe && a0 + 16u > plz) ? pws + a0 : zero;
         const uint64_t s1 = (a1 < pe && a1 + 16u > plz) ? pws + a1 : zero;
-        ra[slot] = vr_ld16(s0);
-        rb[slot] = vr_ld16(s1);
+        vr_issue_stage<slot>(s0, s1);
         ++pst;
     };
-    if (J) {
-        producer_enter(0);
-        unroll_slots<NB - 1>([&](auto sc) __attribute__((always_inline)) { produce(sc); });
+    if (any) {
+        producer_enter();
+        produce(std::integral_constant<uint32_t, 0>{});
     }
 
     // ---- the table image, rebuilt in LDS while stage 0 is in flight.  Wave w
@@ -345,75 +367,60 @@ crc32_vring_kernel(PacketArgs pa, KernelTables tb, const uint32_t* basis) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();                            // (B) the image is complete
     mark(3);
-    if (!J) {
-        trace_end();
+    if (!any) {
+        trace_end();                                         // (the prologue's loads are retired)
         return;
     }
 
     // ---- consumer
-    uint32_t reg = 0, ccnt = 0, clz = 0, ce = 0, cj = 0, cs = 0, cstages = 0, nedge = ~0u;
-    uint32_t cidx = 0;                                       // (BIN: out index of the lane's packet)
+    uint32_t reg = 0, clz = 0, ce = 0, cs = 0, cstages = 0, nedge = ~0u;
+    uint32_t* cout = nullptr;                                // the CRCs of the group's packets
+    uint64_t crem = 0;                                       // packets of its batch from the group's first
     // first stage >= from holding a partly covered head or tail piece (~0u = none)
     auto next_edge = [&](uint32_t from) __attribute__((always_inline)) -> uint32_t {
         const bool live = ce != clz;
         const uint32_t wh = clz >> 5, wl = (ce - 1u) >> 5;
-        uint32_t h = (live && (clz & 15u) && (wh & (P - 1u)) == k) ? wh >> LG : ~0u;
-        uint32_t t = (live && (ce & 15u) && (wl & (P - 1u)) == k) ? wl >> LG : ~0u;
+        uint32_t h = (live && (clz & 15u) && (wh & (P - 1u)) == lane_k()) ? wh >> LG : ~0u;
+        uint32_t t = (live && (ce & 15u) && (wl & (P - 1u)) == lane_k()) ? wl >> LG : ~0u;
         h = h >= from ? h : ~0u;
         t = t >= from ? t : ~0u;
         return wave_min_u(min(h, t));
     };
+    // Entered right after the producer has entered the same group (the producer
+    // runs exactly one stage ahead), so pit / plz / pe are that group's.
     auto consumer_enter = [&]() __attribute__((always_inline)) {
-        if constexpr (NB == 2) {
-            clz = plz;
-            ce = pe;
-            if constexpr (BIN) cidx = pidx;
-        } else {
-            static_assert(!BIN, "binned records: 2 ring slots only");
-            clz = f0lz;
-            ce = f0e;
-            f0lz = f1lz; f0e = f1e;
-            f1lz = f2lz; f1e = f2e;
-            --fn;
-        }
-        const uint32_t nb = ce != clz ? (ce + 31u) >> 5 : 0u;
-        ccnt = nb > k ? ((nb - 1u - k) >> LG) + 1u : 0u;
+        clz = plz;
+        ce = pe;
+        const uint64_t base = group_base(pit);
+        cout = bl.b[pit.b].out + base;
+        crem = bl.b[pit.b].n - base;
+        const uint32_t nb = (ce + 31u) >> 5;                 // 0 for an empty packet ([0, 0))
         cstages = max(1u, wave_max_u((nb + P - 1u) >> LG));
         const uint32_t init = lds_load(init_addr(clz));
-        reg = k == 0u ? (nb ? init : 0xFFFFFFFFu) : 0u;      // packet.cs:144 (empty packet: ~crc = 0)
+        reg = lane_k() == 0u ? (nb ? init : 0xFFFFFFFFu) : 0u;      // packet.cs:144 (empty packet: ~crc = 0)
         nedge = next_edge(0);
         cs = 0;
+        if (TR) ++ngroups;
     };
     consumer_enter();
     bool done = false;
     auto iteration = [&](auto sc) __attribute__((always_inline)) {
         constexpr uint32_t S = decltype(sc)::value;
-        if (pa.prio == 2u) {
-            // equal progress: the SIMD arbiter serves high priority first, then older
-            // waves; a wave with more of its work left than its neighbours goes first,
-            // so no wave is left streaming alone at the end
-            const uint32_t left = (J - cj) * 8u - min(8u, (cs * 8u) / cstages);   // eighths of groups left
-            const uint32_t q = (left * 4u) / (J * 8u + 1u);                        // 0..3
-            if (q >= 3u) __builtin_amdgcn_s_setprio(3);
-            else if (q == 2u) __builtin_amdgcn_s_setprio(2);
-            else if (q == 1u) __builtin_amdgcn_s_setprio(1);
-            else __builtin_amdgcn_s_setprio(0);
-        }
-        produce(std::integral_constant<uint32_t, (S + NB - 1) % NB>{});
-        vr_wait<(kMetaOps + 2) * (NB - 1)>(ra[S], rb[S]);    // stage S has landed (younger: the later produces)
-        u32x4 A = ra[S], B = rb[S];
+        lane = vr_lane();
+        produce(std::integral_constant<uint32_t, S ^ 1u>{});
+        u32x4 A, B;
+        vr_wait_stage<S, 4>(A, B);                           // stage S has landed (the next produce's 4 are younger)
         if (cs == nedge) {                                   // head / tail pieces: keep [clz, ce) only
-            const uint32_t q0 = 32u * (k + P * cs);               // windows < 2 GiB: differences fit int32
-            vr_edge_mask(A, B, s.hs, static_cast<int32_t>(clz - q0), static_cast<int32_t>(ce - q0));
+            const uint32_t q0 = 32u * (lane_k() + P * cs);               // windows < 2 GiB: differences fit int32
+            vr_edge_mask(A, B, make_vr_sched(lane).hs, static_cast<int32_t>(clz - q0), static_cast<int32_t>(ce - q0));
             nedge = next_edge(cs + 1u);
         }
-        const uint32_t nr = vr_fold(reg, A, B, s, lane);
-        reg = cs < ccnt ? nr : reg;
-        if (cj == 0u && cs == 0u) mark(4);
+        const uint32_t nr = vr_fold(reg, A, B, make_vr_sched(lane), lane);
+        reg = 32u * (lane_k() + P * cs) < ce ? nr : reg;            // the lane's block k + P cs is in the window
         if (++cs == cstages) {
             // lane k is o = (k - nb) mod P blocks past the window end: x^(-256 o)
-            const uint32_t nb = ce != clz ? (ce + 31u) >> 5 : 0u;
-            const uint32_t o = (k - nb) & (P - 1u);
+            const uint32_t nb = (ce + 31u) >> 5;
+            const uint32_t o = (lane_k() - nb) & (P - 1u);
             // (lane-uniform byte order: per-lane rotations hoisted out of the loop cost
             // ten VGPRs; four lookups per packet can afford the bank conflicts)
             const uint32_t kk = o ? o : 1u;
@@ -429,13 +436,12 @@ crc32_vring_kernel(PacketArgs pa, KernelTables tb, const uint32_t* basis) {
             reg = o ? corr : reg;
             reg = xor_lanes<0>(LG, reg);
             const uint32_t tz = nb ? 32u * nb - ce : 0u;
-            if (k == 0u && tz) reg = vr_mulmod(reg, lds_load(cinv_addr(tz)));
-            const uint64_t pk = packet_of(cj);
-            if (k == 0u && pk < pa.n) pa.out[BIN ? cidx : pk] = finalize(reg);   // packet.cs:159
-            if (++cj == J) {
-                // the producer's last loads (zero lines past the end) are dead: drain
-                // them, so no register they land in can be reused while in flight
-                vr_drain<BIN>(ra, rb, mL, moff, mrec);
+            if (lane_k() == 0u && tz) reg = vr_mulmod(reg, lds_load(cinv_addr(tz)));
+            if (lane_k() == 0u && lane_p() < crem) cout[lane_p()] = finalize(reg);   // packet.cs:159
+            if (pdone) {
+                // no newer group entered: the wave is done.  The producer's last loads
+                // (zero lines past the end) are dead: retire them before the wave ends
+                vr_drain();
                 done = true;
                 return;
             }
@@ -445,67 +451,79 @@ crc32_vring_kernel(PacketArgs pa, KernelTables tb, const uint32_t* basis) {
     // each slot's iteration leaves the loop at once when the wave is done, so the
     // loop head is reached only from a completed ring turn (no path with the drained
     // loads of the last turn in flight: tools/isa_inflight_check.py)
+    mark(4);                                                 // (streaming starts)
     for (;;) {
         iteration(std::integral_constant<uint32_t, 0>{});
         if (done) break;
         iteration(std::integral_constant<uint32_t, 1>{});
         if (done) break;
-        if constexpr (NB > 2) {
-            iteration(std::integral_constant<uint32_t, 2>{});
-            if (done) break;
-        }
-        if constexpr (NB > 3) {
-            iteration(std::integral_constant<uint32_t, 3>{});
-            if (done) break;
-        }
     }
     trace_end();
 }
 
 // ---------------------------------------------------------------- host side
 
-template <int LG, int NB, int WPE, int TR = 0, int BIN = 0>
+template <int LG, int TR = 0>
 const void* vring_fn() {
-    return reinterpret_cast<const void*>(crc32_vring_kernel<LG, NB, WPE, TR, BIN>);
+    return reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR>);
 }
 
-// The product instance: 2 ring slots, one workgroup per CU per launch, 64 VGPRs
-// (WPE 8) so that the next launch's workgroup -- overlapping batches on other
-// streams -- can share the CU while this one drains (bench: 4831 GiB/s at 59-62
-// VGPRs against 4438 at 66, profiles/r02_*).  With a trace buffer: the same kernel
-// writing per-wave timestamps.  Measured and not kept: 3 and 4 ring slots, and two
-// workgroups of one launch per CU.
-const void* vring_pick(int lg, bool trace, bool bin) {
-    if (trace) return lg == 2 ? vring_fn<2, 2, 4, 1>() : vring_fn<3, 2, 4, 1>();
-    (void)bin;   // the BIN instance stays uninstantiated (see vring_launch)
-    return lg == 2 ? vring_fn<2, 2, 8>() : vring_fn<3, 2, 8>();
+// The product instance: one workgroup per CU per launch, 64 VGPRs (WPE 8) so that
+// the next launch's workgroup -- overlapping batches on other streams -- can share
+// the CU while this one drains (bench: 4831 GiB/s at 59-62 VGPRs against 4438 at
+// 66, profiles/r02_*).  With a trace buffer: the same kernel writing per-wave
+// timestamps.  Measured and not kept: 3 and 4 ring slots, two workgroups of one
+// launch per CU, and a binned-records variant (its record register was copied by
+// hipcc between load and wait: tools/isa_inflight_check.py).
+const void* vring_pick(int lg, bool trace) {
+    if (trace) return lg == 2 ? vring_fn<2, 1>() : vring_fn<3, 1>();
+    return lg == 2 ? vring_fn<2>() : vring_fn<3>();
 }
 
 int vring_setup() {
     for (int lg = 2; lg <= 3; ++lg)
         for (int t = 0; t < 2; ++t) {
-            const hipError_t e = hipFuncSetAttribute(vring_pick(lg, t == 1, false),
+            const hipError_t e = hipFuncSetAttribute(vring_pick(lg, t == 1),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, kVrLds);
             if (e != hipSuccess) return -static_cast<int>(e);
         }
     return 0;
 }
 
-int vring_launch(int lg, int num_cus, hipStream_t st, const PacketArgs& pa, const KernelTables& tb,
-                 const uint32_t* basis2) {
-    // binned records (pa.meta4) run on the lean kernel: the BIN instance of this one
-    // did not pass tools/isa_inflight_check.py (hipcc copies the record register
-    // between its load and its wait), so it is not built
-    if ((lg != 2 && lg != 3) || pa.meta4) return -static_cast<int>(hipErrorInvalidValue);
-    if (pa.n == 0) return 0;
+int vring_launch_list(int lg, int max_wgs, hipStream_t st, const VrBatches& bl, const KernelTables& tb,
+                      const uint32_t* basis2, uint64_t* trace) {
+    if ((lg != 2 && lg != 3) || bl.count > static_cast<uint32_t>(kVrMaxBatches))
+        return -static_cast<int>(hipErrorInvalidValue);
+    // empty batches dropped: the kernel may then read any batch's packet n - 1
+    VrBatches a{};
+    for (uint32_t b = 0; b < bl.count; ++b)
+        if (bl.b[b].n) a.b[a.count++] = bl.b[b];
+    if (a.count == 0) return 0;
     const uint64_t kpk = 64u >> lg;
-    const uint64_t groups = (pa.n + kpk - 1u) / kpk;
+    uint64_t groups = 0;                                     // the largest batch sets the grid
+    for (uint32_t b = 0; b < a.count; ++b) groups = std::max<uint64_t>(groups, (a.b[b].n + kpk - 1u) / kpk);
     const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(
-        1, std::min<uint64_t>((groups + kVrW - 1) / kVrW, static_cast<uint64_t>(num_cus))));
-    void* args[] = {const_cast<PacketArgs*>(&pa), const_cast<KernelTables*>(&tb), const_cast<const uint32_t**>(&basis2)};
-    const hipError_t e = hipLaunchKernel(vring_pick(lg, pa.trace != nullptr, false), dim3(grid), dim3(64 * kVrW), args,
-                                         kVrLds, st);
+        1, std::min<uint64_t>((groups + kVrW - 1) / kVrW, static_cast<uint64_t>(max_wgs))));
+    const uint64_t waves = static_cast<uint64_t>(grid) * kVrW;
+    for (uint32_t b = 0; b < a.count; ++b) {
+        const uint64_t g = (a.b[b].n + kpk - 1u) / kpk;
+        if (g / waves > 0xFFFFFFFFull) return -static_cast<int>(hipErrorInvalidValue);
+        a.b[b].jq = static_cast<uint32_t>(g / waves);
+        a.b[b].jr = static_cast<uint32_t>(g % waves);
+    }
+    void* args[] = {&a, const_cast<KernelTables*>(&tb), const_cast<const uint32_t**>(&basis2), &trace};
+    const hipError_t e = hipLaunchKernel(vring_pick(lg, trace != nullptr), dim3(grid), dim3(64 * kVrW), args, kVrLds, st);
     return e == hipSuccess ? 0 : -static_cast<int>(e);
+}
+
+int vring_launch(int lg, int max_wgs, hipStream_t st, const PacketArgs& pa, const KernelTables& tb,
+                 const uint32_t* basis2) {
+    if (pa.meta4) return -static_cast<int>(hipErrorInvalidValue);   // binned records: the lean kernel
+    if (pa.n == 0) return 0;
+    VrBatches bl{};
+    bl.count = 1;
+    bl.b[0] = VrBatch{pa.bytes, pa.off, pa.len, pa.out, pa.n};
+    return vring_launch_list(lg, max_wgs, st, bl, tb, basis2, pa.trace);
 }
 
 }  // namespace enethip

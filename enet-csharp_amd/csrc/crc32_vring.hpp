@@ -13,14 +13,40 @@ namespace enethip {
 constexpr int kVrBasisRows = 10;
 constexpr int kVrBasisDwords = kVrBasisRows * 64;
 
+// One batch of a batch-list launch (device pointers; packet i of the batch is
+// bytes[off[i] .. off[i] + len[i]), its CRC goes to out[i]).
+struct VrBatch {
+    const uint8_t* bytes;
+    const uint64_t* off;
+    const uint32_t* len;
+    uint32_t* out;
+    uint64_t n;
+    // set by vring_launch_list: the batch's G = ceil(n / packets per group) groups
+    // as G = jq * waves + jr over the launch's waves (wave w takes jq + (w < jr))
+    uint32_t jq, jr;
+};
+// Kernel-argument block (<= 4 KiB): up to kVrMaxBatches batches per launch.
+constexpr int kVrMaxBatches = 48;
+struct VrBatches {
+    uint32_t count;
+    uint32_t pad;
+    VrBatch b[kVrMaxBatches];
+};
+static_assert(sizeof(VrBatches) <= 3072, "kernel arguments");
+
 // Set the dynamic-LDS attribute of every vring kernel instance (once per context).
 int vring_setup();
 
+// Launch over a list of batches (bl.count <= kVrMaxBatches): one launch, each batch
+// spread over the whole chip in turn, at most max_wgs 16-wave workgroups (the CU
+// count: one per CU; twice that: two).  trace = per-wave timestamps or null.
+int vring_launch_list(int lg, int max_wgs, hipStream_t st, const VrBatches& bl, const KernelTables& tb,
+                      const uint32_t* basis2, uint64_t* trace);
 
-// Launch the vring kernel: checksum mode, lanes per packet 2^lg (lg = 2 or 3),
-// one 16-wave workgroup per CU.  basis2 = kVrBasisDwords per image (images for
+// Launch the vring kernel over one batch: checksum mode, lanes per packet 2^lg
+// (lg = 2 or 3), at most max_wgs workgroups.  basis2 = kVrBasisDwords per image (images for
 // P = 1, 4, 8, 16 in that order).  Returns 0 or -hipError_t.
-int vring_launch(int lg, int num_cus, hipStream_t st, const PacketArgs& pa, const KernelTables& tb,
+int vring_launch(int lg, int max_wgs, hipStream_t st, const PacketArgs& pa, const KernelTables& tb,
                  const uint32_t* basis2);
 
 }  // namespace enethip

@@ -27,7 +27,7 @@ LIB_PATH = os.path.join(PKG_ROOT, "libenethip.so")
 EXPORTED_SYMBOLS = (
     "enet_hip_crc32", "enet_hip_crc32_update", "enet_hip_device_count", "enet_hip_context_create",
     "enet_hip_context_destroy", "enet_hip_error_string", "enet_hip_set_tuning",
-    "enet_hip_crc32_batch_device", "enet_hip_binned_workspace_size", "enet_hip_crc32_batch_device_binned",
+    "enet_hip_crc32_batch_device", "enet_hip_crc32_batch_list_device", "enet_hip_binned_workspace_size", "enet_hip_crc32_batch_device_binned",
     "enet_hip_verify_binned_workspace_size", "enet_hip_verify_batch_device_binned",
     "enet_hip_crc32_batch_host", "enet_hip_verify_batch_device",
     "enet_hip_crc32_gather_device", "enet_hip_crc32_batch_multi", "enet_hip_device_alloc",
@@ -36,6 +36,12 @@ EXPORTED_SYMBOLS = (
     "enet_hip_diag_ablation", "enet_hip_diag_trace", "enet_hip_fragment_reassemble_device",
     "enet_hip_range_compress_device", "enet_hip_range_decompress_device",
 )
+
+
+class ENetHipBatch(ctypes.Structure):
+    """include/enet_hip.h ENetHipBatch: one batch of a batch-list call (device pointers)."""
+    _fields_ = [("bytes", ctypes.c_void_p), ("offsets", ctypes.c_void_p), ("lengths", ctypes.c_void_p),
+                ("count", ctypes.c_size_t), ("out", ctypes.c_void_p)]
 
 
 class ENetHipError(RuntimeError):
@@ -83,6 +89,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.enet_hip_set_kernel_path.argtypes = [vp, i32]
     L.enet_hip_crc32_batch_device.restype = i32
     L.enet_hip_crc32_batch_device.argtypes = [vp, vp, vp, vp, sz, vp, vp]
+    L.enet_hip_crc32_batch_list_device.restype = i32
+    L.enet_hip_crc32_batch_list_device.argtypes = [vp, vp, sz, vp]
     L.enet_hip_binned_workspace_size.restype = sz
     L.enet_hip_binned_workspace_size.argtypes = [sz]
     L.enet_hip_crc32_batch_device_binned.restype = i32
@@ -218,6 +226,14 @@ class Context:
     def crc32_batch_device(self, d_bytes, d_off, d_len, n: int, d_out, stream: int = 0) -> None:
         _check("enet_hip_crc32_batch_device", self.lib.enet_hip_crc32_batch_device(
             self.handle, _ptr(d_bytes), _ptr(d_off), _ptr(d_len), int(n), _ptr(d_out), stream or None))
+
+    def crc32_batch_list_device(self, batches, stream: int = 0) -> None:
+        """batches: sequence of (d_bytes, d_off, d_len, n, d_out); one launch per 48 batches."""
+        arr = (ENetHipBatch * max(1, len(batches)))()
+        for i, (b, o, l, n, out) in enumerate(batches):
+            arr[i] = ENetHipBatch(_ptr(b) or None, _ptr(o) or None, _ptr(l) or None, int(n), _ptr(out) or None)
+        _check("enet_hip_crc32_batch_list_device", self.lib.enet_hip_crc32_batch_list_device(
+            self.handle, ctypes.cast(arr, ctypes.c_void_p), len(batches), stream or None))
 
     def binned_workspace_size(self, n: int) -> int:
         return int(self.lib.enet_hip_binned_workspace_size(int(n)))

@@ -94,6 +94,25 @@ ENET_HIP_API int enet_hip_crc32_batch_device(enet_hip_context* ctx, const uint8_
                                              const uint64_t* offsets, const uint32_t* lengths,
                                              size_t count, uint32_t* out, void* stream);
 
+/* ---- several batches in one launch ----
+ * batches[0 .. batchCount) is a HOST array; each entry names one batch exactly as
+ * enet_hip_crc32_batch_device's arguments do (device pointers).  Same results as
+ * one enet_hip_crc32_batch_device call per batch, in one kernel launch per 48
+ * batches: each batch is spread over the whole GPU in turn, with no barrier
+ * between batches, so the per-launch start (table image, metadata) and end
+ * (drain) are paid once per launch instead of once per batch.  Batches may not
+ * share `out` ranges.  Async; graph-capturable (the descriptors are copied into
+ * the kernel arguments at the call). */
+typedef struct {
+    const uint8_t* bytes;
+    const uint64_t* offsets;
+    const uint32_t* lengths;
+    size_t count;
+    uint32_t* out;
+} ENetHipBatch;
+ENET_HIP_API int enet_hip_crc32_batch_list_device(enet_hip_context* ctx, const ENetHipBatch* batches,
+                                                  size_t batchCount, void* stream);
+
 /* Same results as enet_hip_crc32_batch_device (enet_crc32, c/packet.cs:142-160,
  * per packet), for batches of mixed lengths (SURVEY cfg3): inside each tile of
  * 1024 packets the packet records are first ordered by length (32-byte bins,

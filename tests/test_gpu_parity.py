@@ -392,3 +392,134 @@ def test_gather_golden_and_cfg5(ctx, golden, oracle_lib):
 def test_bad_tuning_raises(ctx):
     with pytest.raises(enethip.ENetHipError):
         ctx.set_tuning(3, 0)
+
+
+def test_vring_many_groups(ctx, oracle_lib):
+    """The default VGPR-ring kernel (4 and 8 lanes): tiny packets (one-stage groups,
+    the producer switching group every stage, empty packets among them) and long
+    ones (many stages per group), each against the oracle."""
+    tiny = workloads.mixed(1_200_000, 0, 40, seed=177, len_seed=178)
+    exp_t = oracle_lib.batch(tiny.payload, tiny.off, tiny.lens, threads=16)
+    big = workloads.mixed(40_000, 2000, 9000, seed=179, len_seed=180)
+    exp_b = oracle_lib.batch(big.payload, big.off, big.lens, threads=16)
+    try:
+        for path in (0, 17):
+            ctx.set_kernel_path(path)
+            for lanes in (4, 8):
+                assert (run_batch(ctx, tiny.payload, tiny.off, tiny.lens, lanes) == exp_t).all(), ("tiny", path, lanes)
+                assert (run_batch(ctx, big.payload, big.off, big.lens, lanes) == exp_b).all(), ("big", path, lanes)
+    finally:
+        ctx.set_kernel_path(0)
+        ctx.set_tuning(0, 0)
+
+
+def _batch_list_cases(oracle_lib):
+    """(payload, off, lens, expected) per batch: empty, single packets, golden-like
+    small lengths, cfg2-shaped MTU packets, long packets, tiny packets."""
+    specs = [(0, 0, 0, 1), (1, 0, 0, 2), (1, 1, 1, 3), (17, 0, 64, 4), (65_536, 1200, 1200, 5),
+             (3000, 2000, 9000, 6), (250_000, 0, 40, 7), (5, 31, 33, 8), (70_000, 1, 1400, 9)]
+    out = []
+    for n, lo, hi, seed in specs:
+        b = workloads.mixed(n, lo, hi, seed=300 + seed, len_seed=400 + seed) if n else None
+        if b is None:
+            out.append((np.zeros(16, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint32),
+                        np.zeros(0, np.uint32)))
+        else:
+            out.append((b.payload, b.off, b.lens, oracle_lib.batch(b.payload, b.off, b.lens, threads=16)))
+    return out
+
+
+def _run_list(ctx, cases):
+    keep, descs, outs = [], [], []
+    for payload, off, lens, _ in cases:
+        d = (dev(payload if len(payload) else np.zeros(16, np.uint8)),
+             dev(off) if len(off) else dev(np.zeros(1, np.uint64)),
+             dev(lens) if len(lens) else dev(np.zeros(1, np.uint32)))
+        o = torch.full((max(1, len(off)),), -1, dtype=torch.int32, device="cuda")
+        keep.append(d)
+        outs.append(o)
+        descs.append((d[0], d[1], d[2], len(off), o))
+    ctx.crc32_batch_list_device(descs, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return [o.cpu().numpy().view(np.uint32)[:len(c[1])] for o, c in zip(outs, cases)]
+
+
+def test_batch_list(ctx, oracle_lib):
+    """enet_hip_crc32_batch_list_device: batches of every shape in one launch,
+    each against the oracle; 4 and 8 lanes (vring), 16 lanes (one launch per
+    batch on the stream kernel)."""
+    cases = _batch_list_cases(oracle_lib)
+    try:
+        for lanes in (4, 8, 16):
+            ctx.set_tuning(lanes, 0)
+            for i, (got, c) in enumerate(zip(_run_list(ctx, cases), cases)):
+                assert (got == c[3]).all(), (lanes, i, np.nonzero(got != c[3])[0][:5])
+    finally:
+        ctx.set_tuning(0, 0)
+
+
+def test_batch_list_many_launches(ctx, oracle_lib):
+    """More batches than one launch takes (48): 110 small batches of varied sizes,
+    plus the reverse order (the grid is sized by the largest batch)."""
+    rng = np.random.default_rng(55)
+    cases = []
+    for i in range(110):
+        n = int(rng.integers(0, 3000))
+        b = workloads.mixed(n, 0, 1500, seed=500 + i, len_seed=600 + i) if n else None
+        if b is None:
+            cases.append((np.zeros(16, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint32),
+                          np.zeros(0, np.uint32)))
+        else:
+            cases.append((b.payload, b.off, b.lens, oracle_lib.batch(b.payload, b.off, b.lens, threads=16)))
+    for order in (cases, cases[::-1]):
+        for i, (got, c) in enumerate(zip(_run_list(ctx, order), order)):
+            assert (got == c[3]).all(), (i, len(c[1]))
+
+
+def test_vring_trace_instance(ctx, oracle_lib):
+    """The diagnostics (trace) instance of the vring kernel computes the same CRCs
+    and fills one 8 x u64 record per wave."""
+    b = workloads.mixed(100_000, 0, 3000, seed=91, len_seed=92)
+    exp = oracle_lib.batch(b.payload, b.off, b.lens, threads=16)
+    tr = torch.zeros(256 * 16 * 8, dtype=torch.int64, device="cuda")
+    ctx.diag_trace(tr)
+    try:
+        for lanes in (4, 8):
+            tr.zero_()
+            assert (run_batch(ctx, b.payload, b.off, b.lens, lanes) == exp).all(), lanes
+            t = tr.cpu().numpy().view(np.uint64).reshape(-1, 8)
+            live = t[t[:, 0] > 0]
+            assert len(live) > 0 and (live[:, 5] >= live[:, 0]).all()
+            assert int(live[:, 7].sum()) == (len(b.off) + (64 // lanes) - 1) // (64 // lanes)
+    finally:
+        ctx.diag_trace(None)
+        ctx.set_tuning(0, 0)
+
+
+def test_all_empty_groups_every_path(ctx, oracle_lib):
+    """Groups whose packets are all empty (a stage count of zero before the
+    clamp): a lone empty packet, a batch of empty packets, and runs of empty
+    packets amid others -- every lane count, the default and direct paths, and
+    every stream geometry."""
+    rng = np.random.default_rng(66)
+    lens = rng.integers(0, 300, size=4000).astype(np.uint32)
+    lens[100:300] = 0                          # empty runs longer than any group
+    lens[1000:1064] = 0
+    lens[-70:] = 0                             # the batch ends in empty groups
+    off = np.zeros(len(lens), np.uint64)
+    np.cumsum(lens[:-1].astype(np.uint64), out=off[1:])
+    payload = rng.integers(0, 256, size=int(lens.astype(np.uint64).sum()) + 16, dtype=np.uint8)
+    exp = oracle_lib.batch(payload, off, lens, threads=8)
+    cases = [(np.zeros(16, np.uint8), np.zeros(1, np.uint64), np.zeros(1, np.uint32), np.zeros(1, np.uint32)),
+             (np.zeros(16, np.uint8), np.zeros(64, np.uint64), np.zeros(64, np.uint32), np.zeros(64, np.uint32)),
+             (payload, off, lens, exp)]
+    try:
+        for path in [0, 1] + [2 + g for g in range(N_STREAM_GEOMS)] + [17]:
+            ctx.set_kernel_path(path)
+            for lanes in (1, 2, 4, 8, 16, 32, 64):
+                for i, (p, o, l, e) in enumerate(cases):
+                    got = run_batch(ctx, p, o, l, lanes)
+                    assert (got == e).all(), (path, lanes, i, np.nonzero(got != e)[0][:5])
+    finally:
+        ctx.set_kernel_path(0)
+        ctx.set_tuning(0, 0)

@@ -9,7 +9,8 @@ once, so nothing may read or overwrite it before the wait that retires the load
 This is a dataflow analysis over the kernel's control-flow graph (hipcc -S
 output): the state at each point is the ordered list of VMEM operations that may
 still be in flight (the destination VGPRs of asm loads; other VMEM ops --
-compiler loads / stores, LDS-DMA, scratch -- count with no tracked registers).
+compiler loads, LDS-DMA, scratch loads -- count with no tracked registers;
+stores are not queued, since they may complete out of order with the loads).
 `s_waitcnt vmcnt(N)` keeps only the N youngest; at a join the lists are merged
 aligned at their youngest end (element-wise union), which over-approximates what
 may be in flight on any path.  Any instruction that names a register of an
@@ -59,7 +60,12 @@ def parse(lines):
         if in_asm and op.startswith("global_load") and "lds" not in op:
             kind = "aload"
         elif op.startswith(("global_", "buffer_", "scratch_", "flat_")):
-            kind = "vmem"
+            # a store (or an atomic without return) may complete out of order with
+            # the loads, so it is no younger op a wait can count on: not queued
+            # (loads return in order, so an in-flight load has every younger load
+            # still counted by vmcnt, whatever the stores do)
+            ret = "_load" in op or ("atomic" in op and " glc" in line + " ")
+            kind = "vmem" if ret else "other"
         elif op == "s_waitcnt" and "vmcnt" in line:
             kind = "wait"
         elif op.startswith("s_cbranch") or op == "s_branch":
@@ -158,12 +164,12 @@ def kernels(text):
                 cur = None
 
 
-def main(path, skip_trace=True):
+def main(path, skip_trace=False):
     errs, n = [], 0
     for name, body in kernels(open(path).read()):
-        # crc32_vring_kernel<LG, NB, WPE, TR, BIN>: skip the diagnostics (TR = 1) instance
-        targs = re.findall(r"ILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E", name)
-        if skip_trace and targs and targs[0][3] == "1":
+        # crc32_vring_kernel<LG, TR>: skip the diagnostics (TR = 1) instance if asked
+        targs = re.findall(r"ILi(\d+)ELi(\d+)E", name)
+        if skip_trace and targs and targs[0][1] == "1":
             continue
         n += 1
         errs += check(body, name)

@@ -25,9 +25,13 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rotate", type=int, default=5)
     ap.add_argument("--probe", action="store_true", help="also run the read probe")
+    ap.add_argument("--list", type=int, default=0, help="batches per launch (batch-list entry)")
+    ap.add_argument("--wgs", type=int, default=0)
     a = ap.parse_args()
     batches = bench.make_batches(a.config, a.rotate, 0)
-    eng = bench.GpuEngine(0, batches, a.lanes, 0)
+    eng = bench.GpuEngine(0, batches, a.lanes, a.wgs)
+    if a.list:
+        eng.set_list(a.list)
     eng.ctx.set_kernel_path(a.path)
     eng.ctx.diag_ablation(a.ablate)
     for i in range(a.reps):

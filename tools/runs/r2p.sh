@@ -1,0 +1,12 @@
+set -o pipefail
+# round 2: batch-list vring (fixed ring registers) -- parity, bench per-batch vs batch-list
+out=gpurun_out/r2p
+mkdir -p $out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+tools/gpu_step.sh 300 $out/pytest_new.log python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 120 --timeout-method thread -k "vring or batch_list or golden or cfg2" || exit 1
+grep -q " failed\|Error" $out/pytest_new.log && exit 1
+tools/gpu_step.sh 500 $out/pytest.log python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread || exit 1
+tools/gpu_step.sh 300 $out/bench_default.json python bench.py || exit 1
+tools/gpu_step.sh 300 $out/bench_list5.json python bench.py --list 5 --no-cpu-baseline || exit 1
+tools/gpu_step.sh 300 $out/bench_list5_s1.json python bench.py --list 5 --streams 1 --no-cpu-baseline || exit 1
+tools/gpu_step.sh 300 $out/bench_s1.json python bench.py --streams 1 --no-cpu-baseline || exit 1
