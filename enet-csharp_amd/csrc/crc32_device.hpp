@@ -228,7 +228,7 @@ __device__ __forceinline__ uint32_t wave_max_u(uint32_t v) {
     v = max(v, dpp<kDppRowMirror>(v));
     const uint32_t a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
     const uint32_t c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
-    return max(max(a, b), max(c, d));
+    return __builtin_amdgcn_readfirstlane(max(max(a, b), max(c, d)));   // an SGPR: uniform
 }
 __device__ __forceinline__ uint32_t wave_min_u(uint32_t v) {
     v = min(v, dpp<kDppQuadXor1>(v));
@@ -237,7 +237,7 @@ __device__ __forceinline__ uint32_t wave_min_u(uint32_t v) {
     v = min(v, dpp<kDppRowMirror>(v));
     const uint32_t a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
     const uint32_t c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
-    return min(min(a, b), min(c, d));
+    return __builtin_amdgcn_readfirstlane(min(min(a, b), min(c, d)));   // an SGPR: uniform
 }
 
 // Register after feeding the segment [sp, sp+len) from `reg`, with every block

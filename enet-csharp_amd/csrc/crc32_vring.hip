@@ -37,45 +37,68 @@ namespace enethip {
 
 constexpr int kVrW = 16;                                        // waves per workgroup
 constexpr uint32_t kVrStaging = kLdsTableBytes;                 // basis rows land after the image
-constexpr int kVrLds = kLdsTableBytes + kVrBasisRows * 256;
+// per wave, the metadata of the next group (LDS-DMA): 3 x 256 B -- lengths, then
+// the offsets' low and high dwords, lane l's at +4l
+constexpr uint32_t kVrMeta = kVrStaging + kVrBasisRows * 256;
+constexpr uint32_t kVrMetaWave = 3 * 256;
+constexpr int kVrLds = kVrMeta + kVrW * kVrMetaWave;             // 79.5 KiB: two workgroups per CU
+static_assert(2 * kVrLds <= 160 * 1024, "two workgroups per CU");
 
-// Global loads as inline asm into fixed registers, waited for by explicit
-// counted vmcnt.  The compiler's own wait insertion loses count across the loop's
-// group-switch branches and falls back to vmcnt(0) right after the next stage is
-// issued, which empties the ring; and a loaded value the compiler can see is one
-// it may copy while the load is still in flight.  So the loads write fixed
-// registers -- the ring slots v[44:51] and v[52:59], the metadata v[60:61]
-// (offset) and v62 (length) -- as asm the compiler knows only as clobbering them,
-// and a value exists for the compiler only as the output of the wait that retires
-// its load (an output pinned to that register).  Every load lists its registers
-// as clobbered, so a value is read out before its register is loaded again.  The
-// compiler does not know that a register is busy between a load and its wait:
-// the build checks, on the generated ISA, that no compiler instruction touches
-// one then (tools/isa_inflight_check.py, run by the Makefile).
+// Global loads as inline asm, waited for by explicit counted vmcnt.  The
+// compiler's own wait insertion loses count across the loop's group-switch
+// branches and falls back to vmcnt(0) right after the next stage is issued,
+// which empties the ring; and a loaded value the compiler can see is one it may
+// copy while the load is still in flight.  So the stage loads write fixed
+// registers -- ring slot 0 = v[48:55], slot 1 = v[56:63] -- that the compiler never
+// allocates (amdgpu_num_vgpr on the kernel) and knows only as clobbered by the
+// loads; the fold reads them in place after the wait (vr_shuffle_slot).  The
+// metadata goes to LDS by LDS-DMA (no registers) and is read after its wait.  The
+// build checks on the generated ISA that no compiler instruction touches a
+// register while a load into it may be in flight (tools/isa_inflight_check.py,
+// run by the Makefile).
 template <int SLOT>
 __device__ __forceinline__ void vr_issue_stage(uint64_t a0, uint64_t a1) {
     if constexpr (SLOT == 0)
-        asm volatile("global_load_dwordx4 v[44:47], %0, off\n\tglobal_load_dwordx4 v[48:51], %1, off"
-                     :: "v"(a0), "v"(a1) : "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51");
+        asm volatile("global_load_dwordx4 v[48:51], %0, off\n\tglobal_load_dwordx4 v[52:55], %1, off"
+                     :: "v"(a0), "v"(a1) : "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55");
     else
-        asm volatile("global_load_dwordx4 v[52:55], %0, off\n\tglobal_load_dwordx4 v[56:59], %1, off"
-                     :: "v"(a0), "v"(a1) : "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59");
+        asm volatile("global_load_dwordx4 v[56:59], %0, off\n\tglobal_load_dwordx4 v[60:63], %1, off"
+                     :: "v"(a0), "v"(a1) : "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63");
 }
-// the stage of SLOT once at most N younger loads are in flight
-template <int SLOT, int N>
-__device__ __forceinline__ void vr_wait_stage(u32x4& a, u32x4& b) {
-    if constexpr (SLOT == 0)
-        asm volatile("s_waitcnt vmcnt(%2)" : "={v[44:47]}"(a), "={v[48:51]}"(b) : "n"(N));
-    else
-        asm volatile("s_waitcnt vmcnt(%2)" : "={v[52:55]}"(a), "={v[56:59]}"(b) : "n"(N));
-}
-__device__ __forceinline__ void vr_issue_meta(uint64_t len_addr, uint64_t off_addr) {
-    asm volatile("global_load_dword v62, %0, off\n\tglobal_load_dwordx2 v[60:61], %1, off"
-                 :: "v"(len_addr), "v"(off_addr) : "v60", "v61", "v62");
-}
+// the stage of SLOT has landed once at most N younger loads are in flight (no
+// outputs: the fold reads the slot registers in place, vr_shuffle_slot)
 template <int N>
-__device__ __forceinline__ void vr_wait_meta(uint32_t& L, uint64_t& off) {
-    asm volatile("s_waitcnt vmcnt(%2)" : "={v62}"(L), "={v[60:61]}"(off) : "n"(N));
+__device__ __forceinline__ void vr_wait_stage() {
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
+}
+// a landed slot as values (the edge path, which masks them first)
+template <int SLOT>
+__device__ __forceinline__ void vr_read_stage(u32x4& a, u32x4& b) {
+    if constexpr (SLOT == 0)
+        asm volatile("" : "={v[48:51]}"(a), "={v[52:55]}"(b));
+    else
+        asm volatile("" : "={v[56:59]}"(a), "={v[60:63]}"(b));
+}
+// the lane's metadata, 3 dwords, into the wave's LDS area at `base` (M0-relative
+// LDS-DMA, lane l's dword at +4l); the LDS reads of the previous group's metadata
+// are complete first (lgkmcnt(0)), so the DMA cannot overtake them
+__device__ __forceinline__ void vr_issue_meta(uint64_t len_addr, uint64_t off_addr, uint32_t base) {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\t"
+                 "s_mov_b32 m0, %2\n\t"
+                 "global_load_lds_dword %0, off\n\t"
+                 "s_add_u32 m0, m0, 0x100\n\t"
+                 "global_load_lds_dword %1, off\n\t"
+                 "s_add_u32 m0, m0, 0x100\n\t"
+                 "global_load_lds_dword %3, off"             // (an instruction offset would move the LDS address too)
+                 :: "v"(len_addr), "v"(off_addr), "s"(base), "v"(off_addr + 4u) : "m0", "scc", "memory");
+}
+// the metadata once at most N younger loads are in flight
+template <int N>
+__device__ __forceinline__ void vr_wait_meta(uint32_t base, uint32_t lane, uint32_t& L, uint64_t& off) {
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
+    L = lds_load(base + 4u * lane);
+    off = static_cast<uint64_t>(lds_load(base + 256u + 4u * lane)) |
+          (static_cast<uint64_t>(lds_load(base + 512u + 4u * lane)) << 32);
 }
 // every load retired (the wave's exit: no load may land after it has ended)
 __device__ __forceinline__ void vr_drain() {
@@ -120,7 +143,7 @@ struct VrSched {
 __device__ __forceinline__ VrSched make_vr_sched(uint32_t lane) {
     const LaneSched a = make_sched(lane);
     VrSched s;
-    s.cl = col_byte(lane & 31u) * 0x01010101u;
+    s.cl = __builtin_amdgcn_perm(0u, col_byte(lane & 31u), 0u);   // the byte in all four (no multiply)
     s.sel0 = a.sel[0];
     s.hs = a.hs;
     return s;
@@ -148,24 +171,66 @@ __device__ __forceinline__ constexpr uint32_t vr_col_const() {
     return r;
 }
 
-// fold_block_lane (crc32_device.hpp) with at most 8 table lookups in flight:
-// groups of 4 lookups, group g+1 issued before group g is XOR-reduced, so the
-// kernel fits 64 VGPRs (32 waves per CU hide the LDS latency instead of ILP).
-__device__ __forceinline__ uint32_t vr_fold(uint32_t reg, u32x4 A, u32x4 B, const VrSched& s, uint32_t lane) {
-    const uint32_t a0 = __builtin_amdgcn_bitop3_b32(A.x, reg, s.hs, 0xB4);   // A ^ (reg & ~hs)
-    const uint32_t b0 = __builtin_amdgcn_bitop3_b32(B.x, reg, s.hs, 0x78);   // B ^ (reg & hs)
-    const uint32_t w[8] = {a0, A.y, A.z, A.w, b0, B.y, B.z, B.w};
-    // the dword-swap masks (make_sched's m1, m2) rebuilt per block from the lane
-    // id: two VALU ops instead of two VGPRs held across the loop (asm volatile, so
-    // the compiler cannot hoist them back out)
-    uint32_t m1, m2;
-    asm volatile("v_bfe_i32 %0, %1, 2, 1" : "=v"(m1) : "v"(lane));
-    asm volatile("v_bfe_i32 %0, %1, 3, 1" : "=v"(m2) : "v"(lane));
-    uint32_t x[8], d[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) x[q] = __builtin_amdgcn_bitop3_b32(w[q], w[q ^ 1], m1, 0xD8);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) d[q] = __builtin_amdgcn_bitop3_b32(x[q], x[q ^ 2], m2, 0xD8);
+// The fold's data preparation (fold_block_lane's first half, crc32_device.hpp):
+// the register XORed into the block's first dword (A.x, or B.x when the lane
+// takes the halves swapped: hs), then the two dword-swap rounds -- d[q] =
+// w[q ^ ((lane >> 2) & 3)] -- as bitwise selects by the lane's masks m1, m2.  One
+// asm block, so the 8 source dwords are read where they are (the slot registers
+// of vr_issue_stage, or any registers for the edge path's masked copy) and the
+// only live values are the 8 results and 2 temporaries.
+#define VR_SHUFFLE_ASM(S0, S1, S2, S3, S4, S5, S6, S7)                                            \
+    "v_bfe_i32 %[t0], %[lane], 4, 1\n\t"                      /* hs */                                \
+    "v_bitop3_b32 %[d0], " S0 ", %[reg], %[t0] bitop3:0xb4\n\t" /* w0 = A.x ^ (reg & ~hs) */        \
+    "v_bitop3_b32 %[d4], " S4 ", %[reg], %[t0] bitop3:0x78\n\t" /* w4 = B.x ^ (reg & hs) */         \
+    "v_bfe_i32 %[t0], %[lane], 2, 1\n\t"                      /* m1 */                                \
+    "v_bitop3_b32 %[d1], " S1 ", %[d0], %[t0] bitop3:0xd8\n\t" /* x1 = m1 ? w0 : w1 */              \
+    "v_bitop3_b32 %[d0], %[d0], " S1 ", %[t0] bitop3:0xd8\n\t" /* x0 = m1 ? w1 : w0 */              \
+    "v_bitop3_b32 %[d2], " S2 ", " S3 ", %[t0] bitop3:0xd8\n\t"                                       \
+    "v_bitop3_b32 %[d3], " S3 ", " S2 ", %[t0] bitop3:0xd8\n\t"                                       \
+    "v_bitop3_b32 %[d5], " S5 ", %[d4], %[t0] bitop3:0xd8\n\t"                                        \
+    "v_bitop3_b32 %[d4], %[d4], " S5 ", %[t0] bitop3:0xd8\n\t"                                        \
+    "v_bitop3_b32 %[d6], " S6 ", " S7 ", %[t0] bitop3:0xd8\n\t"                                       \
+    "v_bitop3_b32 %[d7], " S7 ", " S6 ", %[t0] bitop3:0xd8\n\t"                                       \
+    "v_bfe_i32 %[t0], %[lane], 3, 1\n\t"                      /* m2: d[q] = m2 ? x[q^2] : x[q] */    \
+    "v_bitop3_b32 %[t1], %[d0], %[d2], %[t0] bitop3:0xd8\n\t"                                         \
+    "v_bitop3_b32 %[d2], %[d2], %[d0], %[t0] bitop3:0xd8\n\t"                                         \
+    "v_mov_b32 %[d0], %[t1]\n\t"                                                                       \
+    "v_bitop3_b32 %[t1], %[d1], %[d3], %[t0] bitop3:0xd8\n\t"                                         \
+    "v_bitop3_b32 %[d3], %[d3], %[d1], %[t0] bitop3:0xd8\n\t"                                         \
+    "v_mov_b32 %[d1], %[t1]\n\t"                                                                       \
+    "v_bitop3_b32 %[t1], %[d4], %[d6], %[t0] bitop3:0xd8\n\t"                                         \
+    "v_bitop3_b32 %[d6], %[d6], %[d4], %[t0] bitop3:0xd8\n\t"                                         \
+    "v_mov_b32 %[d4], %[t1]\n\t"                                                                       \
+    "v_bitop3_b32 %[t1], %[d5], %[d7], %[t0] bitop3:0xd8\n\t"                                         \
+    "v_bitop3_b32 %[d7], %[d7], %[d5], %[t0] bitop3:0xd8\n\t"                                         \
+    "v_mov_b32 %[d5], %[t1]"
+#define VR_SHUFFLE_OUTS(d)                                                                        \
+    [d0] "=&v"(d[0]), [d1] "=&v"(d[1]), [d2] "=&v"(d[2]), [d3] "=&v"(d[3]), [d4] "=&v"(d[4]),    \
+        [d5] "=&v"(d[5]), [d6] "=&v"(d[6]), [d7] "=&v"(d[7]), [t0] "=&v"(t0), [t1] "=&v"(t1)
+
+template <int SLOT>
+__device__ __forceinline__ void vr_shuffle_slot(uint32_t reg, uint32_t lane, uint32_t (&d)[8]) {
+    uint32_t t0, t1;
+    if constexpr (SLOT == 0)
+        asm volatile(VR_SHUFFLE_ASM("v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55")
+                     : VR_SHUFFLE_OUTS(d) : [reg] "v"(reg), [lane] "v"(lane));
+    else
+        asm volatile(VR_SHUFFLE_ASM("v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63")
+                     : VR_SHUFFLE_OUTS(d) : [reg] "v"(reg), [lane] "v"(lane));
+}
+__device__ __forceinline__ void vr_shuffle(uint32_t reg, uint32_t lane, const u32x4& A, const u32x4& B,
+                                           uint32_t (&d)[8]) {
+    uint32_t t0, t1;
+    asm volatile(VR_SHUFFLE_ASM("%[a0]", "%[a1]", "%[a2]", "%[a3]", "%[b0]", "%[b1]", "%[b2]", "%[b3]")
+                 : VR_SHUFFLE_OUTS(d)
+                 : [reg] "v"(reg), [lane] "v"(lane), [a0] "v"(A.x), [a1] "v"(A.y), [a2] "v"(A.z), [a3] "v"(A.w),
+                   [b0] "v"(B.x), [b1] "v"(B.y), [b2] "v"(B.z), [b3] "v"(B.w));
+}
+
+// fold_block_lane's lookups (crc32_device.hpp) on the prepared dwords, at most 8
+// table lookups in flight: groups of 4, group g+1 issued before group g is
+// XOR-reduced (32 waves per CU hide the LDS latency instead of ILP).
+__device__ __forceinline__ uint32_t vr_lookups(const uint32_t (&d)[8], const VrSched& s) {
     uint32_t v[2][4];
     uint32_t acc = 0;
     auto issue = [&](auto gc) __attribute__((always_inline)) {
@@ -177,7 +242,10 @@ __device__ __forceinline__ uint32_t vr_fold(uint32_t reg, u32x4 A, u32x4 B, cons
     };
     auto reduce = [&](int g) __attribute__((always_inline)) {
         const uint32_t(&u)[4] = v[g & 1];
-        acc = xor3(acc, u[0], u[1]) ^ (u[2] ^ u[3]);
+        acc = xor3(xor3(acc, u[0], u[1]), u[2], u[3]);        // two 3-input XORs per 4 lookups
+        // (pinned here: sunk into the caller's "block in the window" branch, the
+        // XORs would keep all 32 lookups live at once)
+        asm volatile("" : "+v"(acc));
     };
     issue(std::integral_constant<int, 0>{});
     static_for<1, 8>([&](auto gc) __attribute__((always_inline)) {
@@ -197,12 +265,16 @@ __device__ __forceinline__ uint32_t vr_fold(uint32_t reg, u32x4 A, u32x4 B, cons
 // the start (metadata, table image) and the drain are paid once per launch.
 struct VrIt {
     uint32_t b, j, J;   // batch, the wave's group ordinal in it, the wave's share of it
+    uint32_t w;         // the wave's position in the batch's deal (VrBatch::rot)
 };
 
-// 64 VGPRs (8 waves per SIMD: two 16-wave workgroups per CU).
+// 64 VGPRs (8 waves per SIMD: two 16-wave workgroups per CU), of which the compiler
+// may allocate v0-v47 only: amdgpu_num_vgpr(N) limits it to 2N VGPRs on gfx950
+// (the unified VGPR/AGPR file doubles the request), so the ring registers
+// v48-v63 are reserved -- never allocated, still counted in the kernel's VGPRs.
 // TR = 1: the diagnostics instance that writes the per-wave trace.
 template <int LG, int TR = 0>
-__global__ void __launch_bounds__(64 * kVrW) __attribute__((amdgpu_waves_per_eu(8, 8)))
+__global__ void __launch_bounds__(64 * kVrW) __attribute__((amdgpu_waves_per_eu(8, 8), amdgpu_num_vgpr(24)))
 crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_t* trace) {
     constexpr uint32_t P = 1u << LG, kPk = 64u >> LG;
     // The lane id and everything derived from it (k, p, the fold's lane constants)
@@ -218,8 +290,13 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
     const uint64_t zero = reinterpret_cast<uint64_t>(tb.zero);
 
     // ---- the wave's group sequence over the batches (wave-uniform)
+    const uint32_t wv32 = static_cast<uint32_t>(wv), wt32 = static_cast<uint32_t>(wt);
+    auto wpos = [&](uint32_t b) __attribute__((always_inline)) -> uint32_t {
+        const uint32_t r = bl.b[b].rot;                      // < wt
+        return wv32 >= r ? wv32 - r : wv32 + wt32 - r;
+    };
     auto share = [&](uint32_t b) __attribute__((always_inline)) -> uint32_t {   // (no division in the kernel)
-        return bl.b[b].jq + (wv < bl.b[b].jr ? 1u : 0u);
+        return bl.b[b].jq + (wpos(b) < bl.b[b].jr ? 1u : 0u);
     };
     // the batches this wave has groups in (bit b), so that moving to the next one
     // is a bit scan: no loop inside the streaming loop
@@ -233,17 +310,19 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
         const uint32_t nbt = static_cast<uint32_t>(__builtin_ctzll(rest | (1ull << 63)));
         it.j = in_batch ? it.j + 1u : 0u;
         it.J = in_batch ? it.J : share(nbt);
+        it.w = in_batch ? it.w : wpos(nbt);
         it.b = in_batch ? it.b : nbt;
         return true;
     };
     auto group_base = [&](const VrIt& it) __attribute__((always_inline)) -> uint64_t {   // its first packet
-        return (wv + static_cast<uint64_t>(it.j) * wt) * kPk;
+        return (it.w + static_cast<uint64_t>(it.j) * wt) * kPk;
     };
     const bool any = live != 0u;
-    VrIt pit{0u, 0u, 0u};                                    // the producer's group
+    VrIt pit{0u, 0u, 0u, 0u};                                // the producer's group
     if (any) {
         pit.b = static_cast<uint32_t>(__builtin_ctzll(live));
         pit.J = share(pit.b);
+        pit.w = wpos(pit.b);
     }
     VrIt qit = pit;                                          // the group whose metadata is loaded
     bool qlive = any && advance(qit);
@@ -271,6 +350,7 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
     if (wave < static_cast<uint32_t>(kVrBasisRows))
         dma4(basis + static_cast<size_t>(LG == 2 ? 1 : 2) * kVrBasisDwords + 64u * wave + lane,
              kVrStaging + 256u * wave);
+    const uint32_t mbase = kVrMeta + kVrMetaWave * wave;      // the wave's metadata area
     uint32_t mL = 0;                                         // metadata (read out at group switches)
     uint64_t moff = 0;
     auto load_meta = [&](const VrIt& it) __attribute__((always_inline)) {
@@ -281,15 +361,18 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
         const uint64_t left = B.n - 1u - base;               // (uniform: scalar select, no VALU)
         const uint32_t q = min(lane_p(), left < 63u ? static_cast<uint32_t>(left) : 63u);
         vr_issue_meta(reinterpret_cast<uint64_t>(B.len + base) + 4u * q,
-                      reinterpret_cast<uint64_t>(B.off + base) + 8u * q);
+                      reinterpret_cast<uint64_t>(B.off + base) + 8u * q, mbase);
     };
-    load_meta(any ? pit : VrIt{0u, 0u, 0u});                 // (batch 0 exists: count >= 1)
-    vr_wait_meta<0>(mL, moff);                               // basis row and metadata have landed
+    load_meta(any ? pit : VrIt{0u, 0u, 0u, 0u});             // (batch 0 exists: count >= 1)
+    vr_wait_meta<0>(mbase, lane, mL, moff);                  // basis row and metadata have landed
     mark(1);
 
     // ---- producer: window of the group it loads, one stage ahead of the consumer
-    uint64_t pws = 0;                                        // window start (64-byte aligned)
-    uint32_t plz = 0, pe = 0;                                // packet bytes [plz, pe) of the window
+    // the window start (64-byte aligned) with the packet's first byte in it, plz,
+    // in the low 6 bits: one 64-bit register for both; pe = the packet's end
+    uint64_t pwl = 0;
+    uint32_t pe = 0;
+    auto plz = [&]() __attribute__((always_inline)) { return static_cast<uint32_t>(pwl) & 63u; };
     uint32_t pst = 0, pstages = 0;
     bool pdone = !any;
     auto producer_enter = [&]() __attribute__((always_inline)) {   // group pit; metadata in mL / moff
@@ -298,43 +381,58 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
         const uint32_t L = lane_p() < rem ? mL : 0u;
         const uint64_t a = reinterpret_cast<uint64_t>(B.bytes) + moff;
         const uint32_t lz = static_cast<uint32_t>(a) & 63u;
-        pws = a - lz;
-        plz = L ? lz : 0u;                                   // an empty packet: [0, 0)
-        pe = plz + L;
+        const uint32_t z = L ? lz : 0u;                      // an empty packet: [0, 0)
+        pwl = (a - lz) | z;
+        pe = z + L;
         const uint32_t nb = (pe + 31u) >> 5;
         pstages = max(1u, wave_max_u((nb + P - 1u) >> LG));
         pst = 0;
     };
-    // Every produce issues the same four loads -- the metadata of group qit (an L2
-    // hit but at group switches) and the stage's two pieces -- so every wait below
-    // has a fixed count.
-    auto produce = [&](auto slot_c) __attribute__((always_inline)) {
+    // A produce issues the stage's two pieces, preceded -- on a group's first stage,
+    // when a next group exists -- by that group's metadata (two loads), a whole
+    // group ahead of its use.  The wait for the previous stage (slot WS, WS < 0:
+    // none) follows in the same branch, counting the loads just issued (2, or 4
+    // with metadata): one issue-and-wait sequence per path, so the in-flight check
+    // sees each path's own count.
+    auto produce = [&](auto slot_c, auto ws_c) __attribute__((always_inline)) {
         constexpr uint32_t slot = decltype(slot_c)::value;
+        constexpr int WS = decltype(ws_c)::value;
         if (!pdone && pst == pstages) {
             if (qlive) {
-                // last produce's metadata loads are older than its two stage loads
-                // (and a store): at most those may still be in flight
-                vr_wait_meta<2>(mL, moff);
+                // group qit's metadata was issued before the last produce's two stage
+                // loads (on this group's first stage, or at the prologue): retired
+                // once at most those two are in flight (stores do not count: older)
+                vr_wait_meta<2>(mbase, lane, mL, moff);
                 pit = qit;
                 qlive = advance(qit);
                 producer_enter();
             } else {
                 pdone = true;
-                plz = pe = 0;                                // every piece reads the zero line
+                pwl &= ~63ull;                               // [0, 0): every piece reads the zero line
+                pe = 0;
             }
         }
-        load_meta(qit);                                      // (past the end: qit is the last group)
         const uint32_t q0 = 32u * (lane_k() + P * pst);
         const uint32_t hs16 = lane & 16u;                    // this lane takes the block's halves swapped
         const uint32_t a0 = q0 + hs16, a1 = q0 + 16u - hs16;
-        const uint64_t s0 = (a0 < pe && a0 + 16u > plz) ? pws + a0 : zero;
-        const uint64_t s1 = (a1 < pe && a1 + 16u > plz) ? pws + a1 : zero;
-        vr_issue_stage<slot>(s0, s1);
+        const uint32_t lz = plz();
+        const uint64_t ws = pwl & ~63ull;
+        const uint64_t s0 = (a0 < pe && a0 + 16u > lz) ? ws + a0 : zero;
+        const uint64_t s1 = (a1 < pe && a1 + 16u > lz) ? ws + a1 : zero;
+        const bool meta = (pst == 0u) & qlive & !pdone;     // (one branch, no short-circuit flow blocks)
+        if (meta) {
+            load_meta(qit);
+            vr_issue_stage<slot>(s0, s1);
+            if constexpr (WS >= 0) vr_wait_stage<4>();
+        } else {
+            vr_issue_stage<slot>(s0, s1);
+            if constexpr (WS >= 0) vr_wait_stage<2>();
+        }
         ++pst;
     };
     if (any) {
         producer_enter();
-        produce(std::integral_constant<uint32_t, 0>{});
+        produce(std::integral_constant<uint32_t, 0>{}, std::integral_constant<int, -1>{});
     }
 
     // ---- the table image, rebuilt in LDS while stage 0 is in flight.  Wave w
@@ -389,7 +487,7 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
     // Entered right after the producer has entered the same group (the producer
     // runs exactly one stage ahead), so pit / plz / pe are that group's.
     auto consumer_enter = [&]() __attribute__((always_inline)) {
-        clz = plz;
+        clz = plz();
         ce = pe;
         const uint64_t base = group_base(pit);
         cout = bl.b[pit.b].out + base;
@@ -407,15 +505,19 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
     auto iteration = [&](auto sc) __attribute__((always_inline)) {
         constexpr uint32_t S = decltype(sc)::value;
         lane = vr_lane();
-        produce(std::integral_constant<uint32_t, S ^ 1u>{});
-        u32x4 A, B;
-        vr_wait_stage<S, 4>(A, B);                           // stage S has landed (the next produce's 4 are younger)
+        produce(std::integral_constant<uint32_t, S ^ 1u>{}, std::integral_constant<int, static_cast<int>(S)>{});
+        uint32_t d[8];
         if (cs == nedge) {                                   // head / tail pieces: keep [clz, ce) only
+            u32x4 A, B;
+            vr_read_stage<S>(A, B);
             const uint32_t q0 = 32u * (lane_k() + P * cs);               // windows < 2 GiB: differences fit int32
             vr_edge_mask(A, B, make_vr_sched(lane).hs, static_cast<int32_t>(clz - q0), static_cast<int32_t>(ce - q0));
             nedge = next_edge(cs + 1u);
+            vr_shuffle(reg, lane, A, B, d);
+        } else {
+            vr_shuffle_slot<S>(reg, lane, d);
         }
-        const uint32_t nr = vr_fold(reg, A, B, make_vr_sched(lane), lane);
+        const uint32_t nr = vr_lookups(d, make_vr_sched(lane));
         reg = 32u * (lane_k() + P * cs) < ce ? nr : reg;            // the lane's block k + P cs is in the window
         if (++cs == cstages) {
             // lane k is o = (k - nb) mod P blocks past the window end: x^(-256 o)
@@ -500,16 +602,19 @@ int vring_launch_list(int lg, int max_wgs, hipStream_t st, const VrBatches& bl, 
         if (bl.b[b].n) a.b[a.count++] = bl.b[b];
     if (a.count == 0) return 0;
     const uint64_t kpk = 64u >> lg;
-    uint64_t groups = 0;                                     // the largest batch sets the grid
-    for (uint32_t b = 0; b < a.count; ++b) groups = std::max<uint64_t>(groups, (a.b[b].n + kpk - 1u) / kpk);
+    uint64_t groups = 0;                                     // all batches' groups set the grid
+    for (uint32_t b = 0; b < a.count; ++b) groups += (a.b[b].n + kpk - 1u) / kpk;
     const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(
         1, std::min<uint64_t>((groups + kVrW - 1) / kVrW, static_cast<uint64_t>(max_wgs))));
     const uint64_t waves = static_cast<uint64_t>(grid) * kVrW;
+    uint64_t dealt = 0;
     for (uint32_t b = 0; b < a.count; ++b) {
         const uint64_t g = (a.b[b].n + kpk - 1u) / kpk;
         if (g / waves > 0xFFFFFFFFull) return -static_cast<int>(hipErrorInvalidValue);
         a.b[b].jq = static_cast<uint32_t>(g / waves);
         a.b[b].jr = static_cast<uint32_t>(g % waves);
+        a.b[b].rot = static_cast<uint32_t>(dealt % waves);
+        dealt += g;
     }
     void* args[] = {&a, const_cast<KernelTables*>(&tb), const_cast<const uint32_t**>(&basis2), &trace};
     const hipError_t e = hipLaunchKernel(vring_pick(lg, trace != nullptr), dim3(grid), dim3(64 * kVrW), args, kVrLds, st);

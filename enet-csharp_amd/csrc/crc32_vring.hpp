@@ -22,8 +22,11 @@ struct VrBatch {
     uint32_t* out;
     uint64_t n;
     // set by vring_launch_list: the batch's G = ceil(n / packets per group) groups
-    // as G = jq * waves + jr over the launch's waves (wave w takes jq + (w < jr))
-    uint32_t jq, jr;
+    // as G = jq * waves + jr over the launch's waves, dealt from wave rot on (the
+    // running group count of the batches before it, mod waves): wave w has position
+    // w' = (w - rot) mod waves in the batch, takes groups w', w' + waves, ... --
+    // jq + (w' < jr) of them -- so short batches fill the waves the ones before left
+    uint32_t jq, jr, rot, pad;
 };
 // Kernel-argument block (<= 4 KiB): up to kVrMaxBatches batches per launch.
 constexpr int kVrMaxBatches = 48;
