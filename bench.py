@@ -40,16 +40,19 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--rotate", type=int, default=5, help="distinct resident batches cycled through")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per packet (0 = library default)")
-    ap.add_argument("--wgs", type=int, default=0, help="workgroups per CU (0 = library default)")
+    ap.add_argument("--wgs", type=int, default=2, help="workgroups per CU (enet_hip_set_tuning; 0 = library default)")
     ap.add_argument("--streams", type=int, default=6,
                     help="HIP streams the captured steps rotate over: batches are independent, so a "
                          "launch's prologue overlaps the previous launch's tail (1 = serial)")
     ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "small"],
                     help="cfg2 = the metric's workload; cfg3 = mixed lengths; small = harness tests only")
-    ap.add_argument("--list", type=int, default=0,
-                    help="batches per launch through enet_hip_crc32_batch_list_device (0 = one "
-                         "enet_hip_crc32_batch_device call per batch); a step is then one launch "
-                         "over that many distinct resident batches (<= --rotate)")
+    ap.add_argument("--list", type=int, default=5,
+                    help="consecutive steps (batches) checksummed per launch through "
+                         "enet_hip_crc32_batch_list_device (<= --rotate, so the batches of one launch "
+                         "are distinct); 0 = one enet_hip_crc32_batch_device call per step.  A step is "
+                         "always one pass over one batch")
+    ap.add_argument("--path", type=int, default=0,
+                    help="kernel path (enet_hip_set_kernel_path; 0 = the library default -- tuning sweeps only)")
     ap.add_argument("--binned", action="store_true",
                     help="length-binned entry (enet_hip_crc32_batch_device_binned): for mixed lengths (cfg3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -154,23 +157,28 @@ class GpuEngine:
                 self.ws[s.cuda_stream] = self.torch.zeros(nb, dtype=self.torch.uint8, device="cuda")
 
     def set_list(self, n: int):
-        if n > len(self.bufs):
-            raise SystemExit("bench.py: --list must not exceed --rotate (batches of one launch are distinct)")
-        self.list = n
+        self.list = min(n, len(self.bufs))    # the batches of one launch are distinct
 
-    def step_batches(self, i: int) -> list:
-        """Indices of the resident batches step i checksums."""
+    def launch_plan(self, steps: int) -> list:
+        """(first step, step count) of each launch covering steps 0 .. steps-1: one
+        step per launch, or --list consecutive steps per batch-list launch."""
+        per = self.list or 1
+        return [(i, min(per, steps - i)) for i in range(0, steps, per)]
+
+    def launch(self, first: int, count: int, stream=None):
+        """Checksum steps first .. first+count-1 (step i = resident batch i % rotate)."""
+        h = self.h if stream is None else stream.cuda_stream
         if self.list:
-            return [(i * self.list + t) % len(self.bufs) for t in range(self.list)]
-        return [i % len(self.bufs)]
+            bs = [self.bufs[(first + t) % len(self.bufs)] for t in range(count)]
+            self.ctx.crc32_batch_list_device([(x["payload"], x["off"], x["lens"], x["n"], x["out"]) for x in bs], h)
+        else:
+            for t in range(count):
+                self.step(first + t, stream)
 
     def step(self, i: int, stream=None):
         b = self.bufs[i % len(self.bufs)]
         h = self.h if stream is None else stream.cuda_stream
-        if self.list:
-            bs = [self.bufs[j] for j in self.step_batches(i)]
-            self.ctx.crc32_batch_list_device([(x["payload"], x["off"], x["lens"], x["n"], x["out"]) for x in bs], h)
-        elif self.binned:
+        if self.binned:
             w = self.ws[h]
             self.ctx.crc32_batch_device_binned(b["payload"], b["off"], b["lens"], b["n"], b["out"], w, w.numel(), h)
         else:
@@ -184,19 +192,20 @@ class GpuEngine:
         self.torch.cuda.synchronize()
 
     def capture(self, steps: int):
-        """Capture `steps` launches (rotating batches) into one HIP graph: the timed
-        region then replays it with one host call, so host launch overhead (Python +
-        ctypes) cannot starve the GPU.  Each graph node is one ordinary launch; step i
-        goes to stream i % len(streams) (independent batches: consecutive launches may
-        overlap at their boundary, every launch still checksums its whole batch)."""
+        """Capture the launches of `steps` steps (rotating batches) into one HIP graph:
+        the timed region then replays it with one host call, so host launch overhead
+        (Python + ctypes) cannot starve the GPU.  Each graph node is one ordinary
+        launch; launch k goes to stream k % len(streams) (independent batches:
+        consecutive launches may overlap at their boundary, every launch still
+        checksums all of its batches)."""
         torch = self.torch
         self.sync()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=self.stream):
             for s in self.streams[1:]:
                 s.wait_stream(self.stream)
-            for i in range(steps):
-                self.step(i, self.streams[i % len(self.streams)])
+            for k, (first, count) in enumerate(self.launch_plan(steps)):
+                self.launch(first, count, self.streams[k % len(self.streams)])
             for s in self.streams[1:]:
                 self.stream.wait_stream(s)
         self.sync()
@@ -298,6 +307,8 @@ def kernel_name(args) -> str:
     """The dominant kernel of the measured entry point (as rocprofv3 names it)."""
     lanes = args.lanes or 4
     lg = {4: 2, 8: 3}.get(lanes)
+    if getattr(args, "path", 0) and args.path != 17:
+        return f"kernel path {args.path}"
     if args.binned:
         return f"crc32_lean_kernel<0, {lg}, 16, 2, 128>"
     if lg is None:
@@ -324,13 +335,14 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
     eng = (engine_factory or GpuEngine)(local, batches, args.lanes, args.wgs)
     if hasattr(eng, "set_streams"):
         eng.set_streams(args.streams)
+    if args.path:
+        eng.ctx.set_kernel_path(args.path)
     if args.binned:
         eng.set_binned(True)
-    if args.list:
-        if args.binned:
-            raise SystemExit("bench.py: --list and --binned are separate entry points")
+    if args.list > 1 and not args.binned and hasattr(eng, "set_list"):   # (binned: one batch per launch)
         eng.set_list(args.list)
-    per_step = args.list or 1                 # batches one step checksums
+    plan = eng.launch_plan(args.steps) if hasattr(eng, "launch_plan") else [(i, 1) for i in range(args.steps)]
+    per_launch_steps = plan[0][1]             # steps (batches) one launch checksums
 
     # correctness gate (untimed): first resident batch vs the oracle
     eng.step(0)
@@ -341,8 +353,9 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
     if not (eng.outputs(0) == exp).all():
         raise SystemExit("bench.py: GPU CRCs differ from the oracle -- refusing to report a number")
 
-    for i in range(args.warmup):
-        eng.step(i)
+    for first, count in (eng.launch_plan(args.warmup) if hasattr(eng, "launch_plan") else
+                         [(i, 1) for i in range(args.warmup)]):
+        eng.launch(first, count) if hasattr(eng, "launch") else eng.step(first)
     if hasattr(eng, "capture"):
         eng.capture(args.steps)
         for bf in eng.bufs:               # one untimed replay (graph upload / warm), checked:
@@ -350,26 +363,29 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
         eng.replay()
         eng.sync()
         lib = oracle.OracleLib()
-        for j in range(min(args.steps * per_step, len(batches))):
+        for j in range(min(args.steps, len(batches))):
             ref = lib.batch(batches[j].payload, batches[j].off, batches[j].lens, threads=8)
             if not (eng.outputs(j) == ref).all():
                 raise SystemExit(f"bench.py: graph replay CRCs of batch {j} differ from the oracle")
+        eng.replay()                      # untimed again: the GPU idled through the oracle check
+        eng.sync()
         secs = timed_region(dist, eng.sync, 1, eng.replay)
     else:
-        secs = timed_region(dist, eng.sync, args.steps, eng.step)
+        secs = timed_region(dist, eng.sync, args.steps, eng.step)    # (engines without a graph)
     secs_max = max_over_ranks(dist, secs)
-    bytes_rank = float(sum(batches[i % len(batches)].payload_bytes for i in range(args.steps * per_step)))
+    bytes_rank = float(sum(batches[i % len(batches)].payload_bytes for i in range(args.steps)))
     bytes_all = sum_over_ranks(dist, bytes_rank)
     value = bytes_all / secs_max / GIB
 
     # per-launch kernel duration via HIP events on the launch stream (for the roofline)
     # (a) serial timed region, events at its two ends only -> roofline.achieved;
     # (b) each launch bracketed by its own event pair (median), reported beside it
-    nk = min(args.steps, 100)
-    r_ms = eng.region_ms(eng.step, nk)
-    k_ms, span_ms = eng.kernel_ms(eng.step, nk)
+    nk = min(len(plan), 100)
+    lfn = (lambda k: eng.launch(*plan[k])) if hasattr(eng, "launch") else eng.step
+    r_ms = eng.region_ms(lfn, nk)
+    k_ms, span_ms = eng.kernel_ms(lfn, nk)
     p_ms = eng.region_ms(eng.probe, nk)
-    per_launch = float(batches[0].payload_bytes) * per_step
+    per_launch = float(batches[0].payload_bytes) * sum(c for _, c in plan[:nk]) / nk
     probe_bytes = float((batches[0].payload.nbytes // 16) * 16)
     achieved = per_launch / (r_ms * 1e-3) / 1e9
     probe = probe_bytes / (p_ms * 1e-3) / 1e9
@@ -399,13 +415,15 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
                              "small": "small: 2048 packets x 1200 B (harness tests)"}[args.config] +
                             f", {args.rotate} rotating resident batches per GPU",
                 "packets_per_gpu": batches[0].n,
-                "payload_bytes_per_step": int(per_launch),
-                "batches_per_step": per_step,
+                "payload_bytes_per_step": int(batches[0].payload_bytes),
+                "steps_per_launch": per_launch_steps,
                 "parallelism": f"{ws} independent shards (no collective)",
                 "lanes_per_packet": args.lanes or "default",
                 "streams": args.streams,
                 "entry": ("enet_hip_crc32_batch_device_binned" if args.binned else
-                          "enet_hip_crc32_batch_list_device" if args.list else "enet_hip_crc32_batch_device"),
+                          "enet_hip_crc32_batch_list_device" if per_launch_steps > 1 else
+                          "enet_hip_crc32_batch_device"),
+                "workgroups_per_cu": args.wgs,
             },
             "hbm_read_frac": round(value * GIB / 1e9 / (HBM_PEAK_GBPS * ws), 4),
             "roofline": {
@@ -414,7 +432,8 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": (traffic or {}).get("hbm_bytes_per_launch"),
+                "traffic": (None if not (traffic or {}).get("hbm_bytes_per_batch") else
+                            round(traffic["hbm_bytes_per_batch"] * per_launch / float(batches[0].payload_bytes))),
                 "kernel": kernel_name(args),
                 "kernel_ms": round(r_ms, 5),
                 "kernel_ms_timing": f"HIP events around {nk} serial launches on the launch stream",

@@ -20,9 +20,13 @@
 //     folded).  A 16-byte piece wholly outside [lz, lz + L) is read from a zero
 //     line instead; a partly covered piece (a packet start or end off a 16-byte
 //     boundary) is masked on the fold side in a wave-uniform edge branch.
-//   * LDS holds only the 64 KiB table image (rebuilt per workgroup from a 2.5 KiB
-//     GF(2) basis while the first stage is in flight), so two 16-wave
-//     workgroups share a CU (32 waves; VGPRs capped at 64 per lane).
+//   * LDS holds the 64 KiB table image (rebuilt per workgroup from a 2.5 KiB
+//     GF(2) basis while the first stage is in flight) and each wave's 768-B
+//     metadata area (79.5 KiB), so two 16-wave workgroups share a CU (32 waves;
+//     64 VGPRs, of which v48-v63 are the ring).
+//   * One launch may cover a list of batches (enet_hip_crc32_batch_list_device):
+//     each batch's groups dealt over all waves, the launch's start and drain paid
+//     once for the list.
 // Measured design choices (tools/pipebench.hip, profiles/r02_*): 64-byte window
 // starts beat the end-aligned 16-byte windows of the lean kernel (every DMA run
 // then covers whole 64-byte sectors), and the register ring at 32 waves per CU
@@ -389,9 +393,9 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
         pst = 0;
     };
     // A produce issues the stage's two pieces, preceded -- on a group's first stage,
-    // when a next group exists -- by that group's metadata (two loads), a whole
+    // when a next group exists -- by that group's metadata (three LDS-DMA loads), a whole
     // group ahead of its use.  The wait for the previous stage (slot WS, WS < 0:
-    // none) follows in the same branch, counting the loads just issued (2, or 4
+    // none) follows in the same branch, counting the loads just issued (2, or 5
     // with metadata): one issue-and-wait sequence per path, so the in-flight check
     // sees each path's own count.
     auto produce = [&](auto slot_c, auto ws_c) __attribute__((always_inline)) {
@@ -423,7 +427,7 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
         if (meta) {
             load_meta(qit);
             vr_issue_stage<slot>(s0, s1);
-            if constexpr (WS >= 0) vr_wait_stage<4>();
+            if constexpr (WS >= 0) vr_wait_stage<5>();           // 3 metadata + 2 stage loads younger
         } else {
             vr_issue_stage<slot>(s0, s1);
             if constexpr (WS >= 0) vr_wait_stage<2>();

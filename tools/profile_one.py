@@ -34,8 +34,8 @@ def main():
         eng.set_list(a.list)
     eng.ctx.set_kernel_path(a.path)
     eng.ctx.diag_ablation(a.ablate)
-    for i in range(a.reps):
-        eng.step(i)
+    for first, count in eng.launch_plan(a.reps):          # --reps batches, --list per launch
+        eng.launch(first, count)
     if a.probe:
         for i in range(a.reps):
             eng.probe(i)

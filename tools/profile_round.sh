@@ -13,5 +13,5 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$out/bench_trace" -o run 
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$out/bench_s1_trace" -o run --output-format csv \
     -- python3 bench.py --steps 50 --warmup 10 --streams 1 --no-cpu-baseline > "$out/bench_s1_under_rocprof.json" 2> "$out/bench_s1_under_rocprof.err"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$out/fetch" -o run --output-format csv \
-    -- python3 tools/profile_one.py --reps 20 --probe > "$out/fetch.log" 2>&1
-python3 tools/traffic.py "$out/fetch" 78643200 "$out/traffic_cfg2.json"
+    -- python3 tools/profile_one.py --reps 20 --probe --list 5 --wgs 2 > "$out/fetch.log" 2>&1
+python3 tools/traffic.py "$out/fetch" 78643200 5 "$out/traffic_cfg2.json"

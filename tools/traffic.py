@@ -5,7 +5,7 @@ gfx950 reports 1/2 of the bytes of a wide coalesced streaming read, so
 bytes = FETCH_SIZE * 1024 * 2; the read-probe kernel (every payload byte read
 once, 16 B/lane) in the same pass calibrates the correction for this image.
 
-    python tools/traffic.py <pmc dir> <payload bytes per launch> [out.json]
+    python tools/traffic.py <pmc dir> <payload bytes per batch> <batches per launch> [out.json]
 """
 import csv
 import glob
@@ -15,8 +15,9 @@ from collections import defaultdict
 
 
 def main():
-    d, payload = sys.argv[1], float(sys.argv[2])
-    out = sys.argv[3] if len(sys.argv) > 3 else None
+    d, batch, per = sys.argv[1], float(sys.argv[2]), int(sys.argv[3])
+    payload = batch * per
+    out = sys.argv[4] if len(sys.argv) > 4 else None
     vals = defaultdict(list)
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
@@ -28,14 +29,16 @@ def main():
     res = {k: sum(v) / len(v) for k, v in vals.items()}
     stream = res.get("stream")
     probe = res.get("probe")
-    probe_bytes = (int(payload) // 16) * 16
+    probe_bytes = (int(batch) // 16) * 16                 # the probe reads one batch
     doc = {
         "source": "rocprofv3 --pmc FETCH_SIZE (own pass), tools/profile_one.py --probe",
         "correction": "bytes = FETCH_SIZE[KiB] * 1024 * 2 (gfx950 streaming-read 1/2 tally)",
         "fetch_size_kib_stream": stream,
         "fetch_size_kib_probe": probe,
         "payload_bytes_per_launch": payload,
+        "batches_per_launch": per,
         "hbm_bytes_per_launch": None if stream is None else round(stream * 2048),
+        "hbm_bytes_per_batch": None if stream is None else round(stream * 2048 / per),
         "probe_bytes_per_launch": None if probe is None else round(probe * 2048),
         "probe_calibration": None if probe is None else round(probe * 2048 / probe_bytes, 4),
         "traffic_over_algorithmic": None if stream is None else round(stream * 2048 / payload, 4),
