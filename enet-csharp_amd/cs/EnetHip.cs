@@ -38,6 +38,17 @@ namespace enet
         }
     }
 
+    /// <summary>One batch of a batch-list call (include/enet_hip.h ENetHipBatch; device pointers).</summary>
+    [StructLayout(LayoutKind.Sequential)]
+    public unsafe struct ENetHipBatch
+    {
+        public byte* bytes;
+        public ulong* offsets;
+        public uint* lengths;
+        public nuint count;
+        public uint* output;
+    }
+
     [SuppressUnmanagedCodeSecurity]
     public static unsafe class EnetHipNative
     {
@@ -73,6 +84,10 @@ namespace enet
         [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
         public static extern int enet_hip_crc32_batch_device(IntPtr ctx, byte* bytes, ulong* offsets, uint* lengths,
                                                              nuint count, uint* output, IntPtr stream);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_crc32_batch_list_device(IntPtr ctx, ENetHipBatch* batches, nuint batchCount,
+                                                                  IntPtr stream);
 
         [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
         public static extern nuint enet_hip_binned_workspace_size(nuint count);
@@ -207,6 +222,12 @@ namespace enet
         public void BatchDevice(byte* bytes, ulong* offsets, uint* lengths, nuint count, uint* output, IntPtr stream = default)
             => EnetHip.Check("enet_hip_crc32_batch_device",
                 EnetHipNative.enet_hip_crc32_batch_device(Handle, bytes, offsets, lengths, count, output, stream));
+
+        /// <summary>Several device-resident batches in one launch per 48 (same results as one
+        /// BatchDevice call each; the launch's start and drain are paid once for the list).</summary>
+        public void BatchListDevice(ENetHipBatch* batches, nuint batchCount, IntPtr stream = default)
+            => EnetHip.Check("enet_hip_crc32_batch_list_device",
+                EnetHipNative.enet_hip_crc32_batch_list_device(Handle, batches, batchCount, stream));
 
         /// <summary>Device-resident batch of mixed lengths: records ordered by length per 1024-packet
         /// tile in <paramref name="workspace" /> (EnetHipNative.enet_hip_binned_workspace_size bytes),
