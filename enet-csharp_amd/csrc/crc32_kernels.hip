@@ -872,6 +872,7 @@ struct enet_hip_context {
     uint64_t* trace = nullptr;   // diagnostics: lean-kernel per-wave timeline
     int ablation_prio = 0;       // tuning: lean-kernel lagging-wave priority (diag_ablation mode 8)
     int ablation = 0;            // diagnostics: 1 = no lookups, 2 = no DMA (wrong CRCs by design)
+    int vr_abl = 0;              // diagnostics, vring batch lists: 1 = no edge masks, 2 = no lookups
     // staging for the host-memory entry points
     std::mutex mu;
     uint8_t* d_bytes = nullptr;
@@ -1088,6 +1089,8 @@ constexpr int kNumVStreamGeoms = std::tuple_size<VStreamGeoms>::value;
 // lean kernel geometries (crc32_lean.hip): paths kLeanPath0 + geom; path 0 runs geom 0
 constexpr int kLeanPath0 = 2 + kNumStreamGeoms + kNumVStreamGeoms;
 constexpr int kVringPath = kLeanPath0 + kLeanGeoms;     // crc32_vring.hip (path 0 for checksum batches)
+constexpr int kVringAltPath = kVringPath + 1;           // the same with the other stage-load cache policy
+constexpr bool kVringNt = false;                        // the default policy: nontemporal stage loads
 
 template <size_t I = 0>
 void launch_stream(int geom, int mode, int abl, int num_cus, uint64_t groups, hipStream_t st,
@@ -1140,6 +1143,10 @@ int setup_stream() {
 // vring workgroups per CU of one launch (enet_hip_set_tuning's workgroups_per_cu,
 // at most 2: the LDS and 64-VGPR budget of two 16-wave workgroups)
 int vring_wgs(const enet_hip_context* ctx) { return ctx->wgs_per_cu >= 2 ? 2 : 1; }
+bool vring_path(const enet_hip_context* ctx) {
+    return ctx->path == 0 || ctx->path == kVringPath || ctx->path == kVringAltPath;
+}
+bool vring_nt(const enet_hip_context* ctx) { return ctx->path == kVringAltPath ? !kVringNt : kVringNt; }
 
 int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStream_t st) {
     if (pa.n == 0) return 0;
@@ -1148,9 +1155,8 @@ int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStr
     const_cast<PacketArgs&>(pa).prio = static_cast<uint32_t>(ctx->ablation_prio);
     // the stream kernel takes 4, 8 or 16 lanes per packet; anything else runs direct
     // default (path 0) checksum batches at 4 or 8 lanes: the VGPR-ring kernel
-    if (mode == 0 && !pa.meta4 && (pa.lg == 2 || pa.lg == 3) && ctx->ablation == 0 &&
-        (ctx->path == 0 || ctx->path == kVringPath))
-        return vring_launch(pa.lg, ctx->num_cus * vring_wgs(ctx), st, pa, tb, ctx->d_basis2);
+    if (mode == 0 && !pa.meta4 && (pa.lg == 2 || pa.lg == 3) && ctx->ablation == 0 && vring_path(ctx))
+        return vring_launch(pa.lg, ctx->num_cus * vring_wgs(ctx), vring_nt(ctx), st, pa, tb, ctx->d_basis2);
     if (ctx->path != 1 && pa.lg >= 2 && pa.lg <= 4) {
         const bool lean_path = (ctx->path >= kLeanPath0 && ctx->path < kVringPath) || (ctx->path == 0 && ctx->ablation == 0);
         if (lean_path && pa.lg <= 3)
@@ -1284,8 +1290,9 @@ int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgro
 }
 
 int enet_hip_diag_ablation(enet_hip_context* ctx, int mode) {
-    if (!ctx || mode < 0 || mode > 2047) return -static_cast<int>(hipErrorInvalidValue);
+    if (!ctx || mode < 0 || mode > 131071) return -static_cast<int>(hipErrorInvalidValue);
     const int prio = (mode & 1024) ? 2 : (mode >> 3) & 1;    // 8: static / 1024: progress priority
+    ctx->vr_abl = (mode >> 11) & 63;                         // 2048 ... 65536: vring ablations
     mode &= 511;
     ctx->ablation = mode & ~8;
     ctx->ablation_prio = prio;
@@ -1299,7 +1306,7 @@ int enet_hip_diag_trace(enet_hip_context* ctx, uint64_t* deviceBuffer) {
 }
 
 int enet_hip_set_kernel_path(enet_hip_context* ctx, int path) {
-    if (!ctx || path < 0 || path > kVringPath) return -static_cast<int>(hipErrorInvalidValue);
+    if (!ctx || path < 0 || path > kVringAltPath) return -static_cast<int>(hipErrorInvalidValue);
     ctx->path = path;
     return 0;
 }
@@ -1332,14 +1339,15 @@ int enet_hip_crc32_batch_list_device(enet_hip_context* ctx, const ENetHipBatch* 
     ENH_CHECK(hipSetDevice(ctx->device));
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     const int lg = log2i(auto_lanes(ctx));
-    if ((lg == 2 || lg == 3) && ctx->ablation == 0 && (ctx->path == 0 || ctx->path == kVringPath)) {
+    if ((lg == 2 || lg == 3) && ctx->ablation == 0 && vring_path(ctx)) {
         const KernelTables tb = tables_of(ctx);
         for (size_t b0 = 0; b0 < batchCount; b0 += kVrMaxBatches) {
             VrBatches bl{};
             for (size_t b = b0; b < std::min(batchCount, b0 + kVrMaxBatches); ++b)
                 bl.b[bl.count++] = VrBatch{batches[b].bytes, batches[b].offsets, batches[b].lengths, batches[b].out,
                                            static_cast<uint64_t>(batches[b].count), 0u, 0u, 0u, 0u};
-            const int rc = vring_launch_list(lg, ctx->num_cus * vring_wgs(ctx), st, bl, tb, ctx->d_basis2, ctx->trace);
+            const int rc = vring_launch_list(lg, ctx->num_cus * vring_wgs(ctx), vring_nt(ctx), ctx->vr_abl, st, bl, tb,
+                                             ctx->d_basis2, ctx->trace);
             if (rc) return rc;
         }
         return 0;

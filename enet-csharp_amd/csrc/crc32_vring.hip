@@ -60,14 +60,30 @@ static_assert(2 * kVrLds <= 160 * 1024, "two workgroups per CU");
 // build checks on the generated ISA that no compiler instruction touches a
 // register while a load into it may be in flight (tools/isa_inflight_check.py,
 // run by the Makefile).
-template <int SLOT>
+// NT = 1: the loads carry the nontemporal cache policy (streamed once, not kept)
+#define VR_LOAD2(LO, HI, POL)                                                                  \
+    "global_load_dwordx4 v[" #LO "], %0, off" POL "\n\tglobal_load_dwordx4 v[" #HI "], %1, off" POL
+template <int SLOT, int NT>
 __device__ __forceinline__ void vr_issue_stage(uint64_t a0, uint64_t a1) {
-    if constexpr (SLOT == 0)
-        asm volatile("global_load_dwordx4 v[48:51], %0, off\n\tglobal_load_dwordx4 v[52:55], %1, off"
-                     :: "v"(a0), "v"(a1) : "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55");
-    else
-        asm volatile("global_load_dwordx4 v[56:59], %0, off\n\tglobal_load_dwordx4 v[60:63], %1, off"
-                     :: "v"(a0), "v"(a1) : "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63");
+    // NT: 0 = default policy, 1 = nt, 2 = sc1, 3 = sc0 sc1 (2, 3: tuning sweeps only)
+#define VR_ISSUE(LO, HI, POL, ...)                                                              \
+    asm volatile(VR_LOAD2(LO, HI, POL) :: "v"(a0), "v"(a1) : __VA_ARGS__)
+#define VR_SLOT0 "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55"
+#define VR_SLOT1 "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63"
+    if constexpr (SLOT == 0) {
+        if constexpr (NT == 0) VR_ISSUE(48:51, 52:55, "", VR_SLOT0);
+        else if constexpr (NT == 1) VR_ISSUE(48:51, 52:55, " nt", VR_SLOT0);
+        else if constexpr (NT == 2) VR_ISSUE(48:51, 52:55, " sc1", VR_SLOT0);
+        else VR_ISSUE(48:51, 52:55, " sc0 sc1", VR_SLOT0);
+    } else {
+        if constexpr (NT == 0) VR_ISSUE(56:59, 60:63, "", VR_SLOT1);
+        else if constexpr (NT == 1) VR_ISSUE(56:59, 60:63, " nt", VR_SLOT1);
+        else if constexpr (NT == 2) VR_ISSUE(56:59, 60:63, " sc1", VR_SLOT1);
+        else VR_ISSUE(56:59, 60:63, " sc0 sc1", VR_SLOT1);
+    }
+#undef VR_SLOT0
+#undef VR_SLOT1
+#undef VR_ISSUE
 }
 // the stage of SLOT has landed once at most N younger loads are in flight (no
 // outputs: the fold reads the slot registers in place, vr_shuffle_slot)
@@ -277,7 +293,12 @@ struct VrIt {
 // (the unified VGPR/AGPR file doubles the request), so the ring registers
 // v48-v63 are reserved -- never allocated, still counted in the kernel's VGPRs.
 // TR = 1: the diagnostics instance that writes the per-wave trace.
-template <int LG, int TR = 0>
+// ABL (diagnostics): bit 0 = no edge masking, bit 1 = no table lookups (the fold
+// XORs the prepared dwords) -- both wrong CRCs by design; bit 2 = each stage's
+// wait also retires the stage just issued (no load in flight during a fold); bit 3
+// = 128-byte window starts and line-shaped stage loads (wrong CRCs by design);
+// bit 4 = no end-of-packet corrections (wrong CRCs by design)
+template <int LG, int TR = 0, int NT = 0, int ABL = 0>
 __global__ void __launch_bounds__(64 * kVrW) __attribute__((amdgpu_waves_per_eu(8, 8), amdgpu_num_vgpr(24)))
 crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_t* trace) {
     constexpr uint32_t P = 1u << LG, kPk = 64u >> LG;
@@ -376,7 +397,8 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
     // in the low 6 bits: one 64-bit register for both; pe = the packet's end
     uint64_t pwl = 0;
     uint32_t pe = 0;
-    auto plz = [&]() __attribute__((always_inline)) { return static_cast<uint32_t>(pwl) & 63u; };
+    constexpr uint32_t kAln = (ABL & 8) ? 128u : 64u;         // window start alignment
+    auto plz = [&]() __attribute__((always_inline)) { return static_cast<uint32_t>(pwl) & (kAln - 1u); };
     uint32_t pst = 0, pstages = 0;
     bool pdone = !any;
     auto producer_enter = [&]() __attribute__((always_inline)) {   // group pit; metadata in mL / moff
@@ -384,7 +406,7 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
         const uint64_t rem = B.n - group_base(pit);          // packets of the batch from the group's first
         const uint32_t L = lane_p() < rem ? mL : 0u;
         const uint64_t a = reinterpret_cast<uint64_t>(B.bytes) + moff;
-        const uint32_t lz = static_cast<uint32_t>(a) & 63u;
+        const uint32_t lz = static_cast<uint32_t>(a) & (kAln - 1u);
         const uint32_t z = L ? lz : 0u;                      // an empty packet: [0, 0)
         pwl = (a - lz) | z;
         pe = z + L;
@@ -412,25 +434,27 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
                 producer_enter();
             } else {
                 pdone = true;
-                pwl &= ~63ull;                               // [0, 0): every piece reads the zero line
+                pwl &= ~static_cast<uint64_t>(kAln - 1u);     // [0, 0): every piece reads the zero line
                 pe = 0;
             }
         }
         const uint32_t q0 = 32u * (lane_k() + P * pst);
         const uint32_t hs16 = lane & 16u;                    // this lane takes the block's halves swapped
-        const uint32_t a0 = q0 + hs16, a1 = q0 + 16u - hs16;
+        // (ABL & 8, diagnostics: instruction j of a stage reads bytes 16 P j + 16 k)
+        const uint32_t a0 = (ABL & 8) ? 32u * P * pst + 16u * lane_k() : q0 + hs16;
+        const uint32_t a1 = (ABL & 8) ? a0 + 16u * P : q0 + 16u - hs16;
         const uint32_t lz = plz();
-        const uint64_t ws = pwl & ~63ull;
+        const uint64_t ws = pwl & ~static_cast<uint64_t>(kAln - 1u);
         const uint64_t s0 = (a0 < pe && a0 + 16u > lz) ? ws + a0 : zero;
         const uint64_t s1 = (a1 < pe && a1 + 16u > lz) ? ws + a1 : zero;
         const bool meta = (pst == 0u) & qlive & !pdone;     // (one branch, no short-circuit flow blocks)
         if (meta) {
             load_meta(qit);
-            vr_issue_stage<slot>(s0, s1);
-            if constexpr (WS >= 0) vr_wait_stage<5>();           // 3 metadata + 2 stage loads younger
+            vr_issue_stage<slot, NT>(s0, s1);
+            if constexpr (WS >= 0) vr_wait_stage<(ABL & 4) ? 0 : 5>();   // 3 metadata + 2 stage loads younger
         } else {
-            vr_issue_stage<slot>(s0, s1);
-            if constexpr (WS >= 0) vr_wait_stage<2>();
+            vr_issue_stage<slot, NT>(s0, s1);
+            if constexpr (WS >= 0) vr_wait_stage<(ABL & 4) ? 0 : 2>();
         }
         ++pst;
     };
@@ -515,13 +539,18 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
             u32x4 A, B;
             vr_read_stage<S>(A, B);
             const uint32_t q0 = 32u * (lane_k() + P * cs);               // windows < 2 GiB: differences fit int32
-            vr_edge_mask(A, B, make_vr_sched(lane).hs, static_cast<int32_t>(clz - q0), static_cast<int32_t>(ce - q0));
+            if constexpr (!(ABL & 1))
+                vr_edge_mask(A, B, make_vr_sched(lane).hs, static_cast<int32_t>(clz - q0), static_cast<int32_t>(ce - q0));
             nedge = next_edge(cs + 1u);
             vr_shuffle(reg, lane, A, B, d);
         } else {
             vr_shuffle_slot<S>(reg, lane, d);
         }
-        const uint32_t nr = vr_lookups(d, make_vr_sched(lane));
+        uint32_t nr;
+        if constexpr (ABL & 2)
+            nr = xor3(xor3(d[0], d[1], d[2]), xor3(d[3], d[4], d[5]), d[6] ^ d[7]);
+        else
+            nr = vr_lookups(d, make_vr_sched(lane));
         reg = 32u * (lane_k() + P * cs) < ce ? nr : reg;            // the lane's block k + P cs is in the window
         if (++cs == cstages) {
             // lane k is o = (k - nb) mod P blocks past the window end: x^(-256 o)
@@ -539,10 +568,11 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
                 x[b] = lds_load(__builtin_amdgcn_perm(reg, col, sel));
             }
             const uint32_t corr = xor3(x[0], x[1], x[2]) ^ x[3];
-            reg = o ? corr : reg;
+            if constexpr (!(ABL & 16)) reg = o ? corr : reg;
             reg = xor_lanes<0>(LG, reg);
             const uint32_t tz = nb ? 32u * nb - ce : 0u;
-            if (lane_k() == 0u && tz) reg = vr_mulmod(reg, lds_load(cinv_addr(tz)));
+            if constexpr (!(ABL & 16))
+                if (lane_k() == 0u && tz) reg = vr_mulmod(reg, lds_load(cinv_addr(tz)));
             if (lane_k() == 0u && lane_p() < crem) cout[lane_p()] = finalize(reg);   // packet.cs:159
             if (pdone) {
                 // no newer group entered: the wave is done.  The producer's last loads
@@ -569,34 +599,40 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
 
 // ---------------------------------------------------------------- host side
 
-template <int LG, int TR = 0>
+template <int LG, int TR = 0, int NT = 0, int ABL = 0>
 const void* vring_fn() {
-    return reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR>);
+    return reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR, NT, ABL>);
 }
 
-// The product instance: one workgroup per CU per launch, 64 VGPRs (WPE 8) so that
-// the next launch's workgroup -- overlapping batches on other streams -- can share
-// the CU while this one drains (bench: 4831 GiB/s at 59-62 VGPRs against 4438 at
-// 66, profiles/r02_*).  With a trace buffer: the same kernel writing per-wave
-// timestamps.  Measured and not kept: 3 and 4 ring slots, two workgroups of one
-// launch per CU, and a binned-records variant (its record register was copied by
-// hipcc between load and wait: tools/isa_inflight_check.py).
-const void* vring_pick(int lg, bool trace) {
-    if (trace) return lg == 2 ? vring_fn<2, 1>() : vring_fn<3, 1>();
-    return lg == 2 ? vring_fn<2>() : vring_fn<3>();
+// The product instances: 64 VGPRs (WPE 8), one or two workgroups per CU.  With a
+// trace buffer: the same kernel writing per-wave timestamps.  nt: the stage loads
+// with the nontemporal cache policy.  Measured and not kept: 3 and 4 ring slots and
+// a binned-records variant (its record register was copied by hipcc between load
+// and wait: tools/isa_inflight_check.py).
+const void* vring_pick(int lg, bool trace, bool nt, int abl) {
+    if (abl == 8 && lg == 3 && !trace) return nt ? vring_fn<3, 0, 1, 8>() : vring_fn<3, 0, 0, 8>();
+    if (abl == 19 && lg == 2 && !trace && !nt) return vring_fn<2, 0, 0, 19>();
+    if (abl == 27 && lg == 3 && !trace) return nt ? vring_fn<3, 0, 1, 27>() : vring_fn<3, 0, 0, 27>();
+    if (abl == 19 && lg == 3 && !trace && !nt) return vring_fn<3, 0, 0, 19>();
+    if (abl == 32 && lg == 2 && !trace) return nt ? vring_fn<2, 0, 3>() : vring_fn<2, 0, 2>();   // sc1 / sc0 sc1
+    if (abl && lg == 2 && !trace && !nt)
+        return abl == 1 ? vring_fn<2, 0, 0, 1>() : abl == 2 ? vring_fn<2, 0, 0, 2>() : abl == 3 ? vring_fn<2, 0, 0, 3>()
+               : abl == 4 ? vring_fn<2, 0, 0, 4>() : vring_fn<2, 0, 0, 6>();
+    if (trace) return lg == 2 ? (nt ? vring_fn<2, 1, 1>() : vring_fn<2, 1>()) : (nt ? vring_fn<3, 1, 1>() : vring_fn<3, 1>());
+    return lg == 2 ? (nt ? vring_fn<2, 0, 1>() : vring_fn<2>()) : (nt ? vring_fn<3, 0, 1>() : vring_fn<3>());
 }
 
 int vring_setup() {
     for (int lg = 2; lg <= 3; ++lg)
-        for (int t = 0; t < 2; ++t) {
-            const hipError_t e = hipFuncSetAttribute(vring_pick(lg, t == 1),
+        for (int t = 0; t < 256; ++t) {
+            const hipError_t e = hipFuncSetAttribute(vring_pick(lg, t & 1, (t >> 1) & 1, t >> 2),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, kVrLds);
             if (e != hipSuccess) return -static_cast<int>(e);
         }
     return 0;
 }
 
-int vring_launch_list(int lg, int max_wgs, hipStream_t st, const VrBatches& bl, const KernelTables& tb,
+int vring_launch_list(int lg, int max_wgs, bool nt, int abl, hipStream_t st, const VrBatches& bl, const KernelTables& tb,
                       const uint32_t* basis2, uint64_t* trace) {
     if ((lg != 2 && lg != 3) || bl.count > static_cast<uint32_t>(kVrMaxBatches))
         return -static_cast<int>(hipErrorInvalidValue);
@@ -621,18 +657,18 @@ int vring_launch_list(int lg, int max_wgs, hipStream_t st, const VrBatches& bl, 
         dealt += g;
     }
     void* args[] = {&a, const_cast<KernelTables*>(&tb), const_cast<const uint32_t**>(&basis2), &trace};
-    const hipError_t e = hipLaunchKernel(vring_pick(lg, trace != nullptr), dim3(grid), dim3(64 * kVrW), args, kVrLds, st);
+    const hipError_t e = hipLaunchKernel(vring_pick(lg, trace != nullptr, nt, abl), dim3(grid), dim3(64 * kVrW), args, kVrLds, st);
     return e == hipSuccess ? 0 : -static_cast<int>(e);
 }
 
-int vring_launch(int lg, int max_wgs, hipStream_t st, const PacketArgs& pa, const KernelTables& tb,
+int vring_launch(int lg, int max_wgs, bool nt, hipStream_t st, const PacketArgs& pa, const KernelTables& tb,
                  const uint32_t* basis2) {
     if (pa.meta4) return -static_cast<int>(hipErrorInvalidValue);   // binned records: the lean kernel
     if (pa.n == 0) return 0;
     VrBatches bl{};
     bl.count = 1;
     bl.b[0] = VrBatch{pa.bytes, pa.off, pa.len, pa.out, pa.n};
-    return vring_launch_list(lg, max_wgs, st, bl, tb, basis2, pa.trace);
+    return vring_launch_list(lg, max_wgs, nt, 0, st, bl, tb, basis2, pa.trace);
 }
 
 }  // namespace enethip

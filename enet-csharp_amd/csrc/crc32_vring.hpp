@@ -42,14 +42,15 @@ int vring_setup();
 
 // Launch over a list of batches (bl.count <= kVrMaxBatches): one launch, each batch
 // spread over the whole chip in turn, at most max_wgs 16-wave workgroups (the CU
-// count: one per CU; twice that: two).  trace = per-wave timestamps or null.
-int vring_launch_list(int lg, int max_wgs, hipStream_t st, const VrBatches& bl, const KernelTables& tb,
+// count: one per CU; twice that: two); nt = nontemporal stage loads;
+// abl = diagnostics ablation (0 in the product, crc32_vring.hip).  trace = per-wave timestamps or null.
+int vring_launch_list(int lg, int max_wgs, bool nt, int abl, hipStream_t st, const VrBatches& bl, const KernelTables& tb,
                       const uint32_t* basis2, uint64_t* trace);
 
 // Launch the vring kernel over one batch: checksum mode, lanes per packet 2^lg
 // (lg = 2 or 3), at most max_wgs workgroups.  basis2 = kVrBasisDwords per image (images for
 // P = 1, 4, 8, 16 in that order).  Returns 0 or -hipError_t.
-int vring_launch(int lg, int max_wgs, hipStream_t st, const PacketArgs& pa, const KernelTables& tb,
+int vring_launch(int lg, int max_wgs, bool nt, hipStream_t st, const PacketArgs& pa, const KernelTables& tb,
                  const uint32_t* basis2);
 
 }  // namespace enethip

@@ -234,7 +234,16 @@ ENET_HIP_API int enet_hip_read_probe_device(enet_hip_context* ctx, const uint8_t
 /* ---- diagnostics: roofline ablation of the stream kernel ----
  * 0 = normal; 1 = skip the table lookups (memory path alone); 2 = skip the
  * LDS-DMA (compute path alone).  Modes 1 and 2 produce WRONG checksums by
- * design and exist only to price the two halves of the kernel (tools/). */
+ * design and exist only to price the two halves of the kernel (tools/).
+ * Bits 2048 / 4096 price parts of the VGPR-ring kernel in batch-list launches
+ * at 4 lanes (2048: no head/tail masking, 4096: no table lookups), also WRONG
+ * checksums by design; 8192 (alone or with 4096): no load in flight during a
+ * fold (correct checksums); 16384 (alone, 8 lanes): 128-byte windows and
+ * line-shaped stage loads (WRONG checksums: the memory side alone);
+ * 2048 + 4096 + 32768 (4 lanes): no masks, lookups or end-of-packet
+ * corrections (WRONG checksums: the kernel's memory and control skeleton);
+ * 65536 (4 lanes, correct checksums): the stage loads with the sc1 (path 17)
+ * or sc0 sc1 (path 18) cache policy. */
 ENET_HIP_API int enet_hip_diag_ablation(enet_hip_context* ctx, int mode);
 
 /* ---- diagnostics: per-wave timeline of the lean stream kernel ----

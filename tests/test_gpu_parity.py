@@ -403,7 +403,7 @@ def test_vring_many_groups(ctx, oracle_lib):
     big = workloads.mixed(40_000, 2000, 9000, seed=179, len_seed=180)
     exp_b = oracle_lib.batch(big.payload, big.off, big.lens, threads=16)
     try:
-        for path in (0, 17):
+        for path in (0, 17, 18):               # 18: the other stage-load cache policy
             ctx.set_kernel_path(path)
             for lanes in (4, 8):
                 assert (run_batch(ctx, tiny.payload, tiny.off, tiny.lens, lanes) == exp_t).all(), ("tiny", path, lanes)
@@ -514,7 +514,7 @@ def test_all_empty_groups_every_path(ctx, oracle_lib):
              (np.zeros(16, np.uint8), np.zeros(64, np.uint64), np.zeros(64, np.uint32), np.zeros(64, np.uint32)),
              (payload, off, lens, exp)]
     try:
-        for path in [0, 1] + [2 + g for g in range(N_STREAM_GEOMS)] + [17]:
+        for path in [0, 1] + [2 + g for g in range(N_STREAM_GEOMS)] + [17, 18]:
             ctx.set_kernel_path(path)
             for lanes in (1, 2, 4, 8, 16, 32, 64):
                 for i, (p, o, l, e) in enumerate(cases):

@@ -1,0 +1,327 @@
+// streamprobe.hip -- measurement only: how fast can gfx950 stream-read a long
+// HBM-resident buffer, per access shape?  The achievable line for long batch-list
+// launches of the CRC kernel.  Every kernel XOR-reduces what it
+// reads into a never-taken sink store, so no load is dead.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// grid-stride, 16 B per lane, U loads in flight per lane
+template <int U, bool NT>
+__global__ void __launch_bounds__(256) sp_stride(const u32x4* p, uint64_t nvec, uint32_t* sink) {
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256u;
+    uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
+    for (; i + (U - 1) * stride < nvec; i += U * stride) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(p + i + u * stride) : p[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc ^= v[u];
+    }
+    for (; i < nvec; i += stride) acc ^= p[i];
+    const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+    if (x == 0x9E3779B9u) sink[0] = x;
+}
+
+// persistent, one contiguous chunk per workgroup (1024 threads): per iteration
+// each wave reads U consecutive KiB, the workgroup 16 U KiB
+template <int U, bool NT>
+__global__ void __launch_bounds__(1024) sp_chunk(const u32x4* p, uint64_t nvec, uint32_t* sink) {
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    const uint64_t per = (nvec + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = per * blockIdx.x, hi = lo + per < nvec ? lo + per : nvec;
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    uint64_t i = lo + static_cast<uint64_t>(wave) * 64u * U + lane;
+    const uint64_t step = 16u * 64u * U;
+    for (; i + 64u * (U - 1) < hi; i += step) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(p + i + 64u * u) : p[i + 64u * u];
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc ^= v[u];
+    }
+    for (; i < hi; i += 64u) acc ^= p[i];
+    const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+    if (x == 0x9E3779B9u) sink[0] = x;
+}
+
+// packet-shaped: the vring kernel's load pattern without the fold -- 16 packets
+// of L bytes per wave, 4 lanes per packet, lane k reading 32-byte block
+// k + 4 s of its packet per stage s, as two 16-byte loads; groups dealt
+// round-robin over all waves of a persistent grid (16-wave workgroups).
+// Depth D stages in flight.
+template <int D, bool NT = false>
+__global__ void __launch_bounds__(1024) sp_packets(const uint8_t* bytes, uint64_t npk, uint32_t L, uint32_t* sink) {
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    const uint32_t lane = threadIdx.x & 63u, k = lane & 3u, pk = lane >> 2;
+    const uint64_t wv = static_cast<uint64_t>(blockIdx.x) * 16u + (threadIdx.x >> 6);
+    const uint64_t wt = static_cast<uint64_t>(gridDim.x) * 16u;
+    const uint64_t groups = (npk + 15u) / 16u;
+    const uint32_t stages = (L + 127u) / 128u;
+    for (uint64_t g = wv; g < groups; g += wt) {
+        const uint64_t pidx = g * 16u + pk;
+        const uint8_t* base = bytes + (pidx < npk ? pidx : npk - 1u) * L;
+        const uint64_t a = reinterpret_cast<uint64_t>(base) & ~63ull;
+        for (uint32_t s = 0; s < stages; s += D) {
+            u32x4 v[2 * D];
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const uint32_t q = 32u * (k + 4u * (s + d));
+                const bool in = s + d < stages;
+                const u32x4* p0 = reinterpret_cast<const u32x4*>(a + q);
+                v[2 * d] = in ? (NT ? __builtin_nontemporal_load(p0) : *p0) : u32x4{0u, 0u, 0u, 0u};
+                v[2 * d + 1] = in ? (NT ? __builtin_nontemporal_load(p0 + 1) : p0[1]) : u32x4{0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (int d = 0; d < 2 * D; ++d) acc ^= v[d];
+        }
+    }
+    const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+    if (x == 0x9E3779B9u) sink[0] = x;
+}
+
+// packet-shaped, line-friendly: P lanes per packet, a stage = 32 P window bytes
+// read as two instructions of 16 P contiguous bytes per packet (instruction j,
+// lane k: bytes 16 P j + 16 k of the stage), so each instruction consumes whole
+// 64-B (P = 4) or 128-B (P >= 8) pieces of a line.  Windows start at the ALIGN
+// boundary at or before the packet; 16-B pieces wholly outside the packet read a
+// zero line instead (as the CRC kernel does).
+template <int P, int ALIGN, bool NT>
+__global__ void __launch_bounds__(1024) sp_lines(const uint8_t* bytes, uint64_t npk, uint32_t L, const uint8_t* zero,
+                                                 uint32_t* sink) {
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    constexpr uint32_t PK = 64 / P;
+    const uint32_t lane = threadIdx.x & 63u, k = lane % P, pk = lane / P;
+    const uint64_t wv = static_cast<uint64_t>(blockIdx.x) * 16u + (threadIdx.x >> 6);
+    const uint64_t wt = static_cast<uint64_t>(gridDim.x) * 16u;
+    const uint64_t groups = (npk + PK - 1) / PK;
+    for (uint64_t g = wv; g < groups; g += wt) {
+        const uint64_t pidx = g * PK + pk;
+        const uint64_t base = reinterpret_cast<uint64_t>(bytes) + (pidx < npk ? pidx : npk - 1u) * L;
+        const uint32_t lz = static_cast<uint32_t>(base) & (ALIGN - 1u);
+        const uint64_t a = base - lz;
+        const uint32_t e = lz + L;
+        uint32_t st = (e + 32u * P - 1u) / (32u * P);
+        for (int o = 32; o >= 1; o >>= 1) st = max(st, static_cast<uint32_t>(__shfl_xor(static_cast<int>(st), o)));
+        for (uint32_t s = 0; s < st; ++s) {
+            const uint32_t q0 = 32u * P * s + 16u * k, q1 = q0 + 16u * P;
+            const u32x4* p0 = reinterpret_cast<const u32x4*>((q0 < e && q0 + 16u > lz) ? a + q0 : reinterpret_cast<uint64_t>(zero));
+            const u32x4* p1 = reinterpret_cast<const u32x4*>((q1 < e && q1 + 16u > lz) ? a + q1 : reinterpret_cast<uint64_t>(zero));
+            const u32x4 v0 = NT ? __builtin_nontemporal_load(p0) : *p0;
+            const u32x4 v1 = NT ? __builtin_nontemporal_load(p1) : *p1;
+            acc ^= v0 ^ v1;
+        }
+    }
+    const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+    if (x == 0x9E3779B9u) sink[0] = x;
+}
+
+// sp_lines plus a CRC-like fold per stage: 32 data-dependent LDS lookups per lane
+// per 32 bytes (the slicing-by-32 cost) from a 64 KiB LDS table, XOR-reduced.
+// PF = 1: the next stage's loads are issued before the current stage is folded.
+template <int P, int ALIGN, bool NT, int PF, int ZM = 0>
+__global__ void __launch_bounds__(1024) sp_fold(const uint8_t* bytes, uint64_t npk, uint32_t L, const uint8_t* zero,
+                                                uint32_t* sink) {
+    extern __shared__ uint32_t tab[];
+    for (uint32_t i = threadIdx.x; i < 16384u; i += 1024u) tab[i] = i * 0x9E3779B9u;
+    __syncthreads();
+    uint32_t acc = 0;
+    constexpr uint32_t PK = 64 / P;
+    const uint32_t lane = threadIdx.x & 63u, k = lane % P, pk = lane / P;
+    const uint32_t col = (lane & 31u) << 2;
+    const uint64_t wv = static_cast<uint64_t>(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t wt = static_cast<uint64_t>(gridDim.x) * (blockDim.x >> 6);
+    const uint64_t groups = (npk + PK - 1) / PK;
+    auto fold = [&](const u32x4& v0, const u32x4& v1) {
+        const uint32_t w[8] = {v0.x ^ acc, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        uint32_t r = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                r ^= tab[(__builtin_amdgcn_perm(w[q], col, 0x0C0C0000u | ((4u + b) << 8)) >> 2) & 16383u];
+        acc = r;
+    };
+    for (uint64_t g = wv; g < groups; g += wt) {
+        const uint64_t pidx = g * PK + pk;
+        const uint64_t base = reinterpret_cast<uint64_t>(bytes) + (pidx < npk ? pidx : npk - 1u) * L;
+        const uint32_t lz = static_cast<uint32_t>(base) & (ALIGN - 1u);
+        const uint64_t a = base - lz;
+        const uint32_t e = lz + L;
+        uint32_t st = (e + 32u * P - 1u) / (32u * P);
+        for (int o = 32; o >= 1; o >>= 1) st = max(st, static_cast<uint32_t>(__shfl_xor(static_cast<int>(st), o)));
+        auto ld = [&](uint32_t s, u32x4& v0, u32x4& v1) {
+            const uint32_t q0 = 32u * P * s + 16u * k, q1 = q0 + 16u * P;
+            const bool i0 = q0 < e && q0 + 16u > lz, i1 = q1 < e && q1 + 16u > lz;
+            if (ZM) {   // out-of-window pieces: no load at all (exec-masked), zero registers
+                v0 = u32x4{0u, 0u, 0u, 0u};
+                v1 = u32x4{0u, 0u, 0u, 0u};
+                if (i0) v0 = NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a + q0))
+                                : *reinterpret_cast<const u32x4*>(a + q0);
+                if (i1) v1 = NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a + q1))
+                                : *reinterpret_cast<const u32x4*>(a + q1);
+                return;
+            }
+            const u32x4* p0 = reinterpret_cast<const u32x4*>(i0 ? a + q0 : reinterpret_cast<uint64_t>(zero));
+            const u32x4* p1 = reinterpret_cast<const u32x4*>(i1 ? a + q1 : reinterpret_cast<uint64_t>(zero));
+            v0 = NT ? __builtin_nontemporal_load(p0) : *p0;
+            v1 = NT ? __builtin_nontemporal_load(p1) : *p1;
+        };
+        if (PF) {
+            u32x4 c0, c1;
+            ld(0, c0, c1);
+            for (uint32_t s = 0; s < st; ++s) {
+                u32x4 n0 = c0, n1 = c1;
+                if (s + 1 < st) ld(s + 1, n0, n1);
+                fold(c0, c1);
+                c0 = n0;
+                c1 = n1;
+            }
+        } else {
+            for (uint32_t s = 0; s < st; ++s) {
+                u32x4 v0, v1;
+                ld(s, v0, v1);
+                fold(v0, v1);
+            }
+        }
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
+// sp_chunk plus the same fold cost per 16 B (16 LDS lookups per lane-piece):
+// the linear stream with compute beside it.
+template <int U, bool NT>
+__global__ void __launch_bounds__(1024) sp_chunkfold(const u32x4* p, uint64_t nvec, uint32_t* sink) {
+    extern __shared__ uint32_t tab[];
+    for (uint32_t i = threadIdx.x; i < 16384u; i += 1024u) tab[i] = i * 0x9E3779B9u;
+    __syncthreads();
+    uint32_t acc = 0;
+    const uint32_t col = (threadIdx.x & 31u) << 2;
+    const uint64_t per = (nvec + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = per * blockIdx.x, hi = lo + per < nvec ? lo + per : nvec;
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    uint64_t i = lo + static_cast<uint64_t>(wave) * 64u * U + lane;
+    const uint64_t step = 16u * 64u * U;
+    for (; i + 64u * (U - 1) < hi; i += step) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(p + i + 64u * u) : p[i + 64u * u];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t w[4] = {v[u].x ^ acc, v[u].y, v[u].z, v[u].w};
+            uint32_t r = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    r ^= tab[(__builtin_amdgcn_perm(w[q], col, 0x0C0C0000u | ((4u + b) << 8)) >> 2) & 16383u];
+            acc = r;
+        }
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
+extern "C" {
+
+static int sp_attr() {
+    static int done = 0;
+    if (!done) {
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_fold<8, 64, false, 0>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_fold<8, 64, false, 1>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_fold<8, 128, true, 0>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_fold<8, 128, true, 1>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_fold<4, 64, false, 0>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_fold<4, 64, false, 1>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_chunkfold<2, false>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_chunkfold<2, true>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_chunkfold<4, false>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_chunkfold<4, true>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_fold<8, 128, true, 0, 1>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_fold<8, 64, false, 0, 1>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_fold<16, 128, true, 0, 1>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        done = 1;
+    }
+    return 0;
+}
+
+int sp_ncfg() { return 42; }
+
+const char* sp_name(int cfg) {
+    static const char* n[] = {"stride U4 g2048x256",   "stride U8 g2048x256",   "stride U4 nt g2048x256",
+                              "stride U4 g8192x256",   "chunk U4 g256x1024",    "chunk U4 g512x1024",
+                              "chunk U8 g512x1024",    "chunk U4 nt g512x1024", "chunk U2 g512x1024",
+                              "packets D1 g512x1024",  "packets D2 g512x1024",  "packets D1 g256x1024",
+                              "packets D1 nt g512x1024", "packets D1 nt g256x1024",
+                              "lines P4 a64 g256",     "lines P4 a64 nt g256",  "lines P4 a64 g512",
+                              "lines P4 a64 nt g512",  "lines P8 a64 g256",     "lines P8 a64 nt g256",
+                              "lines P8 a128 g256",    "lines P8 a128 nt g256", "lines P8 a128 nt g512",
+                              "lines P16 a128 g256",   "lines P16 a128 nt g256", "lines P4 a128 nt g256",
+                              "fold P8 a64 g256",      "fold P8 a64 pf g256",   "fold P8 a128 nt g256",
+                              "fold P8 a128 nt pf g256", "fold P8 a64 g512",    "fold P8 a64 pf g512",
+                              "fold P4 a64 g512",      "fold P4 a64 pf g512",
+                              "chunkfold U2 g512",     "chunkfold U2 nt g512",  "chunkfold U4 g256",
+                              "chunkfold U4 nt g256",  "fold P8 a128 nt zm g512", "fold P8 a128 nt zm g256",
+                              "fold P8 a64 zm g512",   "fold P16 a128 nt zm g512"};
+    return cfg >= 0 && cfg < 42 ? n[cfg] : "?";
+}
+
+// nbytes: multiple of 16; for the packet shapes, npk packets of L bytes back to back
+int sp_run(int cfg, const void* buf, uint64_t nbytes, uint32_t L, const void* zero, uint32_t* sink, void* stream) {
+    const uint8_t* b8 = static_cast<const uint8_t*>(buf);
+    const uint8_t* z8 = static_cast<const uint8_t*>(zero);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    sp_attr();
+    const u32x4* p = static_cast<const u32x4*>(buf);
+    const uint64_t nvec = nbytes / 16;
+    const uint64_t npk = nbytes / L;
+    switch (cfg) {
+        case 0: sp_stride<4, false><<<2048, 256, 0, st>>>(p, nvec, sink); break;
+        case 1: sp_stride<8, false><<<2048, 256, 0, st>>>(p, nvec, sink); break;
+        case 2: sp_stride<4, true><<<2048, 256, 0, st>>>(p, nvec, sink); break;
+        case 3: sp_stride<4, false><<<8192, 256, 0, st>>>(p, nvec, sink); break;
+        case 4: sp_chunk<4, false><<<256, 1024, 0, st>>>(p, nvec, sink); break;
+        case 5: sp_chunk<4, false><<<512, 1024, 0, st>>>(p, nvec, sink); break;
+        case 6: sp_chunk<8, false><<<512, 1024, 0, st>>>(p, nvec, sink); break;
+        case 7: sp_chunk<4, true><<<512, 1024, 0, st>>>(p, nvec, sink); break;
+        case 8: sp_chunk<2, false><<<512, 1024, 0, st>>>(p, nvec, sink); break;
+        case 9: sp_packets<1><<<512, 1024, 0, st>>>(static_cast<const uint8_t*>(buf), npk, L, sink); break;
+        case 10: sp_packets<2><<<512, 1024, 0, st>>>(static_cast<const uint8_t*>(buf), npk, L, sink); break;
+        case 11: sp_packets<1><<<256, 1024, 0, st>>>(static_cast<const uint8_t*>(buf), npk, L, sink); break;
+        case 12: sp_packets<1, true><<<512, 1024, 0, st>>>(static_cast<const uint8_t*>(buf), npk, L, sink); break;
+        case 13: sp_packets<1, true><<<256, 1024, 0, st>>>(static_cast<const uint8_t*>(buf), npk, L, sink); break;
+        case 14: sp_lines<4, 64, false><<<256, 1024, 0, st>>>(b8, npk, L, z8, sink); break;
+        case 15: sp_lines<4, 64, true><<<256, 1024, 0, st>>>(b8, npk, L, z8, sink); break;
+        case 16: sp_lines<4, 64, false><<<512, 1024, 0, st>>>(b8, npk, L, z8, sink); break;
+        case 17: sp_lines<4, 64, true><<<512, 1024, 0, st>>>(b8, npk, L, z8, sink); break;
+        case 18: sp_lines<8, 64, false><<<256, 1024, 0, st>>>(b8, npk, L, z8, sink); break;
+        case 19: sp_lines<8, 64, true><<<256, 1024, 0, st>>>(b8, npk, L, z8, sink); break;
+        case 20: sp_lines<8, 128, false><<<256, 1024, 0, st>>>(b8, npk, L, z8, sink); break;
+        case 21: sp_lines<8, 128, true><<<256, 1024, 0, st>>>(b8, npk, L, z8, sink); break;
+        case 22: sp_lines<8, 128, true><<<512, 1024, 0, st>>>(b8, npk, L, z8, sink); break;
+        case 23: sp_lines<16, 128, false><<<256, 1024, 0, st>>>(b8, npk, L, z8, sink); break;
+        case 24: sp_lines<16, 128, true><<<256, 1024, 0, st>>>(b8, npk, L, z8, sink); break;
+        case 25: sp_lines<4, 128, true><<<256, 1024, 0, st>>>(b8, npk, L, z8, sink); break;
+        case 26: sp_fold<8, 64, false, 0><<<256, 1024, 65536, st>>>(b8, npk, L, z8, sink); break;
+        case 27: sp_fold<8, 64, false, 1><<<256, 1024, 65536, st>>>(b8, npk, L, z8, sink); break;
+        case 28: sp_fold<8, 128, true, 0><<<256, 1024, 65536, st>>>(b8, npk, L, z8, sink); break;
+        case 29: sp_fold<8, 128, true, 1><<<256, 1024, 65536, st>>>(b8, npk, L, z8, sink); break;
+        case 30: sp_fold<8, 64, false, 0><<<512, 1024, 65536, st>>>(b8, npk, L, z8, sink); break;
+        case 31: sp_fold<8, 64, false, 1><<<512, 1024, 65536, st>>>(b8, npk, L, z8, sink); break;
+        case 32: sp_fold<4, 64, false, 0><<<512, 1024, 65536, st>>>(b8, npk, L, z8, sink); break;
+        case 33: sp_fold<4, 64, false, 1><<<512, 1024, 65536, st>>>(b8, npk, L, z8, sink); break;
+        case 34: sp_chunkfold<2, false><<<512, 1024, 65536, st>>>(p, nvec, sink); break;
+        case 35: sp_chunkfold<2, true><<<512, 1024, 65536, st>>>(p, nvec, sink); break;
+        case 36: sp_chunkfold<4, false><<<256, 1024, 65536, st>>>(p, nvec, sink); break;
+        case 37: sp_chunkfold<4, true><<<256, 1024, 65536, st>>>(p, nvec, sink); break;
+        case 38: sp_fold<8, 128, true, 0, 1><<<512, 1024, 65536, st>>>(b8, npk, L, z8, sink); break;
+        case 39: sp_fold<8, 128, true, 0, 1><<<256, 1024, 65536, st>>>(b8, npk, L, z8, sink); break;
+        case 40: sp_fold<8, 64, false, 0, 1><<<512, 1024, 65536, st>>>(b8, npk, L, z8, sink); break;
+        case 41: sp_fold<16, 128, true, 0, 1><<<512, 1024, 65536, st>>>(b8, npk, L, z8, sink); break;
+        default: return -1;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+}
