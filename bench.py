@@ -55,6 +55,9 @@ def parse(argv=None):
                     help="kernel path (enet_hip_set_kernel_path; 0 = the library default -- tuning sweeps only)")
     ap.add_argument("--binned", action="store_true",
                     help="length-binned entry (enet_hip_crc32_batch_device_binned): for mixed lengths (cfg3)")
+    ap.add_argument("--launch", default="graph", choices=["graph", "direct"],
+                    help="graph = the timed steps replayed from one captured HIP graph; direct = the same "
+                         "launches enqueued one by one inside the timed region")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget per CPU-baseline leg")
     return ap.parse_args(argv)
@@ -214,6 +217,15 @@ class GpuEngine:
     def replay(self, _i: int = 0):
         self.graph.replay()
 
+    def direct(self, steps: int):
+        """The captured launches, enqueued directly (same streams, same fork/join)."""
+        for s in self.streams[1:]:
+            s.wait_stream(self.stream)
+        for k, (first, count) in enumerate(self.launch_plan(steps)):
+            self.launch(first, count, self.streams[k % len(self.streams)])
+        for s in self.streams[1:]:
+            self.stream.wait_stream(s)
+
     def kernel_ms(self, fn, steps: int) -> tuple[float, float]:
         """HIP events on the launch stream: (mean per-launch kernel ms, span ms per
         step).  A spin kernel heads the queue so every event/launch pair is enqueued
@@ -369,7 +381,10 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
                 raise SystemExit(f"bench.py: graph replay CRCs of batch {j} differ from the oracle")
         eng.replay()                      # untimed again: the GPU idled through the oracle check
         eng.sync()
-        secs = timed_region(dist, eng.sync, 1, eng.replay)
+        if args.launch == "direct":
+            secs = timed_region(dist, eng.sync, 1, lambda _i: eng.direct(args.steps))
+        else:
+            secs = timed_region(dist, eng.sync, 1, eng.replay)
     else:
         secs = timed_region(dist, eng.sync, args.steps, eng.step)    # (engines without a graph)
     secs_max = max_over_ranks(dist, secs)
@@ -424,6 +439,7 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
                           "enet_hip_crc32_batch_list_device" if per_launch_steps > 1 else
                           "enet_hip_crc32_batch_device"),
                 "workgroups_per_cu": args.wgs,
+                "launch": args.launch,
             },
             "hbm_read_frac": round(value * GIB / 1e9 / (HBM_PEAK_GBPS * ws), 4),
             "roofline": {
