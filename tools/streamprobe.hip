@@ -224,6 +224,72 @@ __global__ void __launch_bounds__(1024) sp_chunkfold(const u32x4* p, uint64_t nv
     if (acc == 0x9E3779B9u) sink[0] = acc;
 }
 
+// Bursts: P lanes per packet (vring mapping: lane k's 32-byte blocks k + P s),
+// D stages of a packet loaded per burst (2 D loads per lane), the next burst
+// issued before the current one is folded (FOLD = 1: 32 LDS lookups per block)
+// or XORed (FOLD = 0).  Launched with W waves per workgroup, one workgroup per CU.
+template <int P, int D, int FOLD>
+__global__ void __launch_bounds__(1024) sp_burst(const uint8_t* bytes, uint64_t npk, uint32_t L, const uint8_t* zero,
+                                                 uint32_t* sink) {
+    extern __shared__ uint32_t tab[];
+    if (FOLD) {
+        for (uint32_t i = threadIdx.x; i < 16384u; i += blockDim.x) tab[i] = i * 0x9E3779B9u;
+        __syncthreads();
+    }
+    uint32_t acc = 0;
+    constexpr uint32_t PK = 64 / P;
+    const uint32_t lane = threadIdx.x & 63u, k = lane % P, pk = lane / P;
+    const uint32_t col = (lane & 31u) << 2;
+    const uint64_t wv = static_cast<uint64_t>(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t wt = static_cast<uint64_t>(gridDim.x) * (blockDim.x >> 6);
+    const uint64_t groups = (npk + PK - 1) / PK;
+    auto fold = [&](const u32x4& v0, const u32x4& v1) {
+        if (!FOLD) {
+            const u32x4 x = v0 ^ v1;
+            acc ^= x.x ^ x.y ^ x.z ^ x.w;
+            return;
+        }
+        const uint32_t w[8] = {v0.x ^ acc, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        uint32_t r = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                r ^= tab[(__builtin_amdgcn_perm(w[q], col, 0x0C0C0000u | ((4u + b) << 8)) >> 2) & 16383u];
+        acc = r;
+    };
+    for (uint64_t g = wv; g < groups; g += wt) {
+        const uint64_t pidx = g * PK + pk;
+        const uint64_t base = reinterpret_cast<uint64_t>(bytes) + (pidx < npk ? pidx : npk - 1u) * L;
+        const uint32_t lz = static_cast<uint32_t>(base) & 63u;
+        const uint64_t a = base - lz;
+        const uint32_t e = lz + L;
+        uint32_t st = (e + 32u * P - 1u) / (32u * P);
+        for (int o = 32; o >= 1; o >>= 1) st = max(st, static_cast<uint32_t>(__shfl_xor(static_cast<int>(st), o)));
+        const uint32_t nbu = (st + D - 1) / D;
+        auto ld = [&](uint32_t b, u32x4 (&v)[2 * D]) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const uint32_t q = 32u * (k + P * (b * D + d));
+                const bool i0 = q < e && q + 16u > lz, i1 = q + 16u < e && q + 32u > lz;
+                v[2 * d] = *reinterpret_cast<const u32x4*>(i0 ? a + q : reinterpret_cast<uint64_t>(zero));
+                v[2 * d + 1] = *reinterpret_cast<const u32x4*>(i1 ? a + q + 16u : reinterpret_cast<uint64_t>(zero));
+            }
+        };
+        u32x4 cur[2 * D];
+        ld(0, cur);
+        for (uint32_t b = 0; b < nbu; ++b) {
+            u32x4 nxt[2 * D];
+            if (b + 1 < nbu) ld(b + 1, nxt);
+#pragma unroll
+            for (int d = 0; d < D; ++d) fold(cur[2 * d], cur[2 * d + 1]);
+#pragma unroll
+            for (int d = 0; d < 2 * D; ++d) cur[d] = nxt[d];
+        }
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
 extern "C" {
 
 static int sp_attr() {
@@ -242,12 +308,16 @@ static int sp_attr() {
         hipFuncSetAttribute(reinterpret_cast<const void*>(sp_fold<8, 128, true, 0, 1>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
         hipFuncSetAttribute(reinterpret_cast<const void*>(sp_fold<8, 64, false, 0, 1>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
         hipFuncSetAttribute(reinterpret_cast<const void*>(sp_fold<16, 128, true, 0, 1>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_burst<4, 1, 1>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_burst<4, 2, 1>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_burst<4, 4, 1>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_burst<8, 2, 1>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
         done = 1;
     }
     return 0;
 }
 
-int sp_ncfg() { return 42; }
+int sp_ncfg() { return 54; }
 
 const char* sp_name(int cfg) {
     static const char* n[] = {"stride U4 g2048x256",   "stride U8 g2048x256",   "stride U4 nt g2048x256",
@@ -264,8 +334,12 @@ const char* sp_name(int cfg) {
                               "fold P4 a64 g512",      "fold P4 a64 pf g512",
                               "chunkfold U2 g512",     "chunkfold U2 nt g512",  "chunkfold U4 g256",
                               "chunkfold U4 nt g256",  "fold P8 a128 nt zm g512", "fold P8 a128 nt zm g256",
-                              "fold P8 a64 zm g512",   "fold P16 a128 nt zm g512"};
-    return cfg >= 0 && cfg < 42 ? n[cfg] : "?";
+                              "fold P8 a64 zm g512",   "fold P16 a128 nt zm g512",
+                              "burst P4 D1 x W16",     "burst P4 D2 x W8",      "burst P4 D4 x W8",
+                              "burst P4 D4 x W4",      "burst P4 D2 x W16",     "burst P4 D4 x W16",
+                              "burst P4 D1 fold W16",  "burst P4 D2 fold W8",   "burst P4 D4 fold W8",
+                              "burst P4 D2 fold W16",  "burst P4 D4 fold W16",  "burst P8 D2 fold W8"};
+    return cfg >= 0 && cfg < 54 ? n[cfg] : "?";
 }
 
 // nbytes: multiple of 16; for the packet shapes, npk packets of L bytes back to back
@@ -320,6 +394,18 @@ int sp_run(int cfg, const void* buf, uint64_t nbytes, uint32_t L, const void* ze
         case 39: sp_fold<8, 128, true, 0, 1><<<256, 1024, 65536, st>>>(b8, npk, L, z8, sink); break;
         case 40: sp_fold<8, 64, false, 0, 1><<<512, 1024, 65536, st>>>(b8, npk, L, z8, sink); break;
         case 41: sp_fold<16, 128, true, 0, 1><<<512, 1024, 65536, st>>>(b8, npk, L, z8, sink); break;
+        case 42: sp_burst<4, 1, 0><<<256, 1024, 0, st>>>(b8, npk, L, z8, sink); break;
+        case 43: sp_burst<4, 2, 0><<<256, 512, 0, st>>>(b8, npk, L, z8, sink); break;
+        case 44: sp_burst<4, 4, 0><<<256, 512, 0, st>>>(b8, npk, L, z8, sink); break;
+        case 45: sp_burst<4, 4, 0><<<256, 256, 0, st>>>(b8, npk, L, z8, sink); break;
+        case 46: sp_burst<4, 2, 0><<<256, 1024, 0, st>>>(b8, npk, L, z8, sink); break;
+        case 47: sp_burst<4, 4, 0><<<256, 1024, 0, st>>>(b8, npk, L, z8, sink); break;
+        case 48: sp_burst<4, 1, 1><<<256, 1024, 65536, st>>>(b8, npk, L, z8, sink); break;
+        case 49: sp_burst<4, 2, 1><<<256, 512, 65536, st>>>(b8, npk, L, z8, sink); break;
+        case 50: sp_burst<4, 4, 1><<<256, 512, 65536, st>>>(b8, npk, L, z8, sink); break;
+        case 51: sp_burst<4, 2, 1><<<256, 1024, 65536, st>>>(b8, npk, L, z8, sink); break;
+        case 52: sp_burst<4, 4, 1><<<256, 1024, 65536, st>>>(b8, npk, L, z8, sink); break;
+        case 53: sp_burst<8, 2, 1><<<256, 512, 65536, st>>>(b8, npk, L, z8, sink); break;
         default: return -1;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
