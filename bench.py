@@ -322,7 +322,8 @@ def kernel_name(args) -> str:
     if getattr(args, "path", 0) and args.path != 17:
         return f"kernel path {args.path}"
     if args.binned:
-        return f"crc32_lean_kernel<0, {lg}, 16, 2, 128>"
+        return (f"crc32_vring_kernel<{lg}, 0, 0, 0, 1>" if getattr(args, "path", 0) in (17, 18)
+                else f"crc32_lean_kernel<0, {lg}, 16, 2, 128>")
     if lg is None:
         return "crc32_stream_kernel / crc32_direct_kernel"
     return f"crc32_vring_kernel<{lg}, 0>"

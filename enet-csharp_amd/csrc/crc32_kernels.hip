@@ -1155,8 +1155,12 @@ int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStr
     const_cast<PacketArgs&>(pa).prio = static_cast<uint32_t>(ctx->ablation_prio);
     // the stream kernel takes 4, 8 or 16 lanes per packet; anything else runs direct
     // default (path 0) checksum batches at 4 or 8 lanes: the VGPR-ring kernel
-    if (mode == 0 && !pa.meta4 && (pa.lg == 2 || pa.lg == 3) && ctx->ablation == 0 && vring_path(ctx))
-        return vring_launch(pa.lg, ctx->num_cus * vring_wgs(ctx), vring_nt(ctx), st, pa, tb, ctx->d_basis2);
+    // (length-binned records: the lean kernel by default, 60 vs 66 us on cfg3 at 4 lanes,
+    // profiles/r02d_cfg3_*; the vring records instance on path 17 / 18)
+    if (mode == 0 && (pa.lg == 2 || pa.lg == 3) && ctx->ablation == 0 && vring_path(ctx) &&
+        (!pa.meta4 || ctx->path != 0))
+        return vring_launch(pa.lg, ctx->num_cus * (pa.meta4 ? 1 : vring_wgs(ctx)), vring_nt(ctx) && !pa.meta4, st, pa,
+                            tb, ctx->d_basis2);
     if (ctx->path != 1 && pa.lg >= 2 && pa.lg <= 4) {
         const bool lean_path = (ctx->path >= kLeanPath0 && ctx->path < kVringPath) || (ctx->path == 0 && ctx->ablation == 0);
         if (lean_path && pa.lg <= 3)
@@ -1384,9 +1388,10 @@ int enet_hip_crc32_batch_device_binned(enet_hip_context* ctx, const uint8_t* byt
     // (cfg3: 3160-3217 GiB/s at 4 lanes against 2495 at 8, profiles/r01e_*, r01f_*)
     pa.lg = static_cast<uint32_t>(log2i(ctx->lanes_per_packet > 0 ? ctx->lanes_per_packet : 4));
     pa.out = out;
-    // the ordered records only pay on the lean kernel; every other path reads len/off itself
-    const bool lean = ctx->path != 1 && (pa.lg == 2 || pa.lg == 3) &&
-                      ((ctx->path >= kLeanPath0 && ctx->path < kVringPath) || (ctx->path == 0 && ctx->ablation == 0));
+    // the ordered records pay on the vring (path 0) and lean kernels; every other path
+    // reads len/off itself
+    const bool lean = ctx->path != 1 && (pa.lg == 2 || pa.lg == 3) && ctx->ablation == 0 &&
+                      ((ctx->path >= kLeanPath0 && ctx->path < kVringPath) || vring_path(ctx));
     if (lean) {
         int rc;
         if ((rc = length_bin(lengths, offsets, nullptr, nullptr, count, 64u >> pa.lg, workspace, st))) return rc;

@@ -47,6 +47,9 @@ constexpr uint32_t kVrMeta = kVrStaging + kVrBasisRows * 256;
 constexpr uint32_t kVrMetaWave = 3 * 256;
 constexpr int kVrLds = kVrMeta + kVrW * kVrMetaWave;             // 79.5 KiB: two workgroups per CU
 static_assert(2 * kVrLds <= 160 * 1024, "two workgroups per CU");
+// length-binned records (BIN): the 4 dwords {len, off_lo, off_hi, index} per lane
+constexpr uint32_t kVrMetaWaveBin = 4 * 256;
+constexpr int kVrLdsBin = kVrMeta + kVrW * kVrMetaWaveBin;       // 82.5 KiB: one workgroup per CU
 
 // Global loads as inline asm, waited for by explicit counted vmcnt.  The
 // compiler's own wait insertion loses count across the loop's group-switch
@@ -112,13 +115,31 @@ __device__ __forceinline__ void vr_issue_meta(uint64_t len_addr, uint64_t off_ad
                  "global_load_lds_dword %3, off"             // (an instruction offset would move the LDS address too)
                  :: "v"(len_addr), "v"(off_addr), "s"(base), "v"(off_addr + 4u) : "m0", "scc", "memory");
 }
-// the metadata once at most N younger loads are in flight
-template <int N>
-__device__ __forceinline__ void vr_wait_meta(uint32_t base, uint32_t lane, uint32_t& L, uint64_t& off) {
+// a length-binned record {len, off_lo, off_hi, index} (crc32_kernels.hip
+// length_bin), dword f into the wave's area at base + 256 f: four LDS-DMA loads
+__device__ __forceinline__ void vr_issue_rec(uint64_t rec_addr, uint32_t base) {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\t"
+                 "s_mov_b32 m0, %4\n\t"
+                 "global_load_lds_dword %0, off\n\t"
+                 "s_add_u32 m0, m0, 0x100\n\t"
+                 "global_load_lds_dword %1, off\n\t"
+                 "s_add_u32 m0, m0, 0x100\n\t"
+                 "global_load_lds_dword %2, off\n\t"
+                 "s_add_u32 m0, m0, 0x100\n\t"
+                 "global_load_lds_dword %3, off"
+                 :: "v"(rec_addr), "v"(rec_addr + 4u), "v"(rec_addr + 8u), "v"(rec_addr + 12u), "s"(base)
+                 : "m0", "scc", "memory");
+}
+// the metadata once at most N younger loads are in flight (BIN: and the record's
+// caller index, dword 3)
+template <int N, int BIN>
+__device__ __forceinline__ void vr_wait_meta(uint32_t base, uint32_t lane, uint32_t& L, uint64_t& off,
+                                             uint32_t& idx) {
     asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
     L = lds_load(base + 4u * lane);
     off = static_cast<uint64_t>(lds_load(base + 256u + 4u * lane)) |
           (static_cast<uint64_t>(lds_load(base + 512u + 4u * lane)) << 32);
+    if constexpr (BIN) idx = lds_load(base + 768u + 4u * lane);
 }
 // every load retired (the wave's exit: no load may land after it has ended)
 __device__ __forceinline__ void vr_drain() {
@@ -298,7 +319,10 @@ struct VrIt {
 // wait also retires the stage just issued (no load in flight during a fold); bit 3
 // = 128-byte window starts and line-shaped stage loads (wrong CRCs by design);
 // bit 4 = no end-of-packet corrections (wrong CRCs by design)
-template <int LG, int TR = 0, int NT = 0, int ABL = 0>
+// BIN = 1: the batch's metadata are length-binned records (VrBatch::off points at
+// them, 4 dwords per packet), read in record order; packet r's CRC goes to
+// out[record r's index] (enet_hip_crc32_batch_device_binned).  One workgroup per CU.
+template <int LG, int TR = 0, int NT = 0, int ABL = 0, int BIN = 0>
 __global__ void __launch_bounds__(64 * kVrW) __attribute__((amdgpu_waves_per_eu(8, 8), amdgpu_num_vgpr(24)))
 crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_t* trace) {
     constexpr uint32_t P = 1u << LG, kPk = 64u >> LG;
@@ -375,9 +399,10 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
     if (wave < static_cast<uint32_t>(kVrBasisRows))
         dma4(basis + static_cast<size_t>(LG == 2 ? 1 : 2) * kVrBasisDwords + 64u * wave + lane,
              kVrStaging + 256u * wave);
-    const uint32_t mbase = kVrMeta + kVrMetaWave * wave;      // the wave's metadata area
+    const uint32_t mbase = kVrMeta + (BIN ? kVrMetaWaveBin : kVrMetaWave) * wave;   // the wave's metadata area
     uint32_t mL = 0;                                         // metadata (read out at group switches)
     uint64_t moff = 0;
+    uint32_t midx = 0;                                       // BIN: the record's caller index
     auto load_meta = [&](const VrIt& it) __attribute__((always_inline)) {
         const VrBatch& B = bl.b[it.b];
         // the lane's packet, clamped to the batch's last (always a valid address; the
@@ -385,11 +410,14 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
         const uint64_t base = min<uint64_t>(group_base(it), B.n - 1u);
         const uint64_t left = B.n - 1u - base;               // (uniform: scalar select, no VALU)
         const uint32_t q = min(lane_p(), left < 63u ? static_cast<uint32_t>(left) : 63u);
-        vr_issue_meta(reinterpret_cast<uint64_t>(B.len + base) + 4u * q,
-                      reinterpret_cast<uint64_t>(B.off + base) + 8u * q, mbase);
+        if constexpr (BIN)
+            vr_issue_rec(reinterpret_cast<uint64_t>(B.off) + 16u * (base + q), mbase);
+        else
+            vr_issue_meta(reinterpret_cast<uint64_t>(B.len + base) + 4u * q,
+                          reinterpret_cast<uint64_t>(B.off + base) + 8u * q, mbase);
     };
     load_meta(any ? pit : VrIt{0u, 0u, 0u, 0u});             // (batch 0 exists: count >= 1)
-    vr_wait_meta<0>(mbase, lane, mL, moff);                  // basis row and metadata have landed
+    vr_wait_meta<0, BIN>(mbase, lane, mL, moff, midx);       // basis row and metadata have landed
     mark(1);
 
     // ---- producer: window of the group it loads, one stage ahead of the consumer
@@ -400,9 +428,11 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
     constexpr uint32_t kAln = (ABL & 8) ? 128u : 64u;         // window start alignment
     auto plz = [&]() __attribute__((always_inline)) { return static_cast<uint32_t>(pwl) & (kAln - 1u); };
     uint32_t pst = 0, pstages = 0;
+    uint32_t pidx = 0;                                       // BIN: the caller index of the lane's packet
     bool pdone = !any;
     auto producer_enter = [&]() __attribute__((always_inline)) {   // group pit; metadata in mL / moff
         const VrBatch& B = bl.b[pit.b];
+        if constexpr (BIN) pidx = midx;
         const uint64_t rem = B.n - group_base(pit);          // packets of the batch from the group's first
         const uint32_t L = lane_p() < rem ? mL : 0u;
         const uint64_t a = reinterpret_cast<uint64_t>(B.bytes) + moff;
@@ -428,7 +458,7 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
                 // group qit's metadata was issued before the last produce's two stage
                 // loads (on this group's first stage, or at the prologue): retired
                 // once at most those two are in flight (stores do not count: older)
-                vr_wait_meta<2>(mbase, lane, mL, moff);
+                vr_wait_meta<2, BIN>(mbase, lane, mL, moff, midx);
                 pit = qit;
                 qlive = advance(qit);
                 producer_enter();
@@ -451,7 +481,7 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
         if (meta) {
             load_meta(qit);
             vr_issue_stage<slot, NT>(s0, s1);
-            if constexpr (WS >= 0) vr_wait_stage<(ABL & 4) ? 0 : 5>();   // 3 metadata + 2 stage loads younger
+            if constexpr (WS >= 0) vr_wait_stage<(ABL & 4) ? 0 : (BIN ? 6 : 5)>();   // 3 (BIN: 4) metadata + 2 stage loads younger
         } else {
             vr_issue_stage<slot, NT>(s0, s1);
             if constexpr (WS >= 0) vr_wait_stage<(ABL & 4) ? 0 : 2>();
@@ -500,7 +530,8 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
 
     // ---- consumer
     uint32_t reg = 0, clz = 0, ce = 0, cs = 0, cstages = 0, nedge = ~0u;
-    uint32_t* cout = nullptr;                                // the CRCs of the group's packets
+    uint32_t* cout = nullptr;                                // the CRCs of the group's packets (BIN: the batch's)
+    uint32_t cidx = 0;                                       // BIN: the caller index of the lane's packet
     uint64_t crem = 0;                                       // packets of its batch from the group's first
     // first stage >= from holding a partly covered head or tail piece (~0u = none)
     auto next_edge = [&](uint32_t from) __attribute__((always_inline)) -> uint32_t {
@@ -518,7 +549,8 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
         clz = plz();
         ce = pe;
         const uint64_t base = group_base(pit);
-        cout = bl.b[pit.b].out + base;
+        cout = bl.b[pit.b].out + (BIN ? 0u : base);
+        if constexpr (BIN) cidx = pidx;
         crem = bl.b[pit.b].n - base;
         const uint32_t nb = (ce + 31u) >> 5;                 // 0 for an empty packet ([0, 0))
         cstages = max(1u, wave_max_u((nb + P - 1u) >> LG));
@@ -573,7 +605,7 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
             const uint32_t tz = nb ? 32u * nb - ce : 0u;
             if constexpr (!(ABL & 16))
                 if (lane_k() == 0u && tz) reg = vr_mulmod(reg, lds_load(cinv_addr(tz)));
-            if (lane_k() == 0u && lane_p() < crem) cout[lane_p()] = finalize(reg);   // packet.cs:159
+            if (lane_k() == 0u && lane_p() < crem) cout[BIN ? cidx : lane_p()] = finalize(reg);   // packet.cs:159
             if (pdone) {
                 // no newer group entered: the wave is done.  The producer's last loads
                 // (zero lines past the end) are dead: retire them before the wave ends
@@ -599,10 +631,11 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
 
 // ---------------------------------------------------------------- host side
 
-template <int LG, int TR = 0, int NT = 0, int ABL = 0>
+template <int LG, int TR = 0, int NT = 0, int ABL = 0, int BIN = 0>
 const void* vring_fn() {
-    return reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR, NT, ABL>);
+    return reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR, NT, ABL, BIN>);
 }
+const void* vring_pick_bin(int lg) { return lg == 2 ? vring_fn<2, 0, 0, 0, 1>() : vring_fn<3, 0, 0, 0, 1>(); }
 
 // The product instances: 64 VGPRs (WPE 8), one or two workgroups per CU.  With a
 // trace buffer: the same kernel writing per-wave timestamps.  nt: the stage loads
@@ -629,11 +662,15 @@ int vring_setup() {
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, kVrLds);
             if (e != hipSuccess) return -static_cast<int>(e);
         }
+    for (int lg = 2; lg <= 3; ++lg) {
+        const hipError_t e = hipFuncSetAttribute(vring_pick_bin(lg), hipFuncAttributeMaxDynamicSharedMemorySize, kVrLdsBin);
+        if (e != hipSuccess) return -static_cast<int>(e);
+    }
     return 0;
 }
 
 int vring_launch_list(int lg, int max_wgs, bool nt, int abl, hipStream_t st, const VrBatches& bl, const KernelTables& tb,
-                      const uint32_t* basis2, uint64_t* trace) {
+                      const uint32_t* basis2, uint64_t* trace, bool bin) {
     if ((lg != 2 && lg != 3) || bl.count > static_cast<uint32_t>(kVrMaxBatches))
         return -static_cast<int>(hipErrorInvalidValue);
     // empty batches dropped: the kernel may then read any batch's packet n - 1
@@ -657,18 +694,20 @@ int vring_launch_list(int lg, int max_wgs, bool nt, int abl, hipStream_t st, con
         dealt += g;
     }
     void* args[] = {&a, const_cast<KernelTables*>(&tb), const_cast<const uint32_t**>(&basis2), &trace};
-    const hipError_t e = hipLaunchKernel(vring_pick(lg, trace != nullptr, nt, abl), dim3(grid), dim3(64 * kVrW), args, kVrLds, st);
+    const void* fn = bin ? vring_pick_bin(lg) : vring_pick(lg, trace != nullptr, nt, abl);
+    const hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(64 * kVrW), args, bin ? kVrLdsBin : kVrLds, st);
     return e == hipSuccess ? 0 : -static_cast<int>(e);
 }
 
 int vring_launch(int lg, int max_wgs, bool nt, hipStream_t st, const PacketArgs& pa, const KernelTables& tb,
                  const uint32_t* basis2) {
-    if (pa.meta4) return -static_cast<int>(hipErrorInvalidValue);   // binned records: the lean kernel
     if (pa.n == 0) return 0;
     VrBatches bl{};
     bl.count = 1;
-    bl.b[0] = VrBatch{pa.bytes, pa.off, pa.len, pa.out, pa.n};
-    return vring_launch_list(lg, max_wgs, nt, 0, st, bl, tb, basis2, pa.trace);
+    // binned records: the record array rides in the offsets field (BIN instance)
+    bl.b[0] = pa.meta4 ? VrBatch{pa.bytes, reinterpret_cast<const uint64_t*>(pa.meta4), nullptr, pa.out, pa.n}
+                       : VrBatch{pa.bytes, pa.off, pa.len, pa.out, pa.n};
+    return vring_launch_list(lg, max_wgs, nt, 0, st, bl, tb, basis2, pa.meta4 ? nullptr : pa.trace, pa.meta4 != nullptr);
 }
 
 }  // namespace enethip

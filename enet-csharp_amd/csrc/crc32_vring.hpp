@@ -45,10 +45,13 @@ int vring_setup();
 // count: one per CU; twice that: two); nt = nontemporal stage loads;
 // abl = diagnostics ablation (0 in the product, crc32_vring.hip).  trace = per-wave timestamps or null.
 int vring_launch_list(int lg, int max_wgs, bool nt, int abl, hipStream_t st, const VrBatches& bl, const KernelTables& tb,
-                      const uint32_t* basis2, uint64_t* trace);
+                      const uint32_t* basis2, uint64_t* trace, bool bin = false);
 
+// bin = the batches' metadata are length-binned records {len, off_lo, off_hi,
+// index} (VrBatch::off points at them, len unused): results go to out[index];
+// 82.5 KiB of LDS, so at most one workgroup per CU (max_wgs = the CU count).
 // Launch the vring kernel over one batch: checksum mode, lanes per packet 2^lg
-// (lg = 2 or 3), at most max_wgs workgroups.  basis2 = kVrBasisDwords per image (images for
+// (lg = 2 or 3), at most max_wgs workgroups; pa.meta4 set = binned records.  basis2 = kVrBasisDwords per image (images for
 // P = 1, 4, 8, 16 in that order).  Returns 0 or -hipError_t.
 int vring_launch(int lg, int max_wgs, bool nt, hipStream_t st, const PacketArgs& pa, const KernelTables& tb,
                  const uint32_t* basis2);

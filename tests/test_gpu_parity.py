@@ -113,18 +113,36 @@ def run_binned(ctx, payload, off, lens, lanes=0, path=0):
         ctx.set_kernel_path(0)
 
 
+BINNED_PATHS = (0, 17)        # 0: the lean kernel's records instance (default), 17: the vring kernel's
+
+
 def test_binned_cfg3_full(ctx, oracle_lib):
-    """Length-binned entry (records reordered on the GPU): same CRCs, caller order."""
+    """Length-binned entry (records reordered on the GPU): same CRCs, caller order,
+    on the lean (default) and vring record paths."""
     b = workloads.cfg3()
     exp = oracle_lib.batch(b.payload, b.off, b.lens, threads=16)
+    for path in BINNED_PATHS:
+        for lanes in (4, 8):
+            assert (run_binned(ctx, b.payload, b.off, b.lens, lanes, path) == exp).all(), (path, lanes)
+
+
+def test_binned_vring_many_groups(ctx, oracle_lib):
+    """Binned records on the vring kernel: 1.2 M tiny packets (one-stage groups, a
+    record load per group) and 40 K long ones (many stages per group)."""
+    tiny = workloads.mixed(1_200_000, 0, 40, seed=277, len_seed=278)
+    exp_t = oracle_lib.batch(tiny.payload, tiny.off, tiny.lens, threads=16)
+    big = workloads.mixed(40_000, 2000, 9000, seed=279, len_seed=280)
+    exp_b = oracle_lib.batch(big.payload, big.off, big.lens, threads=16)
     for lanes in (4, 8):
-        assert (run_binned(ctx, b.payload, b.off, b.lens, lanes) == exp).all(), lanes
+        assert (run_binned(ctx, tiny.payload, tiny.off, tiny.lens, lanes, 17) == exp_t).all(), ("tiny", lanes)
+        assert (run_binned(ctx, big.payload, big.off, big.lens, lanes, 17) == exp_b).all(), ("big", lanes)
 
 
 @pytest.mark.parametrize("lanes", [1, 4, 8])
-def test_binned_golden_and_edges(ctx, golden, oracle_lib, lanes):
+@pytest.mark.parametrize("path", BINNED_PATHS)
+def test_binned_golden_and_edges(ctx, golden, oracle_lib, lanes, path):
     payload, off, lens, exp = golden_batch(golden)
-    assert (run_binned(ctx, payload, off, lens, lanes) == exp).all()
+    assert (run_binned(ctx, payload, off, lens, lanes, path) == exp).all()
     # lengths over every bin incl. the clamped last one (>= 8160 B), empties, one-packet batches
     rng = np.random.default_rng(7 + lanes)
     n = 20000
@@ -134,8 +152,8 @@ def test_binned_golden_and_edges(ctx, golden, oracle_lib, lanes):
     off = rng.integers(0, 1 << 20, size=n).astype(np.uint64)
     payload = rng.integers(0, 256, size=(1 << 20) + 9000, dtype=np.uint8)
     exp = oracle_lib.batch(payload, off, lens, threads=8)
-    assert (run_binned(ctx, payload, off, lens, lanes) == exp).all()
-    assert (run_binned(ctx, payload, off[:1], lens[:1], lanes) == exp[:1]).all()
+    assert (run_binned(ctx, payload, off, lens, lanes, path) == exp).all()
+    assert (run_binned(ctx, payload, off[:1], lens[:1], lanes, path) == exp[:1]).all()
 
 
 def test_binned_records_are_a_length_ordered_permutation(ctx, oracle_lib):

@@ -108,6 +108,24 @@ def main():
                 print(json.dumps({"kind": "vring-list", "abl": abl, "path": path, "lanes": lanes, "wgs": wgs, "list": L, "us_per_launch": round(us, 2),
                                   "us_per_batch": round(us / L, 3), "GBps": round(L * BATCH / us / 1e3, 1)}), flush=True)
             ctx.close()
+    if what == "big":
+        # one batch of 20 cfg2 batches' packets (1.57 GB): per-launch start and drain amortised
+        import enethip
+        n = 20 * 65536
+        off = torch.arange(n, dtype=torch.int64, device="cuda") * 1200
+        lens = torch.full((n,), 1200, dtype=torch.int32, device="cuda")
+        out = torch.zeros(n, dtype=torch.int32, device="cuda")
+        for path, lanes, wgs in ((17, 4, 2), (17, 4, 1), (17, 8, 2), (13, 8, 0), (13, 4, 0), (14, 8, 0), (14, 4, 0)):
+            ctx = enethip.Context(0, lanes, wgs)
+            ctx.set_kernel_path(path)
+
+            def fn(i, ctx=ctx):
+                base = big[(i % 2) * 20 * BATCH:]
+                ctx.crc32_batch_device(base, off, lens, n, out, st.cuda_stream)
+            us = region_us(torch, st, fn, 8)
+            print(json.dumps({"kind": "one-big-batch", "path": path, "lanes": lanes, "wgs": wgs, "MB": n * 1200 / 1e6,
+                              "us": round(us, 2), "GBps": round(n * 1200 / us / 1e3, 1)}), flush=True)
+            ctx.close()
     print("done", flush=True)
 
 
