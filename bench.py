@@ -315,18 +315,22 @@ def make_batches(cfg: str, rotate: int, rank: int):
     return out
 
 
-def kernel_name(args) -> str:
+def kernel_name(args, list_launch: bool = False) -> str:
     """The dominant kernel of the measured entry point (as rocprofv3 names it)."""
+    path = getattr(args, "path", 0)
+    if list_launch and path == 13 and args.lanes in (0, 4, 8) and not args.binned:
+        # batch lists: the lean kernel's list instance, 8 lanes per packet unless set
+        return f"crc32_lean_list_kernel<{3 if args.lanes in (0, 8) else 2}, 16, 2>"
     lanes = args.lanes or 4
     lg = {4: 2, 8: 3}.get(lanes)
-    if getattr(args, "path", 0) and args.path != 17:
-        return f"kernel path {args.path}"
+    if path and path not in (17, 18):
+        return f"kernel path {path}"
     if args.binned:
-        return (f"crc32_vring_kernel<{lg}, 0, 0, 0, 1>" if getattr(args, "path", 0) in (17, 18)
+        return (f"crc32_vring_kernel<{lg}, 0, 0, 0, 1>" if path in (17, 18)
                 else f"crc32_lean_kernel<0, {lg}, 16, 2, 128>")
     if lg is None:
         return "crc32_stream_kernel / crc32_direct_kernel"
-    return f"crc32_vring_kernel<{lg}, 0>"
+    return f"crc32_vring_kernel<{lg}, 0{', 0, 1' if path == 18 else ''}>"
 
 
 def load_traffic(cfg: str):
@@ -451,7 +455,7 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": (None if not (traffic or {}).get("hbm_bytes_per_batch") else
                             round(traffic["hbm_bytes_per_batch"] * per_launch / float(batches[0].payload_bytes))),
-                "kernel": kernel_name(args),
+                "kernel": kernel_name(args, per_launch_steps > 1),
                 "kernel_ms": round(r_ms, 5),
                 "kernel_ms_timing": f"HIP events around {nk} serial launches on the launch stream",
                 "kernel_ms_bracketed_median": round(k_ms, 5),

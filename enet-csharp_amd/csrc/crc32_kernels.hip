@@ -1342,6 +1342,22 @@ int enet_hip_crc32_batch_list_device(enet_hip_context* ctx, const ENetHipBatch* 
     }
     ENH_CHECK(hipSetDevice(ctx->device));
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    // path 13 (kLeanPath0): the lean kernel over the list, 8 lanes per packet unless
+    // set -- the faster one on long serial lists (20 batches: 5.43 vs 5.10 TB/s), the
+    // slower one when lists of 4-5 batches overlap on streams (bench driver form:
+    // 4548-4784 vs 5011-5186 GiB/s; its one 160-KiB workgroup per CU leaves no room
+    // for the next launch's), profiles/r02d_lists_*; default (path 0) and 17 / 18: vring
+    if (ctx->path == kLeanPath0 && ctx->ablation == 0 && ctx->vr_abl == 0 &&
+        (ctx->lanes_per_packet == 0 || ctx->lanes_per_packet == 4 || ctx->lanes_per_packet == 8)) {
+        const int llg = ctx->lanes_per_packet == 4 ? 2 : 3;
+        const KernelTables tb = tables_of(ctx);
+        for (size_t b0 = 0; b0 < batchCount; b0 += kLeanMaxBatches) {
+            const int rc = lean_launch_list(llg, ctx->num_cus, st, batches + b0,
+                                            std::min<size_t>(batchCount - b0, kLeanMaxBatches), tb);
+            if (rc) return rc;
+        }
+        return 0;
+    }
     const int lg = log2i(auto_lanes(ctx));
     if ((lg == 2 || lg == 3) && ctx->ablation == 0 && vring_path(ctx)) {
         const KernelTables tb = tables_of(ctx);

@@ -145,13 +145,37 @@ __device__ __forceinline__ void wait_vm_sel(uint32_t c) {
 // 128 (product, correct checksums) = metadata from the length-ordered records of the
 // *_binned entry points (PacketArgs::meta4): a separate instance, so the plain path
 // carries no per-op test for it.
-template <int MODE, int LG, int W, int NB, int ABL = 0>
-__global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, KernelTables tb) {
+
+// a wave-uniform 64-bit value as such (both halves through readfirstlane)
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
+    return static_cast<uint64_t>(lo) | (static_cast<uint64_t>(hi) << 32);
+}                     // (the one-batch instances never read it)
+
+// LIST = 1 (checksum mode, no ablation): the batches of a LeanList, their groups
+// concatenated (batch b's groups are global groups g0_b ..) and dealt over the
+// waves as one batch's are; pa is unused.  A wave's groups ascend, so each of its
+// three walkers (metadata, producer, consumer) finds a group's batch with a cursor
+// that only moves forward.
+// The list lives in the kernel-argument segment and is read there (llp, scalar
+// loads): a reference to the by-value argument made hipcc copy all 2.3 KiB of it
+// into scratch.
+using LeanListPtr = const __attribute__((address_space(4))) LeanList*;
+
+template <int MODE, int LG, int W, int NB, int ABL, int LIST>
+__device__ __forceinline__ void lean_body(const PacketArgs& pa, const KernelTables& tb, LeanListPtr llp) {
     using G = LeanGeom<MODE, LG, W, NB>;
     constexpr uint32_t P = G::P, kPk = G::kPk, JM = G::JM;
+    static_assert(!LIST || (MODE == 0 && ABL == 0), "batch lists: checksum mode, product instance");
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t ngroups = (pa.n + kPk - 1u) >> (6 - LG);
+    const uint64_t ngroups = LIST ? llp->groups : (pa.n + kPk - 1u) >> (6 - LG);
+    // the batch of global group gg, from cursor b on (LIST)
+    auto locate = [&](uint64_t gg, uint32_t& b) __attribute__((always_inline)) {
+        while (b + 1u < llp->count && gg >= llp->b[b + 1u].g0) ++b;
+    };
+    uint32_t mb = 0, pb = 0, cb = 0;                         // metadata / producer / consumer cursors (LIST)
     const uint64_t wv = static_cast<uint64_t>(blockIdx.x) * W + wave;
     const uint64_t wt = static_cast<uint64_t>(gridDim.x) * W;
     // groups of this wave: wv, wv + wt, ... (default) or, with ABL & 32, a contiguous range
@@ -197,6 +221,27 @@ __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, Kerne
             const uint32_t x = 64u * o + lane;
             const uint32_t q = x / G::kGroupMeta, f = (x / kPk) % G::kF, p = x % kPk;
             const uint32_t j = min(c * JM + q, J - 1u);
+            if constexpr (LIST) {
+                // an op covers the groups of its first and last lane (1 or 2 groups): their
+                // batches from the metadata cursor, then each lane takes its own
+                const uint32_t qa = 64u * o / G::kGroupMeta, qb = (64u * o + 63u) / G::kGroupMeta;
+                const uint64_t ga = group_of(min(c * JM + qa, J - 1u)), gb = group_of(min(c * JM + qb, J - 1u));
+                locate(ga, mb);
+                const uint32_t ba = mb;
+                locate(gb, mb);
+                // (each field read as a wave-uniform value first: a select of two kernel-argument
+                // addresses would be a divergent index into the argument block, i.e. a scratch copy)
+                const bool ia = q == qa;
+                const uint64_t g0 = ia ? uni64(llp->b[ba].g0) : uni64(llp->b[mb].g0);
+                const uint64_t n = ia ? uni64(llp->b[ba].n) : uni64(llp->b[mb].n);
+                const uint64_t pk = min((group_of(j) - g0) * kPk + p, n - 1u);
+                const uint32_t* lp = reinterpret_cast<const uint32_t*>(
+                    ia ? uni64(reinterpret_cast<uint64_t>(llp->b[ba].len)) : uni64(reinterpret_cast<uint64_t>(llp->b[mb].len)));
+                const uint32_t* op = reinterpret_cast<const uint32_t*>(
+                    ia ? uni64(reinterpret_cast<uint64_t>(llp->b[ba].off)) : uni64(reinterpret_cast<uint64_t>(llp->b[mb].off)));
+                dma4((f == 1u || f == 2u) ? op + 2u * pk + (f - 1u) : lp + pk, half + 256u * o);
+                continue;
+            }
             const uint64_t pk = min(group_of(j) * kPk + p, pa.n - 1u);
             const uint32_t* src = pa.len + pk;
             if (f == 1u || f == 2u) src = reinterpret_cast<const uint32_t*>(pa.off) + 2u * pk + (f - 1u);
@@ -209,14 +254,15 @@ __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, Kerne
     auto meta_at = [&](uint32_t j, uint32_t f) __attribute__((always_inline)) -> uint32_t {
         return lds_load(meta0 + ((j / JM) & 1u) * G::kHalf + 4u * (((j % JM) * G::kF + f) * kPk + pj_lane));
     };
-    auto window_of = [&](uint32_t j) __attribute__((always_inline)) -> Window {
+    // (LIST: b = the group's batch)
+    auto window_of = [&](uint32_t j, uint32_t b) __attribute__((always_inline)) -> Window {
         Window w;
-        const uint64_t pkw = group_of(j) * kPk + pj_lane;
-        w.active = pkw < pa.n;
+        const uint64_t pkw = (group_of(j) - (LIST ? llp->b[b].g0 : 0u)) * kPk + pj_lane;
+        w.active = pkw < (LIST ? llp->b[b].n : pa.n);
         w.L = w.active ? ((ABL & 16) ? 1200u : meta_at(j, 0)) : 0u;
         const uint64_t off = (ABL & 16) ? 1200u * pkw
                                         : static_cast<uint64_t>(meta_at(j, 1)) | (static_cast<uint64_t>(meta_at(j, 2)) << 32);
-        const uint64_t a = reinterpret_cast<uint64_t>(pa.bytes) + off, e = a + w.L;
+        const uint64_t a = reinterpret_cast<uint64_t>(LIST ? llp->b[b].bytes : pa.bytes) + off, e = a + w.L;
         w.tz = w.L ? static_cast<uint32_t>((0u - e) & 15u) : 0u;       // window ends at the granule after the end
         w.nb = w.L ? (w.L + w.tz + 31u) >> 5 : 0u;
         w.lz = 32u * w.nb - w.tz - w.L;
@@ -250,7 +296,8 @@ __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, Kerne
     uint32_t meta_guard = 0;                                 // from this iteration on chunk `issued - 1` has landed
     uint32_t mbits = 0;                                      // bit u: iteration it-1-u issued a metadata chunk
     auto producer_setup = [&](uint32_t j) __attribute__((always_inline)) {
-        const Window w = window_of(j);
+        if constexpr (LIST) locate(group_of(j), pb);
+        const Window w = window_of(j, pb);
         const uint32_t w0 = (k - w.r) & (P - 1u);
         const uint32_t cnt = w0 < w.nb ? ((w.nb - 1u - w0) >> LG) + 1u : 0u;
         const uint32_t np = 2u * w.nb;                       // window pieces
@@ -362,9 +409,14 @@ __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, Kerne
     // ---- consumer
     uint32_t cj = 0, cst = 0, cstages = 0, nedge = ~0u, reg = 0, desired = 0;
     Task t{};
+    uint32_t* cout = pa.out;                                 // (LIST: the consumer's batch's)
     auto consumer_setup = [&](uint32_t j) __attribute__((always_inline)) {
-        const Window w = window_of(j);
-        t.pk = group_of(j) * kPk + pj_lane;
+        if constexpr (LIST) {
+            locate(group_of(j), cb);
+            cout = llp->b[cb].out;
+        }
+        const Window w = window_of(j, cb);
+        t.pk = (group_of(j) - (LIST ? llp->b[cb].g0 : 0u)) * kPk + pj_lane;
         if constexpr (kBin) if (w.active) t.pk = meta_at(j, MODE ? 5u : 3u);   // binned: the packet's caller index
         t.active = w.active;
         t.k = k;
@@ -441,7 +493,7 @@ __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, Kerne
             if (MODE) desired = xor_lanes<0>(LG, desired);
             if (t.active && t.k == 0u) {
                 if (MODE == 0) {
-                    pa.out[t.pk] = finalize(reg);            // packet.cs:159
+                    cout[t.pk] = finalize(reg);              // packet.cs:159
                 } else {
                     const uint32_t comp = t.slot_ok ? finalize(reg) : 0u;
                     pa.ok[t.pk] = (t.slot_ok && comp == desired) ? 1 : 0;   // protocol.cs:1066-1068
@@ -470,6 +522,20 @@ __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, Kerne
     trace_end();
 }
 
+template <int MODE, int LG, int W, int NB, int ABL = 0>
+__global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, KernelTables tb) {
+    lean_body<MODE, LG, W, NB, ABL, 0>(pa, tb, nullptr);
+}
+
+// batch lists (enet_hip_crc32_batch_list_device): checksum mode
+template <int LG, int W, int NB>
+__global__ void __launch_bounds__(64 * W) crc32_lean_list_kernel(LeanList ll, KernelTables tb) {
+    PacketArgs pa{};
+    (void)ll;
+    // the first kernel argument sits at the start of the segment
+    lean_body<0, LG, W, NB, 0, 1>(pa, tb, (LeanListPtr)(__builtin_amdgcn_kernarg_segment_ptr()));
+}
+
 // ---------------------------------------------------------------- host side
 
 template <int W, int NB>
@@ -479,12 +545,15 @@ struct LeanVariant {
         return reinterpret_cast<const void*>(crc32_lean_kernel<MODE, LG, W, NB, ABL>);
     }
     static int setup() {
-        const void* fns[8] = {fn<0, 2>(), fn<0, 3>(), fn<1, 2>(), fn<1, 3>(),
-                              fn<0, 2, 128>(), fn<0, 3, 128>(), fn<1, 2, 128>(), fn<1, 3, 128>()};
-        const int lds[8] = {LeanGeom<0, 2, W, NB>::kLds, LeanGeom<0, 3, W, NB>::kLds, LeanGeom<1, 2, W, NB>::kLds,
-                            LeanGeom<1, 3, W, NB>::kLds, LeanGeom<0, 2, W, NB>::kLds, LeanGeom<0, 3, W, NB>::kLds,
-                            LeanGeom<1, 2, W, NB>::kLds, LeanGeom<1, 3, W, NB>::kLds};
-        for (int i = 0; i < 8; ++i) {
+        const void* fns[10] = {fn<0, 2>(), fn<0, 3>(), fn<1, 2>(), fn<1, 3>(),
+                               fn<0, 2, 128>(), fn<0, 3, 128>(), fn<1, 2, 128>(), fn<1, 3, 128>(),
+                               reinterpret_cast<const void*>(crc32_lean_list_kernel<2, W, NB>),
+                               reinterpret_cast<const void*>(crc32_lean_list_kernel<3, W, NB>)};
+        const int lds[10] = {LeanGeom<0, 2, W, NB>::kLds, LeanGeom<0, 3, W, NB>::kLds, LeanGeom<1, 2, W, NB>::kLds,
+                             LeanGeom<1, 3, W, NB>::kLds, LeanGeom<0, 2, W, NB>::kLds, LeanGeom<0, 3, W, NB>::kLds,
+                             LeanGeom<1, 2, W, NB>::kLds, LeanGeom<1, 3, W, NB>::kLds, LeanGeom<0, 2, W, NB>::kLds,
+                             LeanGeom<0, 3, W, NB>::kLds};
+        for (int i = 0; i < 10; ++i) {
             const hipError_t e = hipFuncSetAttribute(fns[i], hipFuncAttributeMaxDynamicSharedMemorySize, lds[i]);
             if (e != hipSuccess) return -static_cast<int>(e);
         }
@@ -545,6 +614,32 @@ struct LeanVariant {
         }
     }
 };
+
+// A batch list in one launch: the batches' groups concatenated (empty batches
+// dropped) and dealt over one 16-wave workgroup per CU (geometry 0).
+int lean_launch_list(int lg, int num_cus, hipStream_t st, const ENetHipBatch* batches, size_t count,
+                     const KernelTables& tb) {
+    if ((lg != 2 && lg != 3) || count > static_cast<size_t>(kLeanMaxBatches)) return -static_cast<int>(hipErrorInvalidValue);
+    LeanList ll{};
+    const uint64_t kpk = 64u >> lg;
+    for (size_t i = 0; i < count; ++i) {
+        if (!batches[i].count) continue;
+        LeanListBatch& b = ll.b[ll.count++];
+        b = LeanListBatch{batches[i].bytes, batches[i].offsets, batches[i].lengths, batches[i].out,
+                          static_cast<uint64_t>(batches[i].count), ll.groups};
+        ll.groups += (b.n + kpk - 1u) / kpk;
+    }
+    if (ll.count == 0) return 0;
+    const unsigned grid = static_cast<unsigned>(
+        std::max<uint64_t>(1, std::min<uint64_t>((ll.groups + 15u) / 16u, static_cast<uint64_t>(num_cus))));
+    constexpr int lds2 = LeanGeom<0, 2, 16, 2>::kLds, lds3 = LeanGeom<0, 3, 16, 2>::kLds;
+    if (lg == 2)
+        hipLaunchKernelGGL((crc32_lean_list_kernel<2, 16, 2>), dim3(grid), dim3(64 * 16), lds2, st, ll, tb);
+    else
+        hipLaunchKernelGGL((crc32_lean_list_kernel<3, 16, 2>), dim3(grid), dim3(64 * 16), lds3, st, ll, tb);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : -static_cast<int>(e);
+}
 
 int lean_setup() {
     int rc = LeanVariant<16, 2>::setup();

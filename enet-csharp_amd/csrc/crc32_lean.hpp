@@ -4,10 +4,30 @@
 #include <hip/hip_runtime.h>
 
 #include "crc32_stream_common.hpp"
+#include "enet_hip.h"
 
 namespace enethip {
 
-constexpr int kLeanGeoms = 4;   // 0: 16 waves x 2 stages, 1: 12 waves x 3 stages; sweeps: 2: 14 x 3, 3: 10 x 4
+constexpr int kLeanGeoms = 4;
+
+// Batch lists (lean_launch_list): one launch over up to kLeanMaxBatches batches,
+// batch b's groups numbered from g0 in one concatenated group space.
+struct LeanListBatch {
+    const uint8_t* bytes;
+    const uint64_t* off;
+    const uint32_t* len;
+    uint32_t* out;
+    uint64_t n;
+    uint64_t g0;
+};
+constexpr int kLeanMaxBatches = 48;
+struct LeanList {
+    uint32_t count;
+    uint32_t pad;
+    uint64_t groups;   // all batches' groups
+    LeanListBatch b[kLeanMaxBatches];
+};
+static_assert(sizeof(LeanList) <= 3072, "kernel arguments");   // 0: 16 waves x 2 stages, 1: 12 waves x 3 stages; sweeps: 2: 14 x 3, 3: 10 x 4
 
 // Set the dynamic-LDS attribute of every lean kernel instance (once per context).
 int lean_setup();
@@ -17,6 +37,11 @@ int lean_setup();
 // only; wrong checksums by design).  Returns 0 or -hipError_t.
 int lean_launch(int mode, int lg, int geom, int abl, int num_cus, hipStream_t st, const PacketArgs& pa,
                 const KernelTables& tb);
+
+// Checksum a list of batches (count <= kLeanMaxBatches) in one launch at lanes
+// per packet 2^lg (lg = 2 or 3).  Returns 0 or -hipError_t.
+int lean_launch_list(int lg, int num_cus, hipStream_t st, const ENetHipBatch* batches, size_t count,
+                     const KernelTables& tb);
 
 // Order the packet records of each 1024-packet tile by length bin, longest first,
 // and interleave the tiles' groups of kpk records rank by rank (see

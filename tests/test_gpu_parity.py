@@ -462,21 +462,28 @@ def _run_list(ctx, cases):
     return [o.cpu().numpy().view(np.uint32)[:len(c[1])] for o, c in zip(outs, cases)]
 
 
-def test_batch_list(ctx, oracle_lib):
+LIST_PATHS = (0, 13)          # 0: the vring kernel (default), 13: the lean kernel's list instance
+
+
+@pytest.mark.parametrize("path", LIST_PATHS)
+def test_batch_list(ctx, oracle_lib, path):
     """enet_hip_crc32_batch_list_device: batches of every shape in one launch,
-    each against the oracle; 4 and 8 lanes (vring), 16 lanes (one launch per
-    batch on the stream kernel)."""
+    each against the oracle; vring (path 0) or lean (13) lists at the default, 4 and
+    8 lanes; 16 lanes (one launch per batch on the stream kernel)."""
     cases = _batch_list_cases(oracle_lib)
     try:
-        for lanes in (4, 8, 16):
+        ctx.set_kernel_path(path)
+        for lanes in (0, 4, 8, 16):
             ctx.set_tuning(lanes, 0)
             for i, (got, c) in enumerate(zip(_run_list(ctx, cases), cases)):
-                assert (got == c[3]).all(), (lanes, i, np.nonzero(got != c[3])[0][:5])
+                assert (got == c[3]).all(), (path, lanes, i, np.nonzero(got != c[3])[0][:5])
     finally:
+        ctx.set_kernel_path(0)
         ctx.set_tuning(0, 0)
 
 
-def test_batch_list_many_launches(ctx, oracle_lib):
+@pytest.mark.parametrize("path", LIST_PATHS)
+def test_batch_list_many_launches(ctx, oracle_lib, path):
     """More batches than one launch takes (48): 110 small batches of varied sizes,
     plus the reverse order (the grid is sized by the largest batch)."""
     rng = np.random.default_rng(55)
@@ -489,9 +496,13 @@ def test_batch_list_many_launches(ctx, oracle_lib):
                           np.zeros(0, np.uint32)))
         else:
             cases.append((b.payload, b.off, b.lens, oracle_lib.batch(b.payload, b.off, b.lens, threads=16)))
-    for order in (cases, cases[::-1]):
-        for i, (got, c) in enumerate(zip(_run_list(ctx, order), order)):
-            assert (got == c[3]).all(), (i, len(c[1]))
+    try:
+        ctx.set_kernel_path(path)
+        for order in (cases, cases[::-1]):
+            for i, (got, c) in enumerate(zip(_run_list(ctx, order), order)):
+                assert (got == c[3]).all(), (path, i, len(c[1]))
+    finally:
+        ctx.set_kernel_path(0)
 
 
 def test_vring_trace_instance(ctx, oracle_lib):

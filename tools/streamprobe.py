@@ -82,6 +82,8 @@ def main():
         import enethip
         lanes = int(os.environ.get("SP_LANES", "4"))
         combos = [(w, p, 0) for w in (2, 1) for p in (17, 18)]
+        if what == "list":
+            combos = [(0, 13, 0), (2, 17, 0)]
         if what == "abl8":
             combos = [(w, p, a) for w in (2, 1) for p in (17, 18) for a in (2048 + 4096 + 16384 + 32768,)]
             combos += [(w, 17, 2048 + 4096 + 32768) for w in (2, 1)]
@@ -91,7 +93,7 @@ def main():
         if what == "abl":
             combos = [(w, 17, a) for w in (2, 1) for a in (0, 4096, 2048 + 4096 + 32768)]
         for wgs, path, abl in combos:
-            ctx = enethip.Context(0, lanes, wgs)
+            ctx = enethip.Context(0, (8 if lanes == 4 else lanes) if (path == 13 and what == "list") else lanes, wgs)
             ctx.set_kernel_path(path)
             ctx.diag_ablation(abl)
             off = torch.arange(65536, dtype=torch.int64, device="cuda") * 1200
