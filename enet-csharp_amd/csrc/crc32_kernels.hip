@@ -1365,7 +1365,7 @@ int enet_hip_crc32_batch_list_device(enet_hip_context* ctx, const ENetHipBatch* 
             VrBatches bl{};
             for (size_t b = b0; b < std::min(batchCount, b0 + kVrMaxBatches); ++b)
                 bl.b[bl.count++] = VrBatch{batches[b].bytes, batches[b].offsets, batches[b].lengths, batches[b].out,
-                                           static_cast<uint64_t>(batches[b].count), 0u, 0u, 0u, 0u};
+                                           static_cast<uint64_t>(batches[b].count), 0u};
             const int rc = vring_launch_list(lg, ctx->num_cus * vring_wgs(ctx), vring_nt(ctx), ctx->vr_abl, st, bl, tb,
                                              ctx->d_basis2, ctx->trace);
             if (rc) return rc;

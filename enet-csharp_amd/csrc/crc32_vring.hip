@@ -45,11 +45,13 @@ constexpr uint32_t kVrStaging = kLdsTableBytes;                 // basis rows la
 // the offsets' low and high dwords, lane l's at +4l
 constexpr uint32_t kVrMeta = kVrStaging + kVrBasisRows * 256;
 constexpr uint32_t kVrMetaWave = 3 * 256;
-constexpr int kVrLds = kVrMeta + kVrW * kVrMetaWave;             // 79.5 KiB: two workgroups per CU
+constexpr uint32_t kVrCtr = kVrMeta + kVrW * kVrMetaWave;       // the workgroup's slot counter (16 B)
+constexpr int kVrLds = kVrCtr + 16;                              // 79.5 KiB: two workgroups per CU
 static_assert(2 * kVrLds <= 160 * 1024, "two workgroups per CU");
 // length-binned records (BIN): the 4 dwords {len, off_lo, off_hi, index} per lane
 constexpr uint32_t kVrMetaWaveBin = 4 * 256;
-constexpr int kVrLdsBin = kVrMeta + kVrW * kVrMetaWaveBin;       // 82.5 KiB: one workgroup per CU
+constexpr uint32_t kVrCtrBin = kVrMeta + kVrW * kVrMetaWaveBin;
+constexpr int kVrLdsBin = kVrCtrBin + 16;                        // 82.5 KiB: one workgroup per CU
 
 // Global loads as inline asm, waited for by explicit counted vmcnt.  The
 // compiler's own wait insertion loses count across the loop's group-switch
@@ -299,14 +301,19 @@ __device__ __forceinline__ uint32_t vr_lookups(const uint32_t (&d)[8], const VrS
     return acc;
 }
 
-// Batches of one launch: a wave takes its share of batch 0's groups (groups wv,
-// wv + wt, ... of that batch), then of batch 1, and so on -- each batch spread
-// over the whole chip as if launched alone, with no barrier between batches, so a
-// wave that is done with batch b streams b + 1 while its neighbours finish b, and
-// the start (metadata, table image) and the drain are paid once per launch.
+// Batches of one launch: their groups in one concatenated space (batch b's from
+// VrBatch::g0), dealt in slots.  Workgroup k's slot s is global group
+// 16 k + s % 16 + (s / 16) * wt (wt = the launch's waves): rounds of 16 consecutive
+// groups, one round per workgroup every wt groups, so every batch is spread over
+// the whole chip and the start (metadata, table image) and the drain are paid once
+// per launch.  A wave takes its first two slots statically (wave, 16 + wave) and
+// every later one from its workgroup's LDS counter, so the waves a SIMD favours
+// take more groups and the workgroup's waves end together: with a static deal the
+// waves of a 20-batch launch ended between 40 % and 100 % of its span
+// (tools/list_timeline.py, profiles/r02d_list_timeline_*).
 struct VrIt {
-    uint32_t b, j, J;   // batch, the wave's group ordinal in it, the wave's share of it
-    uint32_t w;         // the wave's position in the batch's deal (VrBatch::rot)
+    uint32_t b;         // batch
+    uint64_t g;         // global group
 };
 
 // 64 VGPRs (8 waves per SIMD: two 16-wave workgroups per CU), of which the compiler
@@ -338,41 +345,35 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
     auto lane_p = [&]() __attribute__((always_inline)) { return lane >> LG; };         // packet of the group
     const uint64_t zero = reinterpret_cast<uint64_t>(tb.zero);
 
-    // ---- the wave's group sequence over the batches (wave-uniform)
-    const uint32_t wv32 = static_cast<uint32_t>(wv), wt32 = static_cast<uint32_t>(wt);
-    auto wpos = [&](uint32_t b) __attribute__((always_inline)) -> uint32_t {
-        const uint32_t r = bl.b[b].rot;                      // < wt
-        return wv32 >= r ? wv32 - r : wv32 + wt32 - r;
+    // ---- the wave's group sequence: slots of the workgroup (wave-uniform)
+    auto slot_group = [&](uint32_t sl) __attribute__((always_inline)) -> uint64_t {
+        return static_cast<uint64_t>(blockIdx.x) * kVrW + (sl & (kVrW - 1u)) + static_cast<uint64_t>(sl / kVrW) * wt;
     };
-    auto share = [&](uint32_t b) __attribute__((always_inline)) -> uint32_t {   // (no division in the kernel)
-        return bl.b[b].jq + (wpos(b) < bl.b[b].jr ? 1u : 0u);
-    };
-    // the batches this wave has groups in (bit b), so that moving to the next one
-    // is a bit scan: no loop inside the streaming loop
-    uint64_t live = 0;
-    for (uint32_t b = 0; b < bl.count; ++b) live |= share(b) ? 1ull << b : 0ull;
-    // the next group after `it`, false (it unchanged) past the wave's last group
-    auto advance = [&](VrIt& it) __attribute__((always_inline)) -> bool {
-        const bool in_batch = it.j + 1u < it.J;
-        const uint64_t rest = live & (~1ull << it.b);        // batches after it.b (it.b < 48)
-        if (!in_batch && !rest) return false;
-        const uint32_t nbt = static_cast<uint32_t>(__builtin_ctzll(rest | (1ull << 63)));
-        it.j = in_batch ? it.j + 1u : 0u;
-        it.J = in_batch ? it.J : share(nbt);
-        it.w = in_batch ? it.w : wpos(nbt);
-        it.b = in_batch ? it.b : nbt;
+    // `it` moved to global group gg (its batch found from it.b on: a wave's groups
+    // ascend); false past the launch's last group
+    auto locate = [&](VrIt& it, uint64_t gg) __attribute__((always_inline)) -> bool {
+        if (gg >= bl.groups) return false;
+        while (it.b + 1u < bl.count && gg >= bl.b[it.b + 1u].g0) ++it.b;
+        it.g = gg;
         return true;
     };
-    auto group_base = [&](const VrIt& it) __attribute__((always_inline)) -> uint64_t {   // its first packet
-        return (it.w + static_cast<uint64_t>(it.j) * wt) * kPk;
+    uint32_t taken = 0;                                      // slots this wave has taken
+    // the next slot: the first two static, later ones from the workgroup's counter
+    auto take = [&]() __attribute__((always_inline)) -> uint32_t {
+        if (taken++ < 2u) return wave + kVrW * (taken - 1u);
+        uint32_t sl = 0;
+        if ((threadIdx.x & 63u) == 0u)
+            sl = __atomic_fetch_add(reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(
+                                        static_cast<uintptr_t>(BIN ? kVrCtrBin : kVrCtr)),
+                                    1u, __ATOMIC_RELAXED);
+        return __builtin_amdgcn_readfirstlane(sl);
     };
-    const bool any = live != 0u;
-    VrIt pit{0u, 0u, 0u, 0u};                                // the producer's group
-    if (any) {
-        pit.b = static_cast<uint32_t>(__builtin_ctzll(live));
-        pit.J = share(pit.b);
-        pit.w = wpos(pit.b);
-    }
+    auto advance = [&](VrIt& it) __attribute__((always_inline)) -> bool { return locate(it, slot_group(take())); };
+    auto group_base = [&](const VrIt& it) __attribute__((always_inline)) -> uint64_t {   // its first packet
+        return (it.g - bl.b[it.b].g0) * kPk;
+    };
+    VrIt pit{0u, 0u};                                        // the producer's group
+    const bool any = advance(pit);
     VrIt qit = pit;                                          // the group whose metadata is loaded
     bool qlive = any && advance(qit);
 
@@ -416,7 +417,7 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
             vr_issue_meta(reinterpret_cast<uint64_t>(B.len + base) + 4u * q,
                           reinterpret_cast<uint64_t>(B.off + base) + 8u * q, mbase);
     };
-    load_meta(any ? pit : VrIt{0u, 0u, 0u, 0u});             // (batch 0 exists: count >= 1)
+    load_meta(any ? pit : VrIt{0u, 0u});                     // (batch 0 exists: count >= 1)
     vr_wait_meta<0, BIN>(mbase, lane, mL, moff, midx);       // basis row and metadata have landed
     mark(1);
 
@@ -497,6 +498,9 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
     // writes rows w + 16 i: row j = XOR of basis rows b with bit b of j set (Gray
     // order: one XOR per row), except the INIT and CINV dwords (not linear in j),
     // whose rows < 64 come from basis rows 8 and 9.  Raw s_barrier: no vmcnt drain.
+    // the slot counter: slots 0 .. 2 kVrW - 1 are taken statically; the first dynamic
+    // take comes after barrier B (a wave's second group is entered in the loop)
+    if (threadIdx.x == 0u) lds_store(BIN ? kVrCtrBin : kVrCtr, 2u * kVrW);
     __builtin_amdgcn_s_barrier();                            // (A) every basis row has landed
     {
         uint32_t bb[8];
@@ -679,20 +683,15 @@ int vring_launch_list(int lg, int max_wgs, bool nt, int abl, hipStream_t st, con
         if (bl.b[b].n) a.b[a.count++] = bl.b[b];
     if (a.count == 0) return 0;
     const uint64_t kpk = 64u >> lg;
-    uint64_t groups = 0;                                     // all batches' groups set the grid
-    for (uint32_t b = 0; b < a.count; ++b) groups += (a.b[b].n + kpk - 1u) / kpk;
-    const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(
-        1, std::min<uint64_t>((groups + kVrW - 1) / kVrW, static_cast<uint64_t>(max_wgs))));
-    const uint64_t waves = static_cast<uint64_t>(grid) * kVrW;
-    uint64_t dealt = 0;
-    for (uint32_t b = 0; b < a.count; ++b) {
-        const uint64_t g = (a.b[b].n + kpk - 1u) / kpk;
-        if (g / waves > 0xFFFFFFFFull) return -static_cast<int>(hipErrorInvalidValue);
-        a.b[b].jq = static_cast<uint32_t>(g / waves);
-        a.b[b].jr = static_cast<uint32_t>(g % waves);
-        a.b[b].rot = static_cast<uint32_t>(dealt % waves);
-        dealt += g;
+    for (uint32_t b = 0; b < a.count; ++b) {                 // the concatenated group space
+        a.b[b].g0 = a.groups;
+        a.groups += (a.b[b].n + kpk - 1u) / kpk;
     }
+    const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(
+        1, std::min<uint64_t>((a.groups + kVrW - 1) / kVrW, static_cast<uint64_t>(max_wgs))));
+    // slots are 32-bit: a workgroup's slot count (rounds x 16) must fit
+    if ((a.groups / (static_cast<uint64_t>(grid) * kVrW) + 2u) * kVrW > 0xFFFFFFF0ull)
+        return -static_cast<int>(hipErrorInvalidValue);
     void* args[] = {&a, const_cast<KernelTables*>(&tb), const_cast<const uint32_t**>(&basis2), &trace};
     const void* fn = bin ? vring_pick_bin(lg) : vring_pick(lg, trace != nullptr, nt, abl);
     const hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(64 * kVrW), args, bin ? kVrLdsBin : kVrLds, st);
@@ -705,8 +704,8 @@ int vring_launch(int lg, int max_wgs, bool nt, hipStream_t st, const PacketArgs&
     VrBatches bl{};
     bl.count = 1;
     // binned records: the record array rides in the offsets field (BIN instance)
-    bl.b[0] = pa.meta4 ? VrBatch{pa.bytes, reinterpret_cast<const uint64_t*>(pa.meta4), nullptr, pa.out, pa.n}
-                       : VrBatch{pa.bytes, pa.off, pa.len, pa.out, pa.n};
+    bl.b[0] = pa.meta4 ? VrBatch{pa.bytes, reinterpret_cast<const uint64_t*>(pa.meta4), nullptr, pa.out, pa.n, 0u}
+                       : VrBatch{pa.bytes, pa.off, pa.len, pa.out, pa.n, 0u};
     return vring_launch_list(lg, max_wgs, nt, 0, st, bl, tb, basis2, pa.meta4 ? nullptr : pa.trace, pa.meta4 != nullptr);
 }
 

@@ -21,18 +21,16 @@ struct VrBatch {
     const uint32_t* len;
     uint32_t* out;
     uint64_t n;
-    // set by vring_launch_list: the batch's G = ceil(n / packets per group) groups
-    // as G = jq * waves + jr over the launch's waves, dealt from wave rot on (the
-    // running group count of the batches before it, mod waves): wave w has position
-    // w' = (w - rot) mod waves in the batch, takes groups w', w' + waves, ... --
-    // jq + (w' < jr) of them -- so short batches fill the waves the ones before left
-    uint32_t jq, jr, rot, pad;
+    // set by vring_launch_list: the batch's first group in the launch's concatenated
+    // group space (its G = ceil(n / packets per group) groups follow)
+    uint64_t g0;
 };
 // Kernel-argument block (<= 4 KiB): up to kVrMaxBatches batches per launch.
 constexpr int kVrMaxBatches = 48;
 struct VrBatches {
     uint32_t count;
     uint32_t pad;
+    uint64_t groups;    // all batches' groups (set by vring_launch_list)
     VrBatch b[kVrMaxBatches];
 };
 static_assert(sizeof(VrBatches) <= 3072, "kernel arguments");
