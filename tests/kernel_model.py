@@ -618,3 +618,57 @@ def vring_packet(arena: bytes, addr: int, L: int, P: int, lane_base: int = 0) ->
     if tz:
         total = mulmod(total, img[cinv_addr(tz) // 4])
     return finalize(total)
+
+
+# ---------------------------------------------------------------- vring slots
+def vring_slot_group(blk: int, sl: int, wt: int, W: int = 16) -> int:
+    """crc32_vring.hip slot_group: workgroup blk's slot sl is global group
+    16 blk + sl % 16 + (sl / 16) wt (wt = the launch's waves)."""
+    return W * blk + (sl % W) + (sl // W) * wt
+
+
+def vring_dynamic_deal(batch_groups, grid: int, rng, W: int = 16):
+    """Simulate one launch of the vring kernel's dynamic slots: every wave takes
+    slots wave and 16 + wave, then slots from its workgroup's counter (starting at
+    32) in a random interleaving of the workgroup's waves, until a slot maps past
+    the last group.  Returns {global group: (batch, local group)} as the waves
+    processed them, and the groups per wave."""
+    g0, total = [], 0
+    for n in batch_groups:
+        g0.append(total)
+        total += n
+    wt = grid * W
+    seen, per_wave = {}, []
+
+    def locate(b, gg):
+        while b + 1 < len(g0) and gg >= g0[b + 1]:
+            b += 1
+        return b
+
+    for blk in range(grid):
+        ctr = 2 * W
+        cur = {w: [0, 0, True] for w in range(W)}           # cursor batch, taken, alive
+        count = [0] * W
+        order = []
+        while any(c[2] for c in cur.values()):
+            w = rng.choice([x for x, c in cur.items() if c[2]])
+            c = cur[w]
+            if c[1] < 2:
+                sl = w + W * c[1]
+            else:
+                sl = ctr
+                ctr += 1
+            c[1] += 1
+            gg = vring_slot_group(blk, sl, wt, W)
+            if gg >= total:
+                c[2] = False
+                continue
+            b = locate(c[0], gg)
+            assert b >= c[0], "a wave's groups ascend, so its batch cursor only moves forward"
+            c[0] = b
+            assert gg not in seen, f"group {gg} taken twice"
+            seen[gg] = (b, gg - g0[b])
+            count[w] += 1
+            order.append(w)
+        per_wave.extend(count)
+    return seen, per_wave, total

@@ -247,3 +247,22 @@ def test_vring_model_matches_oracle(P):
         got = km.vring_packet(arena, 128 + a, L, P, lane_base)
         exp = ol.crc32(arena[128 + a:128 + a + L])
         assert got == exp, (a, L, P, hex(got), hex(exp))
+
+
+@pytest.mark.parametrize("batch_groups,grid", [([4096] * 5, 512), ([1], 1), ([0, 3, 0, 17], 2),
+                                               ([5000, 1, 70, 2, 800], 300), ([33] * 48, 7)])
+def test_vring_dynamic_slots_cover_every_group_once(batch_groups, grid):
+    """The vring kernel's dynamic slots (crc32_vring.hip slot_group / take / locate):
+    whatever order a workgroup's waves take slots in, every group of every batch is
+    processed exactly once, in its own batch, and each wave's groups ascend."""
+    import random
+    from kernel_model import vring_dynamic_deal
+    rng = random.Random(sum(batch_groups) + grid)
+    nonempty = [n for n in batch_groups if n]                 # (the host drops empty batches)
+    grid = max(1, min(grid, (sum(nonempty) + 15) // 16))      # (the host's grid rule)
+    seen, per_wave, total = vring_dynamic_deal(nonempty, grid, rng)
+    assert sorted(seen) == list(range(total))
+    g0 = [sum(nonempty[:b]) for b in range(len(nonempty))]
+    for gg, (b, local) in seen.items():
+        assert 0 <= local < nonempty[b] and g0[b] + local == gg
+    assert sum(per_wave) == total
