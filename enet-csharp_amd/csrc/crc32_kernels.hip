@@ -1091,6 +1091,8 @@ constexpr int kLeanPath0 = 2 + kNumStreamGeoms + kNumVStreamGeoms;
 constexpr int kVringPath = kLeanPath0 + kLeanGeoms;     // crc32_vring.hip (path 0 for checksum batches)
 constexpr int kVringAltPath = kVringPath + 1;           // the same with the other stage-load cache policy
 constexpr bool kVringNt = false;                        // the default policy: nontemporal stage loads
+constexpr int kVringWalkPath = kVringAltPath + 1;       // vring, workgroups walking contiguous group ranges
+constexpr int kVringWalkAltPath = kVringWalkPath + 1;   // the same with the other stage-load cache policy
 
 template <size_t I = 0>
 void launch_stream(int geom, int mode, int abl, int num_cus, uint64_t groups, hipStream_t st,
@@ -1144,9 +1146,12 @@ int setup_stream() {
 // at most 2: the LDS and 64-VGPR budget of two 16-wave workgroups)
 int vring_wgs(const enet_hip_context* ctx) { return ctx->wgs_per_cu >= 2 ? 2 : 1; }
 bool vring_path(const enet_hip_context* ctx) {
-    return ctx->path == 0 || ctx->path == kVringPath || ctx->path == kVringAltPath;
+    return ctx->path == 0 || (ctx->path >= kVringPath && ctx->path <= kVringWalkAltPath);
 }
-bool vring_nt(const enet_hip_context* ctx) { return ctx->path == kVringAltPath ? !kVringNt : kVringNt; }
+bool vring_nt(const enet_hip_context* ctx) {
+    return (ctx->path == kVringAltPath || ctx->path == kVringWalkAltPath) ? !kVringNt : kVringNt;
+}
+bool vring_walk(const enet_hip_context* ctx) { return ctx->path == kVringWalkPath || ctx->path == kVringWalkAltPath; }
 
 int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStream_t st) {
     if (pa.n == 0) return 0;
@@ -1160,7 +1165,7 @@ int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStr
     if (mode == 0 && (pa.lg == 2 || pa.lg == 3) && ctx->ablation == 0 && vring_path(ctx) &&
         (!pa.meta4 || ctx->path != 0))
         return vring_launch(pa.lg, ctx->num_cus * (pa.meta4 ? 1 : vring_wgs(ctx)), vring_nt(ctx) && !pa.meta4, st, pa,
-                            tb, ctx->d_basis2);
+                            tb, ctx->d_basis2, vring_walk(ctx));
     if (ctx->path != 1 && pa.lg >= 2 && pa.lg <= 4) {
         const bool lean_path = (ctx->path >= kLeanPath0 && ctx->path < kVringPath) || (ctx->path == 0 && ctx->ablation == 0);
         if (lean_path && pa.lg <= 3)
@@ -1310,7 +1315,7 @@ int enet_hip_diag_trace(enet_hip_context* ctx, uint64_t* deviceBuffer) {
 }
 
 int enet_hip_set_kernel_path(enet_hip_context* ctx, int path) {
-    if (!ctx || path < 0 || path > kVringAltPath) return -static_cast<int>(hipErrorInvalidValue);
+    if (!ctx || path < 0 || path > kVringWalkAltPath) return -static_cast<int>(hipErrorInvalidValue);
     ctx->path = path;
     return 0;
 }
@@ -1367,7 +1372,7 @@ int enet_hip_crc32_batch_list_device(enet_hip_context* ctx, const ENetHipBatch* 
                 bl.b[bl.count++] = VrBatch{batches[b].bytes, batches[b].offsets, batches[b].lengths, batches[b].out,
                                            static_cast<uint64_t>(batches[b].count), 0u};
             const int rc = vring_launch_list(lg, ctx->num_cus * vring_wgs(ctx), vring_nt(ctx), ctx->vr_abl, st, bl, tb,
-                                             ctx->d_basis2, ctx->trace);
+                                             ctx->d_basis2, ctx->trace, false, vring_walk(ctx) && !ctx->trace);
             if (rc) return rc;
         }
         return 0;

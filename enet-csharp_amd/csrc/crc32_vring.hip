@@ -329,7 +329,7 @@ struct VrIt {
 // BIN = 1: the batch's metadata are length-binned records (VrBatch::off points at
 // them, 4 dwords per packet), read in record order; packet r's CRC goes to
 // out[record r's index] (enet_hip_crc32_batch_device_binned).  One workgroup per CU.
-template <int LG, int TR = 0, int NT = 0, int ABL = 0, int BIN = 0>
+template <int LG, int TR = 0, int NT = 0, int ABL = 0, int BIN = 0, int WK = 0>
 __global__ void __launch_bounds__(64 * kVrW) __attribute__((amdgpu_waves_per_eu(8, 8), amdgpu_num_vgpr(24)))
 crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_t* trace) {
     constexpr uint32_t P = 1u << LG, kPk = 64u >> LG;
@@ -346,7 +346,13 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
     const uint64_t zero = reinterpret_cast<uint64_t>(tb.zero);
 
     // ---- the wave's group sequence: slots of the workgroup (wave-uniform)
+    // WK = 1 (walks): workgroup k owns the contiguous groups [k gw, (k + 1) gw) of the
+    // concatenated space and takes them in order, so its waves walk one region of
+    // the arena front to back (the access shape of tools/streamprobe.hip's chunk
+    // and sub-stream probes) instead of a round of 16 groups every wt groups
+    const uint64_t gw = WK ? (bl.groups + gridDim.x - 1u) / gridDim.x : 0u;
     auto slot_group = [&](uint32_t sl) __attribute__((always_inline)) -> uint64_t {
+        if constexpr (WK) return sl < gw ? static_cast<uint64_t>(blockIdx.x) * gw + sl : ~0ull;
         return static_cast<uint64_t>(blockIdx.x) * kVrW + (sl & (kVrW - 1u)) + static_cast<uint64_t>(sl / kVrW) * wt;
     };
     // `it` moved to global group gg (its batch found from it.b on: a wave's groups
@@ -635,9 +641,9 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
 
 // ---------------------------------------------------------------- host side
 
-template <int LG, int TR = 0, int NT = 0, int ABL = 0, int BIN = 0>
+template <int LG, int TR = 0, int NT = 0, int ABL = 0, int BIN = 0, int WK = 0>
 const void* vring_fn() {
-    return reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR, NT, ABL, BIN>);
+    return reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK>);
 }
 const void* vring_pick_bin(int lg) { return lg == 2 ? vring_fn<2, 0, 0, 0, 1>() : vring_fn<3, 0, 0, 0, 1>(); }
 
@@ -646,7 +652,10 @@ const void* vring_pick_bin(int lg) { return lg == 2 ? vring_fn<2, 0, 0, 0, 1>() 
 // with the nontemporal cache policy.  Measured and not kept: 3 and 4 ring slots and
 // a binned-records variant (its record register was copied by hipcc between load
 // and wait: tools/isa_inflight_check.py).
-const void* vring_pick(int lg, bool trace, bool nt, int abl) {
+const void* vring_pick(int lg, bool trace, bool nt, int abl, bool walk) {
+    if (walk && !trace && !abl)
+        return lg == 2 ? (nt ? vring_fn<2, 0, 1, 0, 0, 1>() : vring_fn<2, 0, 0, 0, 0, 1>())
+                       : (nt ? vring_fn<3, 0, 1, 0, 0, 1>() : vring_fn<3, 0, 0, 0, 0, 1>());
     if (abl == 8 && lg == 3 && !trace) return nt ? vring_fn<3, 0, 1, 8>() : vring_fn<3, 0, 0, 8>();
     if (abl == 19 && lg == 2 && !trace && !nt) return vring_fn<2, 0, 0, 19>();
     if (abl == 27 && lg == 3 && !trace) return nt ? vring_fn<3, 0, 1, 27>() : vring_fn<3, 0, 0, 27>();
@@ -662,7 +671,13 @@ const void* vring_pick(int lg, bool trace, bool nt, int abl) {
 int vring_setup() {
     for (int lg = 2; lg <= 3; ++lg)
         for (int t = 0; t < 256; ++t) {
-            const hipError_t e = hipFuncSetAttribute(vring_pick(lg, t & 1, (t >> 1) & 1, t >> 2),
+            const hipError_t e = hipFuncSetAttribute(vring_pick(lg, t & 1, (t >> 1) & 1, t >> 2, false),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, kVrLds);
+            if (e != hipSuccess) return -static_cast<int>(e);
+        }
+    for (int lg = 2; lg <= 3; ++lg)
+        for (int nt = 0; nt < 2; ++nt) {
+            const hipError_t e = hipFuncSetAttribute(vring_pick(lg, false, nt != 0, 0, true),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, kVrLds);
             if (e != hipSuccess) return -static_cast<int>(e);
         }
@@ -674,7 +689,7 @@ int vring_setup() {
 }
 
 int vring_launch_list(int lg, int max_wgs, bool nt, int abl, hipStream_t st, const VrBatches& bl, const KernelTables& tb,
-                      const uint32_t* basis2, uint64_t* trace, bool bin) {
+                      const uint32_t* basis2, uint64_t* trace, bool bin, bool walk) {
     if ((lg != 2 && lg != 3) || bl.count > static_cast<uint32_t>(kVrMaxBatches))
         return -static_cast<int>(hipErrorInvalidValue);
     // empty batches dropped: the kernel may then read any batch's packet n - 1
@@ -693,20 +708,21 @@ int vring_launch_list(int lg, int max_wgs, bool nt, int abl, hipStream_t st, con
     if ((a.groups / (static_cast<uint64_t>(grid) * kVrW) + 2u) * kVrW > 0xFFFFFFF0ull)
         return -static_cast<int>(hipErrorInvalidValue);
     void* args[] = {&a, const_cast<KernelTables*>(&tb), const_cast<const uint32_t**>(&basis2), &trace};
-    const void* fn = bin ? vring_pick_bin(lg) : vring_pick(lg, trace != nullptr, nt, abl);
+    const void* fn = bin ? vring_pick_bin(lg) : vring_pick(lg, trace != nullptr, nt, abl, walk);
     const hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(64 * kVrW), args, bin ? kVrLdsBin : kVrLds, st);
     return e == hipSuccess ? 0 : -static_cast<int>(e);
 }
 
 int vring_launch(int lg, int max_wgs, bool nt, hipStream_t st, const PacketArgs& pa, const KernelTables& tb,
-                 const uint32_t* basis2) {
+                 const uint32_t* basis2, bool walk) {
     if (pa.n == 0) return 0;
     VrBatches bl{};
     bl.count = 1;
     // binned records: the record array rides in the offsets field (BIN instance)
     bl.b[0] = pa.meta4 ? VrBatch{pa.bytes, reinterpret_cast<const uint64_t*>(pa.meta4), nullptr, pa.out, pa.n, 0u}
                        : VrBatch{pa.bytes, pa.off, pa.len, pa.out, pa.n, 0u};
-    return vring_launch_list(lg, max_wgs, nt, 0, st, bl, tb, basis2, pa.meta4 ? nullptr : pa.trace, pa.meta4 != nullptr);
+    return vring_launch_list(lg, max_wgs, nt, 0, st, bl, tb, basis2, pa.meta4 ? nullptr : pa.trace, pa.meta4 != nullptr,
+                             walk && !pa.meta4);
 }
 
 }  // namespace enethip

@@ -43,7 +43,9 @@ int vring_setup();
 // count: one per CU; twice that: two); nt = nontemporal stage loads;
 // abl = diagnostics ablation (0 in the product, crc32_vring.hip).  trace = per-wave timestamps or null.
 int vring_launch_list(int lg, int max_wgs, bool nt, int abl, hipStream_t st, const VrBatches& bl, const KernelTables& tb,
-                      const uint32_t* basis2, uint64_t* trace, bool bin = false);
+                      const uint32_t* basis2, uint64_t* trace, bool bin = false, bool walk = false);
+// walk = each workgroup takes a contiguous range of the launch's groups in order
+// (its waves walk one region of the arena) instead of rounds spread over the chip.
 
 // bin = the batches' metadata are length-binned records {len, off_lo, off_hi,
 // index} (VrBatch::off points at them, len unused): results go to out[index];
@@ -52,6 +54,6 @@ int vring_launch_list(int lg, int max_wgs, bool nt, int abl, hipStream_t st, con
 // (lg = 2 or 3), at most max_wgs workgroups; pa.meta4 set = binned records.  basis2 = kVrBasisDwords per image (images for
 // P = 1, 4, 8, 16 in that order).  Returns 0 or -hipError_t.
 int vring_launch(int lg, int max_wgs, bool nt, hipStream_t st, const PacketArgs& pa, const KernelTables& tb,
-                 const uint32_t* basis2);
+                 const uint32_t* basis2, bool walk = false);
 
 }  // namespace enethip

@@ -421,7 +421,7 @@ def test_vring_many_groups(ctx, oracle_lib):
     big = workloads.mixed(40_000, 2000, 9000, seed=179, len_seed=180)
     exp_b = oracle_lib.batch(big.payload, big.off, big.lens, threads=16)
     try:
-        for path in (0, 17, 18):               # 18: the other stage-load cache policy
+        for path in (0, 17, 18, 19, 20):       # 18: the other stage-load cache policy; 19, 20: walks
             ctx.set_kernel_path(path)
             for lanes in (4, 8):
                 assert (run_batch(ctx, tiny.payload, tiny.off, tiny.lens, lanes) == exp_t).all(), ("tiny", path, lanes)
@@ -462,7 +462,8 @@ def _run_list(ctx, cases):
     return [o.cpu().numpy().view(np.uint32)[:len(c[1])] for o, c in zip(outs, cases)]
 
 
-LIST_PATHS = (0, 13)          # 0: the vring kernel (default), 13: the lean kernel's list instance
+LIST_PATHS = (0, 13, 19, 20)  # 0: the vring kernel (default), 13: the lean kernel's list instance,
+                              # 19 / 20: the vring kernel with workgroups walking contiguous ranges
 
 
 @pytest.mark.parametrize("path", LIST_PATHS)

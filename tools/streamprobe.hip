@@ -290,6 +290,67 @@ __global__ void __launch_bounds__(1024) sp_burst(const uint8_t* bytes, uint64_t 
     if (acc == 0x9E3779B9u) sink[0] = acc;
 }
 
+// Sub-streams (round 2, the linear-stream CRC design): the batch is cut into one
+// contiguous region per group of G lanes (G = 16, 32 or 64); a group reads U
+// instructions of 16 G contiguous bytes per iteration (lane k: 16 k), i.e. whole
+// lines, and folds each 16-B piece with 16 LDS lookups chained through acc.
+// PF = 1: the next iteration's loads are issued before the current one is folded.
+template <int G, int U, bool NT, int PF>
+__global__ void __launch_bounds__(1024) sp_sub(const u32x4* p, uint64_t nvec, uint32_t* sink) {
+    extern __shared__ uint32_t tab[];
+    for (uint32_t i = threadIdx.x; i < 16384u; i += 1024u) tab[i] = i * 0x9E3779B9u;
+    __syncthreads();
+    uint32_t acc = 0;
+    const uint32_t col = (threadIdx.x & 31u) << 2;
+    const uint64_t ng = static_cast<uint64_t>(gridDim.x) * (1024u / G);
+    const uint64_t gi = static_cast<uint64_t>(blockIdx.x) * (1024u / G) + threadIdx.x / G;
+    const uint32_t k = threadIdx.x % G;
+    const uint64_t per = (nvec + ng - 1) / ng;
+    const uint64_t lo = per * gi, hi = lo + per < nvec ? lo + per : nvec;
+    auto ld = [&](uint64_t c, u32x4 (&v)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = c + static_cast<uint64_t>(G) * u + k;
+            const u32x4* q = p + (i < hi ? i : lo);
+            v[u] = NT ? __builtin_nontemporal_load(q) : *q;
+        }
+    };
+    auto fold = [&](const u32x4 (&v)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t w[4] = {v[u].x ^ acc, v[u].y, v[u].z, v[u].w};
+            uint32_t r = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    r ^= tab[(__builtin_amdgcn_perm(w[q], col, 0x0C0C0000u | ((4u + b) << 8)) >> 2) & 16383u];
+            acc = r;
+        }
+    };
+    const uint64_t step = static_cast<uint64_t>(G) * U;
+    if (lo < hi) {
+        if (PF) {
+            u32x4 cur[U];
+            ld(lo, cur);
+            for (uint64_t c = lo; c < hi; c += step) {
+                u32x4 nxt[U];
+                if (c + step < hi) ld(c + step, nxt);
+                fold(cur);
+#pragma unroll
+                for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+            }
+        } else {
+            for (uint64_t c = lo; c < hi; c += step) {
+                u32x4 v[U];
+                ld(c, v);
+                fold(v);
+            }
+        }
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
 extern "C" {
 
 static int sp_attr() {
@@ -312,12 +373,22 @@ static int sp_attr() {
         hipFuncSetAttribute(reinterpret_cast<const void*>(sp_burst<4, 2, 1>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
         hipFuncSetAttribute(reinterpret_cast<const void*>(sp_burst<4, 4, 1>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
         hipFuncSetAttribute(reinterpret_cast<const void*>(sp_burst<8, 2, 1>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_sub<16, 2, true, 0>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_sub<16, 2, false, 0>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_sub<16, 4, true, 0>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_sub<64, 2, true, 0>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_sub<64, 4, true, 0>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_sub<16, 2, true, 1>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_sub<16, 4, true, 1>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_sub<64, 2, true, 1>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_sub<32, 2, true, 0>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_sub<32, 2, true, 1>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
         done = 1;
     }
     return 0;
 }
 
-int sp_ncfg() { return 54; }
+int sp_ncfg() { return 67; }
 
 const char* sp_name(int cfg) {
     static const char* n[] = {"stride U4 g2048x256",   "stride U8 g2048x256",   "stride U4 nt g2048x256",
@@ -338,8 +409,9 @@ const char* sp_name(int cfg) {
                               "burst P4 D1 x W16",     "burst P4 D2 x W8",      "burst P4 D4 x W8",
                               "burst P4 D4 x W4",      "burst P4 D2 x W16",     "burst P4 D4 x W16",
                               "burst P4 D1 fold W16",  "burst P4 D2 fold W8",   "burst P4 D4 fold W8",
-                              "burst P4 D2 fold W16",  "burst P4 D4 fold W16",  "burst P8 D2 fold W8"};
-    return cfg >= 0 && cfg < 54 ? n[cfg] : "?";
+                              "burst P4 D2 fold W16",  "burst P4 D4 fold W16",  "burst P8 D2 fold W8",
+                              "sub G16 U2 nt g256", "sub G16 U2 g256", "sub G16 U4 nt g256", "sub G64 U2 nt g256", "sub G64 U4 nt g256", "sub G16 U2 nt pf g256", "sub G16 U4 nt pf g256", "sub G64 U2 nt pf g256", "sub G16 U2 nt g512", "sub G32 U2 nt g256", "sub G32 U2 nt pf g256", "chunkfold U2 nt g256", "sub G16 U2 nt pf g512"};
+    return cfg >= 0 && cfg < 67 ? n[cfg] : "?";
 }
 
 // nbytes: multiple of 16; for the packet shapes, npk packets of L bytes back to back
@@ -406,6 +478,19 @@ int sp_run(int cfg, const void* buf, uint64_t nbytes, uint32_t L, const void* ze
         case 51: sp_burst<4, 2, 1><<<256, 1024, 65536, st>>>(b8, npk, L, z8, sink); break;
         case 52: sp_burst<4, 4, 1><<<256, 1024, 65536, st>>>(b8, npk, L, z8, sink); break;
         case 53: sp_burst<8, 2, 1><<<256, 512, 65536, st>>>(b8, npk, L, z8, sink); break;
+        case 54: sp_sub<16, 2, true, 0><<<256, 1024, 65536, st>>>(p, nvec, sink); break;
+        case 55: sp_sub<16, 2, false, 0><<<256, 1024, 65536, st>>>(p, nvec, sink); break;
+        case 56: sp_sub<16, 4, true, 0><<<256, 1024, 65536, st>>>(p, nvec, sink); break;
+        case 57: sp_sub<64, 2, true, 0><<<256, 1024, 65536, st>>>(p, nvec, sink); break;
+        case 58: sp_sub<64, 4, true, 0><<<256, 1024, 65536, st>>>(p, nvec, sink); break;
+        case 59: sp_sub<16, 2, true, 1><<<256, 1024, 65536, st>>>(p, nvec, sink); break;
+        case 60: sp_sub<16, 4, true, 1><<<256, 1024, 65536, st>>>(p, nvec, sink); break;
+        case 61: sp_sub<64, 2, true, 1><<<256, 1024, 65536, st>>>(p, nvec, sink); break;
+        case 62: sp_sub<16, 2, true, 0><<<512, 1024, 65536, st>>>(p, nvec, sink); break;
+        case 63: sp_sub<32, 2, true, 0><<<256, 1024, 65536, st>>>(p, nvec, sink); break;
+        case 64: sp_sub<32, 2, true, 1><<<256, 1024, 65536, st>>>(p, nvec, sink); break;
+        case 65: sp_chunkfold<2, true><<<256, 1024, 65536, st>>>(p, nvec, sink); break;
+        case 66: sp_sub<16, 2, true, 1><<<512, 1024, 65536, st>>>(p, nvec, sink); break;
         default: return -1;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
