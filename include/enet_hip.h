@@ -81,7 +81,9 @@ ENET_HIP_API int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet
  * verify and the length-binned entries the lean LDS-DMA kernel (crc32_lean.hip),
  * 16 lanes the LDS-ring stream kernel, other lane counts the direct kernel.
  * Tuning sweeps: 1 = direct loads only, 2 + k = stream kernel geometry k (k < 11),
- * 13 + g = lean kernel geometry g (g < 4), 17 = the vring kernel. */
+ * 13 + g = lean kernel geometry g (g < 4), 17 = the vring kernel, 18 = the same
+ * with the other stage-load cache policy, 19 / 20 = the vring kernel with each
+ * workgroup walking a contiguous range of groups (plain / nontemporal loads). */
 ENET_HIP_API int enet_hip_set_kernel_path(enet_hip_context* ctx, int path);
 
 /* ---- batched checksum, device-resident ----

@@ -78,7 +78,7 @@ def main():
                 us = region_us(torch, st, fn, reps)
                 print(json.dumps({"kind": "probe", "name": lib.sp_name(cfg).decode(), "MB": size / 1e6,
                                   "us": round(us, 2), "GBps": round(size / us / 1e3, 1)}), flush=True)
-    if what in ("list", "all", "abl", "abl8", "pol"):
+    if what in ("list", "all", "abl", "abl8", "pol", "ls"):
         import enethip
         lanes = int(os.environ.get("SP_LANES", "4"))
         combos = [(w, p, 0) for w in (2, 1) for p in (17, 18)]
@@ -87,6 +87,11 @@ def main():
         if what == "abl8":
             combos = [(w, p, a) for w in (2, 1) for p in (17, 18) for a in (2048 + 4096 + 16384 + 32768,)]
             combos += [(w, 17, 2048 + 4096 + 32768) for w in (2, 1)]
+            lanes = 8
+        if what == "ls":
+            # line-shaped stage loads + 128-B windows (ABL 8, wrong CRCs by design) with the
+            # full fold, and its skeleton (ABL 27), plain (17) and nt (18), against the product
+            combos = [(w, p, a) for w in (2, 1) for p in (17, 18) for a in (0, 16384, 2048 + 4096 + 16384 + 32768)]
             lanes = 8
         if what == "pol":
             combos = [(w, p, a) for w in (2, 1) for p in (17, 18) for a in (0, 65536)]
@@ -100,7 +105,7 @@ def main():
             lens = torch.full((65536,), 1200, dtype=torch.int32, device="cuda")
             outs = [torch.zeros(65536, dtype=torch.int32, device="cuda") for _ in range(nb)]
             descs = [(big[j * BATCH:(j + 1) * BATCH + 4096], off, lens, 65536, outs[j]) for j in range(nb)]
-            for L in ((5, 20) if what.startswith("abl") or what == "pol" else (1, 2, 5, 10, 20, 40)):
+            for L in ((5, 20) if what.startswith("abl") or what in ("pol", "ls") else (1, 2, 5, 10, 20, 40)):
                 launches = max(4, 80 // L)
 
                 def fn(i, L=L):
