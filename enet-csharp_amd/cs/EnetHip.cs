@@ -49,6 +49,20 @@ namespace enet
         public uint* output;
     }
 
+    /// <summary>One batch of a receive-verify list call (include/enet_hip.h ENetHipVerifyBatch; device pointers).</summary>
+    [StructLayout(LayoutKind.Sequential)]
+    public unsafe struct ENetHipVerifyBatch
+    {
+        public byte* bytes;
+        public ulong* offsets;
+        public uint* lengths;
+        public uint* slotOffsets;
+        public uint* connectIds;
+        public nuint count;
+        public byte* ok;
+        public uint* computed;
+    }
+
     [SuppressUnmanagedCodeSecurity]
     public static unsafe class EnetHipNative
     {
@@ -114,6 +128,10 @@ namespace enet
         public static extern int enet_hip_verify_batch_device(IntPtr ctx, byte* bytes, ulong* offsets, uint* lengths,
                                                               uint* slotOffsets, uint* connectIds, nuint count,
                                                               byte* ok, uint* computed, IntPtr stream);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_verify_batch_list_device(IntPtr ctx, ENetHipVerifyBatch* batches,
+                                                                   nuint batchCount, IntPtr stream);
 
         [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
         public static extern int enet_hip_crc32_gather_device(IntPtr ctx, byte* bytes, ulong* segOffsets,
@@ -255,6 +273,11 @@ namespace enet
             => EnetHip.Check("enet_hip_verify_batch_device",
                 EnetHipNative.enet_hip_verify_batch_device(Handle, bytes, offsets, lengths, slotOffsets, connectIds,
                     count, ok, computed, stream));
+
+        /// <summary>Receive verify over a list of batches, one launch per 32 (same ok[] / computed[] as VerifyDevice per batch).</summary>
+        public void VerifyListDevice(ENetHipVerifyBatch* batches, nuint batchCount, IntPtr stream = default)
+            => EnetHip.Check("enet_hip_verify_batch_list_device",
+                EnetHipNative.enet_hip_verify_batch_list_device(Handle, batches, batchCount, stream));
 
         public void FragmentReassembleDevice(byte* bytes, ulong* cmdOffsets, uint* cmdAvail, int* slots, nuint count,
                                              uint maximumPacketSize, byte* msgBytes, ulong* msgOffsets,

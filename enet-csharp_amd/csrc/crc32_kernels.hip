@@ -1442,6 +1442,40 @@ int enet_hip_verify_batch_device(enet_hip_context* ctx, const uint8_t* bytes, co
     return launch_packets(ctx, 1, pa, stream ? static_cast<hipStream_t>(stream) : ctx->stream);
 }
 
+int enet_hip_verify_batch_list_device(enet_hip_context* ctx, const ENetHipVerifyBatch* batches, size_t batchCount,
+                                      void* stream) {
+    if (!ctx) return -static_cast<int>(hipErrorInvalidValue);
+    if (batchCount == 0) return 0;
+    if (!batches) return -static_cast<int>(hipErrorInvalidValue);
+    for (size_t b = 0; b < batchCount; ++b) {
+        const ENetHipVerifyBatch& e = batches[b];
+        if (e.count && (!e.bytes || !e.offsets || !e.lengths || !e.slotOffsets || !e.connectIds || !e.ok))
+            return -static_cast<int>(hipErrorInvalidValue);
+    }
+    ENH_CHECK(hipSetDevice(ctx->device));
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    const int lg = log2i(auto_lanes(ctx, 1));
+    // the lean kernel's verify-list instance (geometry 0) on the paths where single
+    // verify batches run the lean kernel (launch_packets, mode 1)
+    if ((lg == 2 || lg == 3) && ctx->ablation == 0 && ctx->vr_abl == 0 &&
+        (ctx->path == 0 || (ctx->path >= kLeanPath0 && ctx->path < kVringPath))) {
+        const KernelTables tb = tables_of(ctx);
+        for (size_t b0 = 0; b0 < batchCount; b0 += kLeanMaxVBatches) {
+            const int rc = lean_launch_vlist(lg, ctx->num_cus, st, batches + b0,
+                                             std::min<size_t>(batchCount - b0, kLeanMaxVBatches), tb);
+            if (rc) return rc;
+        }
+        return 0;
+    }
+    for (size_t b = 0; b < batchCount; ++b) {                // other lane counts / paths: one launch per batch
+        const ENetHipVerifyBatch& e = batches[b];
+        const int rc = enet_hip_verify_batch_device(ctx, e.bytes, e.offsets, e.lengths, e.slotOffsets, e.connectIds,
+                                                    e.count, e.ok, e.computed, st);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
 int enet_hip_verify_batch_device_binned(enet_hip_context* ctx, const uint8_t* bytes, const uint64_t* offsets,
                                         const uint32_t* lengths, const uint32_t* slotOffsets,
                                         const uint32_t* connectIds, size_t count, uint8_t* ok, uint32_t* computed,

@@ -162,12 +162,14 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
 // loads): a reference to the by-value argument made hipcc copy all 2.3 KiB of it
 // into scratch.
 using LeanListPtr = const __attribute__((address_space(4))) LeanList*;
+// receive-verify lists (MODE 1): LeanVList, the same walkers
+using LeanVListPtr = const __attribute__((address_space(4))) LeanVList*;
 
-template <int MODE, int LG, int W, int NB, int ABL, int LIST>
-__device__ __forceinline__ void lean_body(const PacketArgs& pa, const KernelTables& tb, LeanListPtr llp) {
+template <int MODE, int LG, int W, int NB, int ABL, int LIST, typename LLP = LeanListPtr>
+__device__ __forceinline__ void lean_body(const PacketArgs& pa, const KernelTables& tb, LLP llp) {
     using G = LeanGeom<MODE, LG, W, NB>;
     constexpr uint32_t P = G::P, kPk = G::kPk, JM = G::JM;
-    static_assert(!LIST || (MODE == 0 && ABL == 0), "batch lists: checksum mode, product instance");
+    static_assert(!LIST || ABL == 0, "batch lists: product instances");
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t ngroups = LIST ? llp->groups : (pa.n + kPk - 1u) >> (6 - LG);
@@ -239,7 +241,18 @@ __device__ __forceinline__ void lean_body(const PacketArgs& pa, const KernelTabl
                     ia ? uni64(reinterpret_cast<uint64_t>(llp->b[ba].len)) : uni64(reinterpret_cast<uint64_t>(llp->b[mb].len)));
                 const uint32_t* op = reinterpret_cast<const uint32_t*>(
                     ia ? uni64(reinterpret_cast<uint64_t>(llp->b[ba].off)) : uni64(reinterpret_cast<uint64_t>(llp->b[mb].off)));
-                dma4((f == 1u || f == 2u) ? op + 2u * pk + (f - 1u) : lp + pk, half + 256u * o);
+                const uint32_t* src = (f == 1u || f == 2u) ? op + 2u * pk + (f - 1u) : lp + pk;
+                if constexpr (MODE) {                        // receive verify: slot offset, connectID
+                    const uint32_t* sp = reinterpret_cast<const uint32_t*>(
+                        ia ? uni64(reinterpret_cast<uint64_t>(llp->b[ba].slot_off))
+                           : uni64(reinterpret_cast<uint64_t>(llp->b[mb].slot_off)));
+                    const uint32_t* cp = reinterpret_cast<const uint32_t*>(
+                        ia ? uni64(reinterpret_cast<uint64_t>(llp->b[ba].connect))
+                           : uni64(reinterpret_cast<uint64_t>(llp->b[mb].connect)));
+                    if (f == 3u) src = sp + pk;
+                    if (f == 4u) src = cp + pk;
+                }
+                dma4(src, half + 256u * o);
                 continue;
             }
             const uint64_t pk = min(group_of(j) * kPk + p, pa.n - 1u);
@@ -410,10 +423,12 @@ __device__ __forceinline__ void lean_body(const PacketArgs& pa, const KernelTabl
     uint32_t cj = 0, cst = 0, cstages = 0, nedge = ~0u, reg = 0, desired = 0;
     Task t{};
     uint32_t* cout = pa.out;                                 // (LIST: the consumer's batch's)
+    uint8_t* cok = pa.ok;                                    // (MODE 1)
     auto consumer_setup = [&](uint32_t j) __attribute__((always_inline)) {
         if constexpr (LIST) {
             locate(group_of(j), cb);
             cout = llp->b[cb].out;
+            if constexpr (MODE) cok = llp->b[cb].ok;
         }
         const Window w = window_of(j, cb);
         t.pk = (group_of(j) - (LIST ? llp->b[cb].g0 : 0u)) * kPk + pj_lane;
@@ -496,8 +511,8 @@ __device__ __forceinline__ void lean_body(const PacketArgs& pa, const KernelTabl
                     cout[t.pk] = finalize(reg);              // packet.cs:159
                 } else {
                     const uint32_t comp = t.slot_ok ? finalize(reg) : 0u;
-                    pa.ok[t.pk] = (t.slot_ok && comp == desired) ? 1 : 0;   // protocol.cs:1066-1068
-                    if (pa.out) pa.out[t.pk] = comp;
+                    cok[t.pk] = (t.slot_ok && comp == desired) ? 1 : 0;     // protocol.cs:1066-1068
+                    if (cout) cout[t.pk] = comp;
                 }
             }
             if (++cj == J) {
@@ -524,7 +539,7 @@ __device__ __forceinline__ void lean_body(const PacketArgs& pa, const KernelTabl
 
 template <int MODE, int LG, int W, int NB, int ABL = 0>
 __global__ void __launch_bounds__(64 * W) crc32_lean_kernel(PacketArgs pa, KernelTables tb) {
-    lean_body<MODE, LG, W, NB, ABL, 0>(pa, tb, nullptr);
+    lean_body<MODE, LG, W, NB, ABL, 0>(pa, tb, static_cast<LeanListPtr>(nullptr));
 }
 
 // batch lists (enet_hip_crc32_batch_list_device): checksum mode
@@ -536,6 +551,14 @@ __global__ void __launch_bounds__(64 * W) crc32_lean_list_kernel(LeanList ll, Ke
     lean_body<0, LG, W, NB, 0, 1>(pa, tb, (LeanListPtr)(__builtin_amdgcn_kernarg_segment_ptr()));
 }
 
+// receive-verify lists (enet_hip_verify_batch_list_device): MODE 1
+template <int LG, int W, int NB>
+__global__ void __launch_bounds__(64 * W) crc32_lean_vlist_kernel(LeanVList ll, KernelTables tb) {
+    PacketArgs pa{};
+    (void)ll;
+    lean_body<1, LG, W, NB, 0, 1, LeanVListPtr>(pa, tb, (LeanVListPtr)(__builtin_amdgcn_kernarg_segment_ptr()));
+}
+
 // ---------------------------------------------------------------- host side
 
 template <int W, int NB>
@@ -545,15 +568,17 @@ struct LeanVariant {
         return reinterpret_cast<const void*>(crc32_lean_kernel<MODE, LG, W, NB, ABL>);
     }
     static int setup() {
-        const void* fns[10] = {fn<0, 2>(), fn<0, 3>(), fn<1, 2>(), fn<1, 3>(),
+        const void* fns[12] = {fn<0, 2>(), fn<0, 3>(), fn<1, 2>(), fn<1, 3>(),
                                fn<0, 2, 128>(), fn<0, 3, 128>(), fn<1, 2, 128>(), fn<1, 3, 128>(),
                                reinterpret_cast<const void*>(crc32_lean_list_kernel<2, W, NB>),
-                               reinterpret_cast<const void*>(crc32_lean_list_kernel<3, W, NB>)};
-        const int lds[10] = {LeanGeom<0, 2, W, NB>::kLds, LeanGeom<0, 3, W, NB>::kLds, LeanGeom<1, 2, W, NB>::kLds,
+                               reinterpret_cast<const void*>(crc32_lean_list_kernel<3, W, NB>),
+                               reinterpret_cast<const void*>(crc32_lean_vlist_kernel<2, W, NB>),
+                               reinterpret_cast<const void*>(crc32_lean_vlist_kernel<3, W, NB>)};
+        const int lds[12] = {LeanGeom<0, 2, W, NB>::kLds, LeanGeom<0, 3, W, NB>::kLds, LeanGeom<1, 2, W, NB>::kLds,
                              LeanGeom<1, 3, W, NB>::kLds, LeanGeom<0, 2, W, NB>::kLds, LeanGeom<0, 3, W, NB>::kLds,
                              LeanGeom<1, 2, W, NB>::kLds, LeanGeom<1, 3, W, NB>::kLds, LeanGeom<0, 2, W, NB>::kLds,
-                             LeanGeom<0, 3, W, NB>::kLds};
-        for (int i = 0; i < 10; ++i) {
+                             LeanGeom<0, 3, W, NB>::kLds, LeanGeom<1, 2, W, NB>::kLds, LeanGeom<1, 3, W, NB>::kLds};
+        for (int i = 0; i < 12; ++i) {
             const hipError_t e = hipFuncSetAttribute(fns[i], hipFuncAttributeMaxDynamicSharedMemorySize, lds[i]);
             if (e != hipSuccess) return -static_cast<int>(e);
         }
@@ -637,6 +662,34 @@ int lean_launch_list(int lg, int num_cus, hipStream_t st, const ENetHipBatch* ba
         hipLaunchKernelGGL((crc32_lean_list_kernel<2, 16, 2>), dim3(grid), dim3(64 * 16), lds2, st, ll, tb);
     else
         hipLaunchKernelGGL((crc32_lean_list_kernel<3, 16, 2>), dim3(grid), dim3(64 * 16), lds3, st, ll, tb);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : -static_cast<int>(e);
+}
+
+// A receive-verify list: the same deal as lean_launch_list (MODE 1 metadata, 8
+// dwords per packet), one 16-wave workgroup per CU.
+int lean_launch_vlist(int lg, int num_cus, hipStream_t st, const ENetHipVerifyBatch* batches, size_t count,
+                      const KernelTables& tb) {
+    if ((lg != 2 && lg != 3) || count > static_cast<size_t>(kLeanMaxVBatches))
+        return -static_cast<int>(hipErrorInvalidValue);
+    LeanVList ll{};
+    const uint64_t kpk = 64u >> lg;
+    for (size_t i = 0; i < count; ++i) {
+        if (!batches[i].count) continue;
+        LeanVListBatch& b = ll.b[ll.count++];
+        b = LeanVListBatch{batches[i].bytes, batches[i].offsets, batches[i].lengths, batches[i].slotOffsets,
+                           batches[i].connectIds, batches[i].ok, batches[i].computed,
+                           static_cast<uint64_t>(batches[i].count), ll.groups};
+        ll.groups += (b.n + kpk - 1u) / kpk;
+    }
+    if (ll.count == 0) return 0;
+    const unsigned grid = static_cast<unsigned>(
+        std::max<uint64_t>(1, std::min<uint64_t>((ll.groups + 15u) / 16u, static_cast<uint64_t>(num_cus))));
+    constexpr int lds2 = LeanGeom<1, 2, 16, 2>::kLds, lds3 = LeanGeom<1, 3, 16, 2>::kLds;
+    if (lg == 2)
+        hipLaunchKernelGGL((crc32_lean_vlist_kernel<2, 16, 2>), dim3(grid), dim3(64 * 16), lds2, st, ll, tb);
+    else
+        hipLaunchKernelGGL((crc32_lean_vlist_kernel<3, 16, 2>), dim3(grid), dim3(64 * 16), lds3, st, ll, tb);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : -static_cast<int>(e);
 }

@@ -29,6 +29,28 @@ struct LeanList {
 };
 static_assert(sizeof(LeanList) <= 3072, "kernel arguments");   // 0: 16 waves x 2 stages, 1: 12 waves x 3 stages; sweeps: 2: 14 x 3, 3: 10 x 4
 
+// Receive-verify batch lists (lean_launch_vlist): the same, with each batch's
+// slot offsets, connectIDs and ok[] (out = the computed CRCs, may be null).
+struct LeanVListBatch {
+    const uint8_t* bytes;
+    const uint64_t* off;
+    const uint32_t* len;
+    const uint32_t* slot_off;
+    const uint32_t* connect;
+    uint8_t* ok;
+    uint32_t* out;
+    uint64_t n;
+    uint64_t g0;
+};
+constexpr int kLeanMaxVBatches = 32;
+struct LeanVList {
+    uint32_t count;
+    uint32_t pad;
+    uint64_t groups;
+    LeanVListBatch b[kLeanMaxVBatches];
+};
+static_assert(sizeof(LeanVList) <= 3072, "kernel arguments");
+
 // Set the dynamic-LDS attribute of every lean kernel instance (once per context).
 int lean_setup();
 
@@ -42,6 +64,11 @@ int lean_launch(int mode, int lg, int geom, int abl, int num_cus, hipStream_t st
 // per packet 2^lg (lg = 2 or 3).  Returns 0 or -hipError_t.
 int lean_launch_list(int lg, int num_cus, hipStream_t st, const ENetHipBatch* batches, size_t count,
                      const KernelTables& tb);
+
+// Receive-verify a list of batches (count <= kLeanMaxVBatches) in one launch at
+// lanes per packet 2^lg (lg = 2 or 3).  Returns 0 or -hipError_t.
+int lean_launch_vlist(int lg, int num_cus, hipStream_t st, const ENetHipVerifyBatch* batches, size_t count,
+                      const KernelTables& tb);
 
 // Order the packet records of each 1024-packet tile by length bin, longest first,
 // and interleave the tiles' groups of kpk records rank by rank (see

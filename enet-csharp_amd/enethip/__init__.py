@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = (
     "enet_hip_context_destroy", "enet_hip_error_string", "enet_hip_set_tuning",
     "enet_hip_crc32_batch_device", "enet_hip_crc32_batch_list_device", "enet_hip_binned_workspace_size", "enet_hip_crc32_batch_device_binned",
     "enet_hip_verify_binned_workspace_size", "enet_hip_verify_batch_device_binned",
-    "enet_hip_crc32_batch_host", "enet_hip_verify_batch_device",
+    "enet_hip_crc32_batch_host", "enet_hip_verify_batch_device", "enet_hip_verify_batch_list_device",
     "enet_hip_crc32_gather_device", "enet_hip_crc32_batch_multi", "enet_hip_device_alloc",
     "enet_hip_device_free", "enet_hip_host_alloc", "enet_hip_host_free", "enet_hip_memcpy_h2d",
     "enet_hip_memcpy_d2h", "enet_hip_synchronize", "enet_hip_read_probe_device", "enet_hip_set_kernel_path",
@@ -42,6 +42,13 @@ class ENetHipBatch(ctypes.Structure):
     """include/enet_hip.h ENetHipBatch: one batch of a batch-list call (device pointers)."""
     _fields_ = [("bytes", ctypes.c_void_p), ("offsets", ctypes.c_void_p), ("lengths", ctypes.c_void_p),
                 ("count", ctypes.c_size_t), ("out", ctypes.c_void_p)]
+
+
+class ENetHipVerifyBatch(ctypes.Structure):
+    """include/enet_hip.h ENetHipVerifyBatch: one batch of a receive-verify list call."""
+    _fields_ = [("bytes", ctypes.c_void_p), ("offsets", ctypes.c_void_p), ("lengths", ctypes.c_void_p),
+                ("slotOffsets", ctypes.c_void_p), ("connectIds", ctypes.c_void_p), ("count", ctypes.c_size_t),
+                ("ok", ctypes.c_void_p), ("computed", ctypes.c_void_p)]
 
 
 class ENetHipError(RuntimeError):
@@ -91,6 +98,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.enet_hip_crc32_batch_device.argtypes = [vp, vp, vp, vp, sz, vp, vp]
     L.enet_hip_crc32_batch_list_device.restype = i32
     L.enet_hip_crc32_batch_list_device.argtypes = [vp, vp, sz, vp]
+    L.enet_hip_verify_batch_list_device.restype = i32
+    L.enet_hip_verify_batch_list_device.argtypes = [vp, vp, sz, vp]
     L.enet_hip_binned_workspace_size.restype = sz
     L.enet_hip_binned_workspace_size.argtypes = [sz]
     L.enet_hip_crc32_batch_device_binned.restype = i32
@@ -233,6 +242,16 @@ class Context:
         for i, (b, o, l, n, out) in enumerate(batches):
             arr[i] = ENetHipBatch(_ptr(b) or None, _ptr(o) or None, _ptr(l) or None, int(n), _ptr(out) or None)
         _check("enet_hip_crc32_batch_list_device", self.lib.enet_hip_crc32_batch_list_device(
+            self.handle, ctypes.cast(arr, ctypes.c_void_p), len(batches), stream or None))
+
+    def verify_batch_list_device(self, batches, stream: int = 0) -> None:
+        """batches: sequence of (d_bytes, d_off, d_len, d_slot, d_connect, n, d_ok, d_computed or None);
+        one launch per 32 batches (c/protocol.cs:1052-1068 per DGRAM)."""
+        arr = (ENetHipVerifyBatch * max(1, len(batches)))()
+        for i, (b, o, l, so, cid, n, ok, comp) in enumerate(batches):
+            arr[i] = ENetHipVerifyBatch(_ptr(b) or None, _ptr(o) or None, _ptr(l) or None, _ptr(so) or None,
+                                        _ptr(cid) or None, int(n), _ptr(ok) or None, _ptr(comp) or None)
+        _check("enet_hip_verify_batch_list_device", self.lib.enet_hip_verify_batch_list_device(
             self.handle, ctypes.cast(arr, ctypes.c_void_p), len(batches), stream or None))
 
     def binned_workspace_size(self, n: int) -> int:

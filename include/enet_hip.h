@@ -149,6 +149,28 @@ ENET_HIP_API int enet_hip_verify_batch_device(enet_hip_context* ctx, const uint8
                                               const uint32_t* slotOffsets, const uint32_t* connectIds,
                                               size_t count, uint8_t* ok, uint32_t* computed, void* stream);
 
+/* Receive verify over a list of batches (a receive batcher's DGRAM batches,
+ * c/protocol.cs:1052-1068 per DGRAM): batches[0 .. batchCount) is a HOST array,
+ * each entry names one batch exactly as enet_hip_verify_batch_device's arguments
+ * do (device pointers; computed may be NULL).  Same ok[] / computed[] as one
+ * enet_hip_verify_batch_device call per batch, in one kernel launch per 32
+ * batches (4 or 8 lanes per packet: the lean kernel's list instance; other lane
+ * counts: one launch per batch), so the per-launch start and drain are paid once
+ * per launch.  Batches may not share ok / computed ranges.  Async;
+ * graph-capturable. */
+typedef struct {
+    const uint8_t* bytes;
+    const uint64_t* offsets;
+    const uint32_t* lengths;
+    const uint32_t* slotOffsets;
+    const uint32_t* connectIds;
+    size_t count;
+    uint8_t* ok;
+    uint32_t* computed;
+} ENetHipVerifyBatch;
+ENET_HIP_API int enet_hip_verify_batch_list_device(enet_hip_context* ctx, const ENetHipVerifyBatch* batches,
+                                                   size_t batchCount, void* stream);
+
 /* enet_hip_verify_batch_device for batches of mixed lengths: the same per-tile
  * length ordering as enet_hip_crc32_batch_device_binned, with 32-byte records
  * {len, off_lo, off_hi, slotOffset, connectId, index, 0, 0} in `workspace`

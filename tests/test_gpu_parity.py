@@ -344,6 +344,62 @@ def test_verify_batch(ctx, oracle_lib):
         assert (d_comp.cpu().numpy().view(np.uint32) == exp_comp).all()
 
 
+def _verify_list_batch(oracle_lib, rng, n):
+    """One receive batch for the list tests: half the DGRAMs stamped with their true
+    CRC (vectorised stamp), a tenth of all corrupted; the oracle's ok / computed."""
+    payload, off, lens, slot, conn = _verify_inputs(rng, n)
+    if n:
+        stamped = oracle_lib.batch(payload, off, lens, threads=8)
+        good = np.nonzero(rng.integers(0, 2, size=n) == 1)[0]
+        pos = (off[good] + slot[good]).astype(np.int64)[:, None] + np.arange(4)
+        payload[pos] = stamped[good].view(np.uint8).reshape(-1, 4)
+        bad = rng.choice(n, size=max(1, n // 10), replace=False)
+        payload[off[bad].astype(np.int64) + rng.integers(0, lens[bad].astype(np.int64))] ^= np.uint8(0x20)
+    exp_ok, exp_comp = oracle_lib.verify(payload, off, lens, slot, conn)
+    return payload, off, lens, slot, conn, exp_ok, exp_comp
+
+
+def _run_verify_list(ctx, batches, with_computed=True):
+    keep, descs, outs = [], [], []
+    for payload, off, lens, slot, conn, _, _ in batches:
+        n = len(off)
+        d = [dev(payload if len(payload) else np.zeros(16, np.uint8))] + \
+            [dev(x) if n else dev(np.zeros(1, x.dtype)) for x in (off, lens, slot, conn)]
+        ok = torch.full((max(1, n),), 7, dtype=torch.uint8, device="cuda")
+        comp = torch.full((max(1, n),), -1, dtype=torch.int32, device="cuda") if with_computed else None
+        keep.append(d)
+        outs.append((ok, comp))
+        descs.append((d[0], d[1], d[2], d[3], d[4], n, ok, comp))
+    ctx.verify_batch_list_device(descs, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return [(ok.cpu().numpy()[:len(b[1])], None if comp is None else comp.cpu().numpy().view(np.uint32)[:len(b[1])])
+            for (ok, comp), b in zip(outs, batches)]
+
+
+def test_verify_batch_list(ctx, oracle_lib):
+    """enet_hip_verify_batch_list_device: receive batches of every shape (empty,
+    one DGRAM, odd sizes, 20 000 mixed DGRAMs) in one launch, at the default, 4,
+    8 and 16 lanes (16: one launch per batch), with and without computed[]; and 70
+    batches (three launches of at most 32), each against the oracle's verify."""
+    rng = np.random.default_rng(91)
+    batches = [_verify_list_batch(oracle_lib, rng, n) for n in (0, 1, 3, 700, 20_000, 0, 5000, 33)]
+    try:
+        for lanes in (0, 4, 8, 16):
+            ctx.set_tuning(lanes, 0)
+            for wc in (True, False):
+                for i, ((ok, comp), b) in enumerate(zip(_run_verify_list(ctx, batches, wc), batches)):
+                    assert (ok == b[5]).all(), (lanes, wc, i)
+                    if wc:
+                        assert (comp == b[6]).all(), (lanes, i)
+        ctx.set_tuning(0, 0)
+        many = [_verify_list_batch(oracle_lib, rng, int(rng.integers(0, 900))) for _ in range(70)]
+        for i, ((ok, comp), b) in enumerate(zip(_run_verify_list(ctx, many), many)):
+            assert (ok == b[5]).all() and (comp == b[6]).all(), i
+        assert sum(int(b[5].sum()) for b in batches) > 0
+    finally:
+        ctx.set_tuning(0, 0)
+
+
 @pytest.mark.parametrize("n", [1, 3000, 70_000])
 def test_verify_binned(ctx, oracle_lib, n):
     """Binned receive verify: mixed-length DGRAMs (6..1400 B, 2- and 4-byte headers),
