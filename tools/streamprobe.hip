@@ -351,6 +351,96 @@ __global__ void __launch_bounds__(1024) sp_sub(const u32x4* p, uint64_t nvec, ui
     if (acc == 0x9E3779B9u) sink[0] = acc;
 }
 
+// Sub-stream with the real per-stage costs of a CRC kernel (measurement only;
+// the CRCs are not computed correctly): 16-lane groups, 4 nt stages of 256 B per
+// iteration, cfg2's 1200-B packets from the buffer start.  Per 16-B piece: the
+// register injection, the conflict-free dword shuffle and 16 LDS lookups with the
+// XOR Latin square over 16 tables x 2 copies (the layout a sub-stream CRC kernel
+// needs); per stage: the packet cursor (reset at a packet start, pending flush of
+// the old packet's register); once per iteration, if any lane has one pending:
+// the per-lane end-of-packet multiply (4 byte lookups in a 64 KiB table indexed
+// by o = (k - l_e - 1) mod 16) and the XOR over the group's 16 lanes.
+__device__ __forceinline__ uint32_t ssr_sel(uint32_t bsel, uint32_t h) {   // byte0 <- col byte h, byte1 <- data byte
+    return 0x0C0C0000u | h | ((4u + (h ^ bsel)) << 8);
+}
+template <bool NT>
+__global__ void __launch_bounds__(1024) sp_ssr(const u32x4* p, uint64_t nvec, uint32_t* sink) {
+    extern __shared__ uint32_t tab[];                        // 64 KiB fold image + 64 KiB corrections
+    for (uint32_t i = threadIdx.x; i < 32768u; i += 1024u) tab[i] = i * 0x9E3779B9u;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, k = lane & 15u, gp = (lane >> 4) & 1u;
+    const uint32_t cl = (64u * gp + 4u * k) * 0x01010101u;   // lane part of the column bytes
+    const uint32_t m1 = 0u - ((k >> 2) & 1u), m2 = 0u - ((k >> 3) & 1u);
+    const uint64_t ng = static_cast<uint64_t>(gridDim.x) * 64u;
+    const uint64_t gi = static_cast<uint64_t>(blockIdx.x) * 64u + (threadIdx.x >> 4);
+    const uint64_t per = (nvec / ng) & ~15ull;
+    const uint64_t lo = per * gi, hi = lo + per;
+    uint32_t reg = 0, pend = 0, po = 0, acc = 0;
+    bool pf = false;
+    uint64_t ec = (lo + k) / 75u * 75u + 75u;                 // end (16-B units) of the lane's packet
+    for (uint64_t c = lo; c < hi; c += 64u) {
+        u32x4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const u32x4* q = p + c + 16u * u + k;
+            v[u] = NT ? __builtin_nontemporal_load(q) : *q;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint64_t unit = c + 16u * u + k, b = c + 16u * u;
+            if (unit >= ec) {                                 // the lane's packet ended in this stage, below it
+                const uint32_t le = static_cast<uint32_t>(ec - 1u - b);
+                pend = reg;
+                po = (k - le - 1u) & 15u;
+                pf = true;
+                reg = unit == ec ? 0xFFFFFFFFu : 0u;
+                ec += 75u;
+            }
+            uint32_t w0 = v[u].x ^ reg, w1 = v[u].y, w2 = v[u].z, w3 = v[u].w;
+            // d[q] = w[q ^ (k >> 2)]
+            uint32_t x0 = __builtin_amdgcn_bitop3_b32(w1, w0, m1, 0xd8), x1 = __builtin_amdgcn_bitop3_b32(w0, w1, m1, 0xd8);
+            uint32_t x2 = __builtin_amdgcn_bitop3_b32(w3, w2, m1, 0xd8), x3 = __builtin_amdgcn_bitop3_b32(w2, w3, m1, 0xd8);
+            const uint32_t d0 = __builtin_amdgcn_bitop3_b32(x2, x0, m2, 0xd8), d2 = __builtin_amdgcn_bitop3_b32(x0, x2, m2, 0xd8);
+            const uint32_t d1 = __builtin_amdgcn_bitop3_b32(x3, x1, m2, 0xd8), d3 = __builtin_amdgcn_bitop3_b32(x1, x3, m2, 0xd8);
+            const uint32_t d[4] = {d0, d1, d2, d3};
+            uint32_t r = 0;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                uint32_t cc = 0;
+#pragma unroll
+                for (int h = 0; h < 4; ++h) cc |= (4u * (15u ^ (4u * g + h))) << (8 * h);
+                const uint32_t col = cc ^ cl;
+                uint32_t t[4];
+#pragma unroll
+                for (int h = 0; h < 4; ++h)
+                    t[h] = tab[__builtin_amdgcn_perm(d[g], col, ssr_sel(k & 3u, h)) >> 2];
+                r = __builtin_amdgcn_bitop3_b32(r, t[0], t[1], 0x96) ^ __builtin_amdgcn_bitop3_b32(t[2], t[3], 0u, 0x96);
+            }
+            reg = r;
+            if (ec <= b + 16u) {                              // the packet ends in this stage, at or above this lane
+                const uint32_t le = static_cast<uint32_t>(ec - 1u - b);
+                pend = reg;
+                po = (k + 15u - le) & 15u;
+                pf = true;
+            }
+        }
+        if (__builtin_amdgcn_ballot_w64(pf)) {                // once per iteration: end-of-packet multiplies
+            uint32_t x = 0;
+#pragma unroll
+            for (int bq = 0; bq < 4; ++bq) {
+                const uint32_t bb = static_cast<uint32_t>(bq) ^ gp;
+                const uint32_t a = 16384u + ((((pend >> (8u * bb)) & 255u) * 4u + bb) * 16u + po);
+                x ^= pf ? tab[a] : 0u;
+            }
+#pragma unroll
+            for (int o = 8; o >= 1; o >>= 1) x ^= __shfl_xor(x, o, 16);
+            acc ^= x;
+            pf = false;
+        }
+    }
+    if ((acc ^ reg) == 0x9E3779B9u) sink[0] = acc;
+}
+
 extern "C" {
 
 static int sp_attr() {
@@ -383,12 +473,14 @@ static int sp_attr() {
         hipFuncSetAttribute(reinterpret_cast<const void*>(sp_sub<64, 2, true, 1>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
         hipFuncSetAttribute(reinterpret_cast<const void*>(sp_sub<32, 2, true, 0>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
         hipFuncSetAttribute(reinterpret_cast<const void*>(sp_sub<32, 2, true, 1>), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_ssr<true>), hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(sp_ssr<false>), hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
         done = 1;
     }
     return 0;
 }
 
-int sp_ncfg() { return 67; }
+int sp_ncfg() { return 69; }
 
 const char* sp_name(int cfg) {
     static const char* n[] = {"stride U4 g2048x256",   "stride U8 g2048x256",   "stride U4 nt g2048x256",
@@ -410,8 +502,8 @@ const char* sp_name(int cfg) {
                               "burst P4 D4 x W4",      "burst P4 D2 x W16",     "burst P4 D4 x W16",
                               "burst P4 D1 fold W16",  "burst P4 D2 fold W8",   "burst P4 D4 fold W8",
                               "burst P4 D2 fold W16",  "burst P4 D4 fold W16",  "burst P8 D2 fold W8",
-                              "sub G16 U2 nt g256", "sub G16 U2 g256", "sub G16 U4 nt g256", "sub G64 U2 nt g256", "sub G64 U4 nt g256", "sub G16 U2 nt pf g256", "sub G16 U4 nt pf g256", "sub G64 U2 nt pf g256", "sub G16 U2 nt g512", "sub G32 U2 nt g256", "sub G32 U2 nt pf g256", "chunkfold U2 nt g256", "sub G16 U2 nt pf g512"};
-    return cfg >= 0 && cfg < 67 ? n[cfg] : "?";
+                              "sub G16 U2 nt g256", "sub G16 U2 g256", "sub G16 U4 nt g256", "sub G64 U2 nt g256", "sub G64 U4 nt g256", "sub G16 U2 nt pf g256", "sub G16 U4 nt pf g256", "sub G64 U2 nt pf g256", "sub G16 U2 nt g512", "sub G32 U2 nt g256", "sub G32 U2 nt pf g256", "chunkfold U2 nt g256", "sub G16 U2 nt pf g512", "ssr G16 U4 nt g256", "ssr G16 U4 g256"};
+    return cfg >= 0 && cfg < 69 ? n[cfg] : "?";
 }
 
 // nbytes: multiple of 16; for the packet shapes, npk packets of L bytes back to back
@@ -491,6 +583,8 @@ int sp_run(int cfg, const void* buf, uint64_t nbytes, uint32_t L, const void* ze
         case 64: sp_sub<32, 2, true, 1><<<256, 1024, 65536, st>>>(p, nvec, sink); break;
         case 65: sp_chunkfold<2, true><<<256, 1024, 65536, st>>>(p, nvec, sink); break;
         case 66: sp_sub<16, 2, true, 1><<<512, 1024, 65536, st>>>(p, nvec, sink); break;
+        case 67: sp_ssr<true><<<256, 1024, 131072, st>>>(p, nvec, sink); break;
+        case 68: sp_ssr<false><<<256, 1024, 131072, st>>>(p, nvec, sink); break;
         default: return -1;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
