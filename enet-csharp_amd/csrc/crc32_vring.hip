@@ -148,6 +148,10 @@ __device__ __forceinline__ void vr_drain() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// false: the lane id and its derived constants are computed once and may be kept
+// live across the ring loop (the kernel has VGPRs to spare below the ring)
+constexpr bool kVrLaneRecompute = false;
+
 // the lane id, not hoistable (see the kernel)
 __device__ __forceinline__ uint32_t vr_lane() {
     uint32_t l;
@@ -574,7 +578,7 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
     bool done = false;
     auto iteration = [&](auto sc) __attribute__((always_inline)) {
         constexpr uint32_t S = decltype(sc)::value;
-        lane = vr_lane();
+        if constexpr (kVrLaneRecompute || BIN) lane = vr_lane();   // (BIN: its record register needs the room)
         produce(std::integral_constant<uint32_t, S ^ 1u>{}, std::integral_constant<int, static_cast<int>(S)>{});
         uint32_t d[8];
         if (cs == nedge) {                                   // head / tail pieces: keep [clz, ce) only
