@@ -44,8 +44,9 @@ def parse(argv=None):
     ap.add_argument("--streams", type=int, default=6,
                     help="HIP streams the captured steps rotate over: batches are independent, so a "
                          "launch's prologue overlaps the previous launch's tail (1 = serial)")
-    ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "small"],
-                    help="cfg2 = the metric's workload; cfg3 = mixed lengths; small = harness tests only")
+    ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "small"],
+                    help="cfg2 = the metric's workload; cfg3 = mixed lengths; cfg4 = 1 M x 1200 B split into one "
+                         "contiguous shard per rank (strong scaling); small = harness tests only")
     ap.add_argument("--list", type=int, default=5,
                     help="consecutive steps (batches) checksummed per launch through "
                          "enet_hip_crc32_batch_list_device (<= --rotate, so the batches of one launch "
@@ -297,8 +298,17 @@ def cpu_baseline(batch, budget_s: float):
 
 # ------------------------------------------------------------------ main
 
-def make_batches(cfg: str, rotate: int, rank: int):
+# cfg4: a shard must stay out of the Infinity Cache (256 MiB) across steps, so a
+# rank whose shard is smaller keeps this many bytes of copies of it resident
+CFG4_RESIDENT = 320 << 20
+
+
+def make_batches(cfg: str, rotate: int, rank: int, world: int = 1):
     from enethip import workloads
+    if cfg == "cfg4":                                  # shard `rank` of `world`, contiguous packets
+        b = workloads.cfg4(rank, world)
+        copies = max(1, -(-CFG4_RESIDENT // max(1, b.payload_bytes)))
+        return [b] * copies                            # the same bytes in `copies` distinct device buffers
     out = []
     for j in range(rotate):
         seed = workloads.SEED_PAYLOAD + 7919 * (rank * rotate + j)
@@ -348,7 +358,7 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
     if ws > 1 and args.gpus != ws:
         args.gpus = ws
     dist = dist_init(ws)
-    batches = make_batches(args.config, args.rotate, rank)
+    batches = make_batches(args.config, args.rotate, rank, ws)
     eng = (engine_factory or GpuEngine)(local, batches, args.lanes, args.wgs)
     if hasattr(eng, "set_streams"):
         eng.set_streams(args.streams)
@@ -425,15 +435,16 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
             "warmup": args.warmup,
             "ms_per_step": round(secs_max / args.steps * 1e3, 5),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.config == "cfg4" else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (splitmix64 payload, device-resident)",
             "config": {
                 "workload": {"cfg2": "cfg2: 65536 packets x 1200 B packed",
                              "cfg3": "cfg3: 262144 packets x U[64,1400] B packed",
+                             "cfg4": f"cfg4: 1048576 packets x 1200 B, shard {rank} of {ws} (contiguous packets)",
                              "small": "small: 2048 packets x 1200 B (harness tests)"}[args.config] +
-                            f", {args.rotate} rotating resident batches per GPU",
+                            f", {len(batches)} rotating resident batches per GPU",
                 "packets_per_gpu": batches[0].n,
                 "payload_bytes_per_step": int(batches[0].payload_bytes),
                 "steps_per_launch": per_launch_steps,

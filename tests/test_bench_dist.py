@@ -92,3 +92,26 @@ def test_two_rank_gloo_harness():
     assert d["value"] == pytest.approx(2 * per_rank / (d["ms_per_step"] * 6e-3) / 2**30, rel=0.02)
     assert d["roofline"]["bound"] == "hbm" and d["roofline"]["peak"] == 8000.0
     assert d["cpu_baseline"]["cores"] == 2 and d["cpu_baseline"]["kind"] == "port"
+
+
+def test_cfg4_shards_partition_the_million_packets():
+    """bench.py --config cfg4 (SURVEY §8e, strong scaling): rank r of k checksums
+    the contiguous packet range [r N/k, (r+1) N/k) of the 1 M x 1200 B workload --
+    the shards cover every packet once, each shard's bytes are that range of the
+    one splitmix64 payload stream, and a shard under 320 MiB is kept resident in
+    enough copies to stay out of the 256 MiB Infinity Cache."""
+    import bench
+    from enethip import workloads
+    n, L = 1 << 20, 1200
+    for k in (4, 8):
+        total = 0
+        for r in (0, k - 1):
+            bs = bench.make_batches("cfg4", 5, r, k)
+            b = bs[0]
+            lo = n * r // k
+            assert b.n == n * (r + 1) // k - lo and (b.lens == L).all()
+            assert len(bs) * b.payload_bytes >= bench.CFG4_RESIDENT and all(x is b for x in bs)
+            ref = workloads.splitmix64(workloads.SEED_PAYLOAD, 4, start=lo * L // 8).view(np.uint8)
+            assert (b.payload[:32] == ref).all()
+            total += b.n
+        assert total == 2 * (n // k)
