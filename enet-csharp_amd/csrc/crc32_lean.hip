@@ -153,9 +153,10 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
     return static_cast<uint64_t>(lo) | (static_cast<uint64_t>(hi) << 32);
 }                     // (the one-batch instances never read it)
 
-// LIST = 1 (checksum mode, no ablation): the batches of a LeanList, their groups
-// concatenated (batch b's groups are global groups g0_b ..) and dealt over the
-// waves as one batch's are; pa is unused.  A wave's groups ascend, so each of its
+// LIST = 1 (no ablation): the batches of a LeanList (checksum, MODE 0) or a
+// LeanVList (receive verify, MODE 1: also each batch's slot offsets, connectIDs and
+// ok[]), their groups concatenated (batch b's groups are global groups g0_b ..) and
+// dealt over the waves as one batch's are; pa is unused.  A wave's groups ascend, so each of its
 // three walkers (metadata, producer, consumer) finds a group's batch with a cursor
 // that only moves forward.
 // The list lives in the kernel-argument segment and is read there (llp, scalar
