@@ -331,7 +331,7 @@ def kernel_name(args, list_launch: bool = False) -> str:
     if list_launch and path == 13 and args.lanes in (0, 4, 8) and not args.binned:
         # batch lists: the lean kernel's list instance, 8 lanes per packet unless set
         return f"crc32_lean_list_kernel<{3 if args.lanes in (0, 8) else 2}, 16, 2>"
-    lanes = args.lanes or 4
+    lanes = args.lanes or 8                       # the library's default (auto_lanes)
     lg = {4: 2, 8: 3}.get(lanes)
     if path and path not in (17, 18):
         return f"kernel path {path}"

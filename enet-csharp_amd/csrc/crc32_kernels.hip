@@ -998,11 +998,14 @@ const HostTables& host_tables() {
     return t;
 }
 
-// Default lanes per packet: 4 for checksum batches (vring kernel: 5650 vs 5369 GB/s
-// at 8 on cfg2 with overlapped launches, profiles/r02_*), 8 for receive verify
-// (lean kernel).
+// Default lanes per packet: 8 for checksum batches and for receive verify.  The
+// vring kernel with its lane constants kept live runs cfg2 at 5.26-5.34 TB/s in the
+// serial 5-batch region at 8 lanes against 5.14-5.26 at 4, with the same bench value
+// (three interleaved repeats on one box, profiles/r02e_lanes_4_vs_8/); before that, 4
+// lanes had led (profiles/r02_*).  The length-binned entries keep their own default (4).
 int auto_lanes(const enet_hip_context* ctx, int mode = 0) {
-    return ctx->lanes_per_packet > 0 ? ctx->lanes_per_packet : (mode == 0 ? 4 : 8);
+    (void)mode;
+    return ctx->lanes_per_packet > 0 ? ctx->lanes_per_packet : 8;
 }
 
 int log2i(int v) {

@@ -71,7 +71,7 @@ ENET_HIP_API int enet_hip_context_destroy(enet_hip_context* ctx);
 ENET_HIP_API const char* enet_hip_error_string(int code);
 
 /* Tuning knobs (0 = automatic).  lanes_per_packet: 1,2,4,...,64 lanes share one
- * packet (a power of two; default 4 for checksum batches, 8 for receive verify);
+ * packet (a power of two; default 8, and 4 for the length-binned entries);
  * workgroups_per_cu: resident workgroups per CU the direct / gather grids are
  * sized for. */
 ENET_HIP_API int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgroups_per_cu);
