@@ -138,6 +138,15 @@ namespace enet
                                                               uint* segLengths, uint* segFirst, nuint dgramCount,
                                                               uint* output, IntPtr stream);
 
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern nuint enet_hip_gather_binned_workspace_size(nuint segCount);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_crc32_gather_binned_device(IntPtr ctx, byte* bytes, ulong* segOffsets,
+                                                                     uint* segLengths, nuint segCount, uint* segFirst,
+                                                                     nuint dgramCount, uint* output, void* workspace,
+                                                                     nuint workspaceBytes, IntPtr stream);
+
         // batched range coder, c/compress.cs:69-943
         [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
         public static extern int enet_hip_range_compress_device(IntPtr ctx, byte* input, ulong* inOffsets,
@@ -273,6 +282,15 @@ namespace enet
             => EnetHip.Check("enet_hip_verify_batch_device",
                 EnetHipNative.enet_hip_verify_batch_device(Handle, bytes, offsets, lengths, slotOffsets, connectIds,
                     count, ok, computed, stream));
+
+        /// <summary>Send-side gather-list CRCs (c/protocol.cs:1690-1698), segment count known on the host:
+        /// a length-binned pass over the segments, then a join per DGRAM.</summary>
+        public void GatherDeviceBinned(byte* bytes, ulong* segOffsets, uint* segLengths, nuint segCount, uint* segFirst,
+                                       nuint dgramCount, uint* output, void* workspace, nuint workspaceBytes,
+                                       IntPtr stream = default)
+            => EnetHip.Check("enet_hip_crc32_gather_binned_device",
+                EnetHipNative.enet_hip_crc32_gather_binned_device(Handle, bytes, segOffsets, segLengths, segCount,
+                    segFirst, dgramCount, output, workspace, workspaceBytes, stream));
 
         /// <summary>Receive verify over a list of batches, one launch per 32 (same ok[] / computed[] as VerifyDevice per batch).</summary>
         public void VerifyListDevice(ENetHipVerifyBatch* batches, nuint batchCount, IntPtr stream = default)

@@ -834,6 +834,30 @@ __global__ void __launch_bounds__(kThreads) crc32_gather_kernel(GatherArgs ga, K
     }
 }
 
+// The join of enet_hip_crc32_gather_binned_device: thread per DGRAM.  seg_crc[q] =
+// finalize(reg(0xFFFFFFFF, segment q)) from the length-binned checksum pass over the
+// segments.  reg(s, A||B) = adv_|B|(reg(s, A)) ^ reg(0, B) and reg(0, B) =
+// reg(0xFFFFFFFF, B) ^ adv_|B|(0xFFFFFFFF), so one multiply per segment:
+// reg' = (reg ^ 0xFFFFFFFF) x^(8|B|) ^ reg(0xFFFFFFFF, B), from reg = 0xFFFFFFFF
+// (packet.cs:144-159 over the concatenated buffers, as enet_crc32 walks them).
+__global__ void __launch_bounds__(kThreads) crc32_gather_join_kernel(GatherArgs ga, const uint32_t* seg_crc,
+                                                                     KernelTables tb) {
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
+    for (uint64_t d = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; d < ga.n; d += stride) {
+        const uint32_t s0 = ga.seg_first[d], s1 = ga.seg_first[d + 1];
+        uint32_t reg = 0xFFFFFFFFu;
+        bool first = true;
+        for (uint32_t q = s0; q < s1; ++q) {
+            const uint32_t L = ga.seg_len[q];
+            if (L == 0) continue;
+            const uint32_t r = ~bswap32(seg_crc[q]);
+            reg = (first ? 0u : mulmod(reg ^ 0xFFFFFFFFu, x8n_dev(L, tb))) ^ r;   // (first: reg ^ ~0 = 0)
+            first = false;
+        }
+        ga.out[d] = finalize(reg);
+    }
+}
+
 // Read-roofline probe: every byte loaded once by 16-byte coalesced loads,
 // 4 loads in flight per lane, XOR-folded so nothing is dead code.
 __global__ void __launch_bounds__(kThreads) read_probe_kernel(const uint8_t* bytes, uint64_t nvec, uint32_t* sink) {
@@ -1522,6 +1546,35 @@ int enet_hip_crc32_gather_device(enet_hip_context* ctx, const uint8_t* bytes, co
     const unsigned grid = grid_for(ctx, dgramCount);
     hipLaunchKernelGGL(crc32_gather_kernel, dim3(grid), dim3(kThreads), kLdsTableBytes,
                        stream ? static_cast<hipStream_t>(stream) : ctx->stream, ga, tables_of(ctx));
+    return herr(hipGetLastError());
+}
+
+size_t enet_hip_gather_binned_workspace_size(size_t segCount) {
+    return ((enet_hip_binned_workspace_size(segCount) + 15u) & ~static_cast<size_t>(15u)) + 4u * segCount;
+}
+
+int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* bytes, const uint64_t* segOffsets,
+                                        const uint32_t* segLengths, size_t segCount, const uint32_t* segFirst,
+                                        size_t dgramCount, uint32_t* out, void* workspace, size_t workspaceBytes,
+                                        void* stream) {
+    if (!ctx) return -static_cast<int>(hipErrorInvalidValue);
+    if (dgramCount == 0) return 0;
+    if (!bytes || !segFirst || !out || (segCount && (!segOffsets || !segLengths || !workspace)) ||
+        segCount > 0xFFFFFFFFull || workspaceBytes < enet_hip_gather_binned_workspace_size(segCount) ||
+        (reinterpret_cast<uintptr_t>(workspace) & 15u))
+        return -static_cast<int>(hipErrorInvalidValue);
+    ENH_CHECK(hipSetDevice(ctx->device));
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    const size_t bws = (enet_hip_binned_workspace_size(segCount) + 15u) & ~static_cast<size_t>(15u);
+    uint32_t* seg_crc = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(workspace) + bws);
+    if (segCount) {                                        // every segment's CRC, mixed lengths: length-binned
+        const int rc = enet_hip_crc32_batch_device_binned(ctx, bytes, segOffsets, segLengths, segCount, seg_crc,
+                                                          workspace, bws, st);
+        if (rc) return rc;
+    }
+    GatherArgs ga{bytes, segOffsets, segLengths, segFirst, dgramCount, out};
+    const unsigned grid = grid_for(ctx, dgramCount);
+    hipLaunchKernelGGL(crc32_gather_join_kernel, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx));
     return herr(hipGetLastError());
 }
 

@@ -30,7 +30,8 @@ EXPORTED_SYMBOLS = (
     "enet_hip_crc32_batch_device", "enet_hip_crc32_batch_list_device", "enet_hip_binned_workspace_size", "enet_hip_crc32_batch_device_binned",
     "enet_hip_verify_binned_workspace_size", "enet_hip_verify_batch_device_binned",
     "enet_hip_crc32_batch_host", "enet_hip_verify_batch_device", "enet_hip_verify_batch_list_device",
-    "enet_hip_crc32_gather_device", "enet_hip_crc32_batch_multi", "enet_hip_device_alloc",
+    "enet_hip_crc32_gather_device", "enet_hip_gather_binned_workspace_size", "enet_hip_crc32_gather_binned_device",
+    "enet_hip_crc32_batch_multi", "enet_hip_device_alloc",
     "enet_hip_device_free", "enet_hip_host_alloc", "enet_hip_host_free", "enet_hip_memcpy_h2d",
     "enet_hip_memcpy_d2h", "enet_hip_synchronize", "enet_hip_read_probe_device", "enet_hip_set_kernel_path",
     "enet_hip_diag_ablation", "enet_hip_diag_trace", "enet_hip_fragment_reassemble_device",
@@ -112,6 +113,10 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.enet_hip_crc32_batch_host.argtypes = [vp, vp, sz, vp, vp, sz, vp]
     L.enet_hip_verify_batch_device.restype = i32
     L.enet_hip_verify_batch_device.argtypes = [vp, vp, vp, vp, vp, vp, sz, vp, vp, vp]
+    L.enet_hip_gather_binned_workspace_size.restype = sz
+    L.enet_hip_gather_binned_workspace_size.argtypes = [sz]
+    L.enet_hip_crc32_gather_binned_device.restype = i32
+    L.enet_hip_crc32_gather_binned_device.argtypes = [vp, vp, vp, vp, sz, vp, sz, vp, vp, sz, vp]
     L.enet_hip_crc32_gather_device.restype = i32
     L.enet_hip_crc32_gather_device.argtypes = [vp, vp, vp, vp, vp, sz, vp, vp]
     L.enet_hip_crc32_batch_multi.restype = i32
@@ -283,6 +288,17 @@ class Context:
         _check("enet_hip_crc32_gather_device", self.lib.enet_hip_crc32_gather_device(
             self.handle, _ptr(d_bytes), _ptr(d_seg_off), _ptr(d_seg_len), _ptr(d_seg_first), int(n_dgrams),
             _ptr(d_out), stream or None))
+
+    def gather_binned_workspace_size(self, seg_count: int) -> int:
+        return int(self.lib.enet_hip_gather_binned_workspace_size(int(seg_count)))
+
+    def gather_binned_device(self, d_bytes, d_seg_off, d_seg_len, seg_count: int, d_seg_first, n_dgrams: int,
+                             d_out, d_workspace, workspace_bytes: int, stream: int = 0) -> None:
+        """Gather-list CRCs via a length-binned pass over the segments and a join (enet_hip.h)."""
+        _check("enet_hip_crc32_gather_binned_device", self.lib.enet_hip_crc32_gather_binned_device(
+            self.handle, _ptr(d_bytes), _ptr(d_seg_off) or None, _ptr(d_seg_len) or None, int(seg_count),
+            _ptr(d_seg_first), int(n_dgrams), _ptr(d_out), _ptr(d_workspace) or None, int(workspace_bytes),
+            stream or None))
 
     def fragment_reassemble_device(self, d_bytes, d_cmd_off, d_cmd_avail, d_slots, n: int, max_packet: int,
                                    d_msg_bytes, d_msg_off, d_msg_len, d_msg_count, d_fragments, words: int,

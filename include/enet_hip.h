@@ -193,6 +193,21 @@ ENET_HIP_API int enet_hip_crc32_gather_device(enet_hip_context* ctx, const uint8
                                               const uint32_t* segFirst, size_t dgramCount, uint32_t* out,
                                               void* stream);
 
+/* Same results as enet_hip_crc32_gather_device, with the segment count known on
+ * the host (segCount = segFirst[dgramCount]).  Two passes on `stream`: every
+ * segment's CRC as one length-binned checksum batch (enet_hip_crc32_batch_device_binned:
+ * the 8-B headers, 24-B commands and MTU payloads of a send batch run in groups of
+ * about one length), then one thread per DGRAM joins its segments' CRCs with one
+ * GF(2) multiply by x^(8 len) each.  `workspace`: caller-owned device memory of at
+ * least enet_hip_gather_binned_workspace_size(segCount) bytes, 16-byte aligned, not
+ * shared with a call in flight; segCount < 2^32.  Async; graph-capturable. */
+ENET_HIP_API size_t enet_hip_gather_binned_workspace_size(size_t segCount);
+ENET_HIP_API int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* bytes,
+                                                     const uint64_t* segOffsets, const uint32_t* segLengths,
+                                                     size_t segCount, const uint32_t* segFirst, size_t dgramCount,
+                                                     uint32_t* out, void* workspace, size_t workspaceBytes,
+                                                     void* stream);
+
 /* ---- batched fragment reassembly (receive side, c/protocol.cs:529-637) ----
  * The data movement of enet_protocol_handle_send_fragment for a batch of
  * SEND_FRAGMENT commands; replaces its per-command validation, bitmap update,

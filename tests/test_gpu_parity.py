@@ -463,6 +463,59 @@ def test_gather_golden_and_cfg5(ctx, golden, oracle_lib):
                                                                    g.seg_first)).all()
 
 
+def _run_gather_binned(ctx, payload, seg_off, seg_len, seg_first):
+    n, ns = len(seg_first) - 1, int(seg_first[-1])
+    out = torch.full((max(1, n),), -1, dtype=torch.int32, device="cuda")
+    wsb = ctx.gather_binned_workspace_size(ns)
+    ws = torch.zeros(max(16, wsb), dtype=torch.uint8, device="cuda")
+    ctx.gather_binned_device(dev(payload if len(payload) else np.zeros(16, np.uint8)),
+                             dev(seg_off) if ns else None, dev(seg_len) if ns else None, ns,
+                             dev(seg_first), n, out, ws, wsb, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint32)[:n]
+
+
+def test_gather_binned(ctx, golden, oracle_lib):
+    """enet_hip_crc32_gather_binned_device (send-side gather lists, protocol.cs:1690-1698):
+    the golden multi-buffer vectors, cfg5's 3-segment DGRAMs, random gather lists of 0-65
+    segments (empty segments and empty DGRAMs among them, arbitrary byte alignment,
+    segments shared between DGRAMs), a list of only empty DGRAMs, each against the
+    oracle's gather, at the default, 4 and 8 lanes."""
+    vecs, blob = golden
+    seg_off, seg_len, first, exp = [], [], [0], []
+    for v in vecs:
+        for o, n in v["segments"]:
+            seg_off.append(o)
+            seg_len.append(n)
+        first.append(len(seg_off))
+        exp.append(int(v["crc"], 16))
+    cases = [(blob, np.array(seg_off, np.uint64), np.array(seg_len, np.uint32), np.array(first, np.uint32),
+              np.array(exp, np.uint32))]
+    g = workloads.cfg5(messages=256)
+    cases.append((g.payload, g.seg_off, g.seg_len, g.seg_first,
+                  oracle_lib.gather(g.payload, g.seg_off, g.seg_len, g.seg_first)))
+    rng = np.random.default_rng(77)
+    payload = rng.integers(0, 256, size=3 << 20, dtype=np.uint8)
+    cnt = rng.integers(0, 66, size=3000)
+    cnt[::50] = 0
+    ns = int(cnt.sum())
+    lens = np.where(rng.integers(0, 8, size=ns) == 0, 0, rng.integers(1, 1500, size=ns)).astype(np.uint32)
+    offs = rng.integers(0, len(payload) - 1500, size=ns).astype(np.uint64)
+    sf = np.zeros(len(cnt) + 1, np.uint32)
+    np.cumsum(cnt, out=sf[1:])
+    cases.append((payload, offs, lens, sf, oracle_lib.gather(payload, offs, lens, sf)))
+    empty_first = np.zeros(7, np.uint32)
+    cases.append((payload[:64], np.zeros(0, np.uint64), np.zeros(0, np.uint32), empty_first, np.zeros(6, np.uint32)))
+    try:
+        for lanes in (0, 4, 8):
+            ctx.set_tuning(lanes, 0)
+            for i, (p, so, sl, f, e) in enumerate(cases):
+                got = _run_gather_binned(ctx, p, so, sl, f)
+                assert (got == e).all(), (lanes, i, np.nonzero(got != e)[0][:5])
+    finally:
+        ctx.set_tuning(0, 0)
+
+
 def test_bad_tuning_raises(ctx):
     with pytest.raises(enethip.ENetHipError):
         ctx.set_tuning(3, 0)

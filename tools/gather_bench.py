@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Send-side gather-list CRC throughput (c/protocol.cs:1690-1698, SURVEY §8a a5 and
+§8f row 2) on cfg5: 4096 x 64 KiB messages -> 200 704 DGRAMs, each a 3-buffer gather
+list [8 B header+slot][24 B SendFragment][1360 or 256 B chunk], device-resident.
+Algorithmic bytes per call = the DGRAM bytes (274.9 MB).  Times
+enet_hip_crc32_gather_device (one lane per DGRAM) against
+enet_hip_crc32_gather_binned_device (a length-binned checksum pass over the 602 112
+segments, then a join per DGRAM), serial region as bench.py's roofline: HIP events on
+the launch stream around back-to-back calls, a spin kernel ahead.  Both outputs are
+checked against the oracle first.
+
+    python tools/gather_bench.py [--messages 4096] [--reps 20]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "enet-csharp_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import numpy as np  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--messages", type=int, default=4096)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--lanes", type=int, default=0)
+    a = ap.parse_args()
+    import torch
+    import enethip
+    from enethip import workloads
+    import oracle as orc
+    g = workloads.cfg5(a.messages)
+    ctx = enethip.Context(0, a.lanes, 0)
+    st = torch.cuda.Stream()
+    t = lambda x, dt: torch.from_numpy(np.ascontiguousarray(x).view(dt)).cuda()  # noqa: E731
+    d_p, d_so, d_sl, d_sf = t(g.payload, np.uint8), t(g.seg_off, np.int64), t(g.seg_len, np.int32), t(g.seg_first, np.int32)
+    ns = int(g.seg_first[-1])
+    out = torch.zeros(g.n, dtype=torch.int32, device="cuda")
+    wsb = ctx.gather_binned_workspace_size(ns)
+    ws = torch.zeros(wsb, dtype=torch.uint8, device="cuda")
+
+    def plain(_i):
+        ctx.gather_device(d_p, d_so, d_sl, d_sf, g.n, out, st.cuda_stream)
+
+    def binned(_i):
+        ctx.gather_binned_device(d_p, d_so, d_sl, ns, d_sf, g.n, out, ws, wsb, st.cuda_stream)
+
+    exp = orc.OracleLib().gather(g.payload, g.seg_off, g.seg_len, g.seg_first)
+    res = {"kind": "gather-bench", "dgrams": g.n, "segments": ns, "bytes": g.dgram_bytes,
+           "lanes": a.lanes or "default"}
+    for name, fn in (("gather", plain), ("gather_binned", binned)):
+        out.zero_()
+        fn(0)
+        torch.cuda.synchronize()
+        ok = bool((out.cpu().numpy().view(np.uint32) == exp).all())
+        assert ok, name + " differs from the oracle"
+        for i in range(3):
+            fn(i)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(st):
+            torch.cuda._sleep(int(2e8))
+            e0.record(st)
+            for i in range(a.reps):
+                fn(i)
+            e1.record(st)
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / a.reps * 1e3
+        res[name + "_us"] = round(us, 2)
+        res[name + "_GBps"] = round(g.dgram_bytes / us / 1e3, 1)
+        res[name + "_GiBps"] = round(g.dgram_bytes / us * 1e6 / 2 ** 30, 1)
+        res[name + "_bit_exact"] = ok
+    print(json.dumps(res), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
