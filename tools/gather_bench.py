@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--messages", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--lanes", type=int, default=0)
+    ap.add_argument("--path", type=int, default=0, help="kernel path (enet_hip_set_kernel_path; 17 = vring records)")
     a = ap.parse_args()
     import torch
     import enethip
@@ -35,6 +36,8 @@ def main():
     import oracle as orc
     g = workloads.cfg5(a.messages)
     ctx = enethip.Context(0, a.lanes, 0)
+    if a.path:
+        ctx.set_kernel_path(a.path)
     st = torch.cuda.Stream()
     t = lambda x, dt: torch.from_numpy(np.ascontiguousarray(x).view(dt)).cuda()  # noqa: E731
     d_p, d_so, d_sl, d_sf = t(g.payload, np.uint8), t(g.seg_off, np.int64), t(g.seg_len, np.int32), t(g.seg_first, np.int32)
