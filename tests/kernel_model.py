@@ -672,3 +672,18 @@ def vring_dynamic_deal(batch_groups, grid: int, rng, W: int = 16):
             order.append(w)
         per_wave.extend(count)
     return seen, per_wave, total
+
+
+# ---------------------------------------------------------------- gather join
+def gather_join(seg_crcs, seg_lens) -> int:
+    """crc32_gather_join_kernel (enet_hip_crc32_gather_binned_device): a DGRAM's CRC from
+    its segments' finalized CRCs (each = finalize(reg(0xFFFFFFFF, segment))).
+    reg' = (reg ^ ~0) x^(8 len) ^ reg(~0, segment), from reg = ~0; empty segments skipped."""
+    reg, first = 0xFFFFFFFF, True
+    for c, L in zip(seg_crcs, seg_lens):
+        if L == 0:
+            continue
+        r = ~int.from_bytes(c.to_bytes(4, "little"), "big") & 0xFFFFFFFF     # ~bswap32(crc)
+        reg = (0 if first else mulmod(reg ^ 0xFFFFFFFF, x8n(L))) ^ r
+        first = False
+    return finalize(reg)

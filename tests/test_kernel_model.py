@@ -266,3 +266,16 @@ def test_vring_dynamic_slots_cover_every_group_once(batch_groups, grid):
     for gg, (b, local) in seen.items():
         assert 0 <= local < nonempty[b] and g0[b] + local == gg
     assert sum(per_wave) == total
+
+
+def test_gather_join_matches_oracle(oracle_lib):
+    """The binned gather's join (crc32_gather_join_kernel, restated as
+    km.gather_join) turns per-segment CRCs into the DGRAM's enet_crc32 over the
+    concatenated buffers (packet.cs:142-160 walking the gather list), for lists of
+    0-6 segments with empty ones among them, against the oracle."""
+    rng = random.Random(2024)
+    for _ in range(300):
+        segs = [bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 0, 1, 3, 8, 24, 57, 200])))
+                for _ in range(rng.randint(0, 6))]
+        crcs = [oracle_lib.crc32(s) for s in segs]
+        assert km.gather_join(crcs, [len(s) for s in segs]) == oracle_lib.crc32(b"".join(segs))
