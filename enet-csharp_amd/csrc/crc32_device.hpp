@@ -42,6 +42,11 @@ constexpr uint32_t kCinvCol = 30;   // CINV[n] = x^(-8n), n < 512: row n & 255 o
 __host__ __device__ constexpr uint32_t init_addr(uint32_t r) { return 256u * r + free_col(kInitCol); }
 __host__ __device__ constexpr uint32_t cinv_addr(uint32_t n) { return 256u * (n & 255u) + free_col(kCinvCol + (n >> 8)); }
 __host__ __device__ constexpr uint32_t corr_col(uint32_t k, uint32_t b) { return free_col(kCorrCol + 4u * (k - 1u) + b); }
+// U[h] (free column 28, GF(2)-linear in h): one zero byte undone, reg x^(-8) =
+// (reg << 8) ^ U[reg >> 24]; U[t0(b) >> 24] = (t0(b) << 8) | b (the top bytes of the
+// Sarwate table are a permutation)
+constexpr uint32_t kUnstepCol = 28;
+__host__ __device__ constexpr uint32_t unstep_addr(uint32_t h) { return 256u * h + free_col(kUnstepCol); }
 constexpr int kXnEntries = 65536;                  // x^(8n) for n < 65536 (+ high part)
 // Lean-kernel table basis (crc32_lean.hip): every image column but INIT and CINV
 // is GF(2)-linear in the row index, so rows 2^b (b < 8) rebuild it; row 8 holds

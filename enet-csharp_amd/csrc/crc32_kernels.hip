@@ -966,6 +966,10 @@ struct HostTables {
                 for (uint32_t b = 0; b < 4; ++b)
                     for (uint32_t v = 0; v < 256; ++v)
                         img[(256u * v + corr_col(k, b)) / 4] = gf2_mulmod(v << (8 * b), cinv[32 * k]);
+            for (uint32_t b = 0; b < 256; ++b) {                // U: reg x^(-8) = (reg << 8) ^ U[reg >> 24]
+                const uint32_t t = crc_table_entry(b);
+                img[unstep_addr(t >> 24) / 4] = (t << 8) | b;
+            }
             for (uint32_t r = 0; r < 64; ++r) img[init_addr(r) / 4] = init[r];
             for (uint32_t i = 0; i < static_cast<uint32_t>(kCinvEntries); ++i) img[cinv_addr(i) / 4] = cinv[i];
             // lean-kernel basis: image rows 2^b of the linear columns, then INIT | CINV

@@ -687,3 +687,22 @@ def gather_join(seg_crcs, seg_lens) -> int:
         reg = (0 if first else mulmod(reg ^ 0xFFFFFFFF, x8n(L))) ^ r
         first = False
     return finalize(reg)
+
+
+# ---------------------------------------------------------------- unstep column
+def unstep_table() -> list[int]:
+    """Free column 28 of every image (kUnstepCol): U[t0(b) >> 24] = (t0(b) << 8) | b, so one
+    zero byte is undone as reg x^(-8) = (reg << 8) ^ U[reg >> 24].  The vring kernel applies
+    CINV[tz] = x^(-8 tz) as tz such unsteps (vr_unstep)."""
+    U = [0] * 256
+    for b in range(256):
+        t = t0(b)
+        U[t >> 24] = ((t << 8) & 0xFFFFFFFF) | b
+    return U
+
+
+def unstep(reg: int, n: int, U=None) -> int:
+    U = U or unstep_table()
+    for _ in range(n):
+        reg = ((reg << 8) & 0xFFFFFFFF) ^ U[reg >> 24]
+    return reg

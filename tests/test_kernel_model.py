@@ -279,3 +279,18 @@ def test_gather_join_matches_oracle(oracle_lib):
                 for _ in range(rng.randint(0, 6))]
         crcs = [oracle_lib.crc32(s) for s in segs]
         assert km.gather_join(crcs, [len(s) for s in segs]) == oracle_lib.crc32(b"".join(segs))
+
+
+def test_unstep_column_is_cinv():
+    """The vring kernel's tz correction: tz unsteps through the U column equal the multiply
+    by CINV[tz] = x^(-8 tz) for every tz < 32 (random registers), U is a permutation-derived
+    table that is GF(2)-linear in its row (so the image basis rebuilds it), and it undoes a
+    zero-byte Sarwate step exactly."""
+    U = km.unstep_table()
+    assert all(U[a ^ b] == U[a] ^ U[b] for a in range(256) for b in (1, 2, 4, 8, 16, 32, 64, 128))
+    cinv = km.cinv_table(32)
+    rng = random.Random(7)
+    for _ in range(300):
+        r, tz = rng.getrandbits(32), rng.randrange(32)
+        assert km.unstep(r, tz, U) == km.mulmod(r, cinv[tz])
+        assert km.unstep(km.zstep(r), 1, U) == r
