@@ -584,7 +584,10 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
         if constexpr (BIN) cidx = pidx;
         crem = bl.b[pit.b].n - base;
         const uint32_t nb = (ce + 31u) >> 5;                 // 0 for an empty packet ([0, 0))
-        cstages = max(1u, wave_max_u((nb + P - 1u) >> LG));
+        // the producer's count for this same group (no second wave reduction; the trace
+        // instance keeps the reduction: without it, it spilled a VGPR)
+        if constexpr (TR) cstages = max(1u, wave_max_u((nb + P - 1u) >> LG));
+        else cstages = pstages;
         const uint32_t init = lds_load(init_addr(clz));
         reg = lane_k() == 0u ? (nb ? init : 0xFFFFFFFFu) : 0u;      // packet.cs:144 (empty packet: ~crc = 0)
         nedge = next_edge(0);
