@@ -160,6 +160,45 @@ __device__ __forceinline__ uint32_t xor_lanes(uint32_t lg, uint32_t v) {
     return v;
 }
 
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+
+// One zero byte undone: reg x^(-8) = (reg << 8) ^ U[reg >> 24] (U in free column
+// kUnstepCol of the image, unstep_addr).  In asm with immediate constants: written
+// in C++, hipcc hoisted the address constants into VGPRs and spilled one.
+__device__ __forceinline__ uint32_t unstep_byte(uint32_t reg) {
+    uint32_t t;
+    static_assert(unstep_addr(0) == 0xe0u, "the U column's byte offset in a row");
+    asm volatile("v_lshrrev_b32 %[t], 16, %[r]\n\t"
+                 "v_and_b32 %[t], 0xff00, %[t]\n\t"
+                 "v_or_b32 %[t], 0xe0, %[t]\n\t"
+                 "ds_read_b32 %[t], %[t]\n\t"
+                 "v_lshlrev_b32 %[r], 8, %[r]\n\t"
+                 "s_waitcnt lgkmcnt(0)\n\t"
+                 "v_xor_b32 %[r], %[r], %[t]"
+                 : [r] "+v"(reg), [t] "=&v"(t) :: "memory");
+    return reg;
+}
+
+// reg x^(-8 tz), tz < 32: tz zero-byte unsteps, straight-line by the bits of tz
+// (the wave runs a block when any lane needs it; about 6 VALU per byte against ~160
+// for a bit-serial multiply by CINV[tz])
+__device__ __forceinline__ uint32_t unstep_bytes(uint32_t reg, uint32_t tz) {
+    static_for<0, 5>([&](auto bc) __attribute__((always_inline)) {
+        constexpr int bit = 4 - decltype(bc)::value;
+        if (tz & (1u << bit)) {
+#pragma unroll
+            for (int j = 0; j < (1 << bit); ++j) reg = unstep_byte(reg);
+        }
+    });
+    return reg;
+}
+
 // End of a group: lane k sits 32k + tz bytes past the data end.  Undo the 32k
 // by x^(-256k) -- four byte-indexed lookups in the image's correction columns
 // (each lane starts at a different byte so the lanes sharing k spread over four
@@ -182,17 +221,10 @@ __device__ __forceinline__ uint32_t finish_packet(uint32_t lg, uint32_t k, uint3
         reg = mulmod(reg, lds_load(cinv_addr(32u * k)));
     }
     reg = xor_lanes<0>(lg, reg);
-    if (k == 0 && tz) reg = mulmod(reg, lds_load(cinv_addr(tz)));
+    if (k == 0) reg = unstep_bytes(reg, tz);                 // x^(-8 tz), tz < 16 here
     return reg;
 }
 
-template <int I, int N, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-    if constexpr (I < N) {
-        f(std::integral_constant<int, I>{});
-        static_for<I + 1, N>(f);
-    }
-}
 
 template <int N, class F>
 __device__ __forceinline__ void unroll_slots(F&& f) {

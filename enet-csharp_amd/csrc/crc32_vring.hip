@@ -196,23 +196,6 @@ __device__ __forceinline__ VrSched make_vr_sched(uint32_t lane) {
     return s;
 }
 
-// One zero byte undone: reg x^(-8) = (reg << 8) ^ U[reg >> 24] (U in free column
-// kUnstepCol of the image, unstep_addr).  In asm with immediate constants: written
-// in C++, hipcc hoisted the address constants into VGPRs and spilled one.
-__device__ __forceinline__ uint32_t vr_unstep(uint32_t reg) {
-    uint32_t t;
-    static_assert(unstep_addr(0) == 0xe0u, "the U column's byte offset in a row");
-    asm volatile("v_lshrrev_b32 %[t], 16, %[r]\n\t"
-                 "v_and_b32 %[t], 0xff00, %[t]\n\t"
-                 "v_or_b32 %[t], 0xe0, %[t]\n\t"
-                 "ds_read_b32 %[t], %[t]\n\t"
-                 "v_lshlrev_b32 %[r], 8, %[r]\n\t"
-                 "s_waitcnt lgkmcnt(0)\n\t"
-                 "v_xor_b32 %[r], %[r], %[t]"
-                 : [r] "+v"(reg), [t] "=&v"(t) :: "memory");
-    return reg;
-}
-
 // mulmod (crc32_device.hpp) as a rolled loop: once per packet, so the few
 // cycles of loop overhead buy registers (the unrolled form set the kernel's peak)
 __device__ __forceinline__ uint32_t vr_mulmod(uint32_t a, uint32_t b) {
@@ -637,20 +620,11 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
             if constexpr (!(ABL & 16)) reg = o ? corr : reg;
             reg = xor_lanes<0>(LG, reg);
             const uint32_t tz = nb ? 32u * nb - ce : 0u;
-            // x^(-8 tz) as tz zero-byte unsteps, one LDS lookup each (the U column): about
-            // 5 VALU per byte against the 170 of a bit-serial multiply by CINV[tz], which
-            // ran whenever any of the wave's packets had a ragged end
-            // (by the bits of tz < 32, straight-line: a loop counter cost a spilled VGPR)
+            // x^(-8 tz) as tz zero-byte unsteps, one LDS lookup each (the U column,
+            // unstep_bytes): about 6 VALU per byte against the 170 of a bit-serial multiply
+            // by CINV[tz], which ran whenever any of the wave's packets had a ragged end
             if constexpr (!(ABL & 16))
-                if (lane_k() == 0u)
-                    static_for<0, 5>([&](auto bc) __attribute__((always_inline)) {
-                        constexpr int bit = 4 - decltype(bc)::value;
-                        if (tz & (1u << bit)) {
-#pragma unroll
-                            for (int j = 0; j < (1 << bit); ++j)
-                                reg = vr_unstep(reg);
-                        }
-                    });
+                if (lane_k() == 0u) reg = unstep_bytes(reg, tz);
             if (lane_k() == 0u && lane_p() < crem) cout[BIN ? cidx : lane_p()] = finalize(reg);   // packet.cs:159
             if (pdone) {
                 // no newer group entered: the wave is done.  The producer's last loads
