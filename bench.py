@@ -40,7 +40,8 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--rotate", type=int, default=5, help="distinct resident batches cycled through")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per packet (0 = library default)")
-    ap.add_argument("--wgs", type=int, default=2, help="workgroups per CU (enet_hip_set_tuning; 0 = library default)")
+    ap.add_argument("--wgs", type=int, default=0,
+                    help="workgroups per CU (enet_hip_set_tuning; 0 = the library default, 2 for the vring kernel)")
     ap.add_argument("--streams", type=int, default=6,
                     help="HIP streams the captured steps rotate over: batches are independent, so a "
                          "launch's prologue overlaps the previous launch's tail (1 = serial)")
@@ -53,7 +54,8 @@ def parse(argv=None):
                          "are distinct); 0 = one enet_hip_crc32_batch_device call per step.  A step is "
                          "always one pass over one batch")
     ap.add_argument("--path", type=int, default=0,
-                    help="kernel path (enet_hip_set_kernel_path; 0 = the library default -- tuning sweeps only)")
+                    help="kernel path (enet_hip_set_kernel_path; 0 = the library default -- tuning sweeps only; "
+                         "a path the product library does not build runs on libenethip_diag.so)")
     ap.add_argument("--binned", action="store_true",
                     help="length-binned entry (enet_hip_crc32_batch_device_binned): for mixed lengths (cfg3)")
     ap.add_argument("--launch", default="graph", choices=["graph", "direct"],
@@ -61,6 +63,10 @@ def parse(argv=None):
                          "launches enqueued one by one inside the timed region")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget per CPU-baseline leg")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (0 = every core this process may run on, sched_getaffinity)")
+    ap.add_argument("--sustain-ms", type=float, default=30.0,
+                    help="length of the serial sustained-rate region reported beside the value (0 = skip)")
     return ap.parse_args(argv)
 
 
@@ -124,14 +130,14 @@ def timed_region(dist, sync, steps: int, step_fn):
 class GpuEngine:
     """Resident batches + launches through the C-ABI on torch's current stream."""
 
-    def __init__(self, device: int, batches, lanes: int, wgs: int):
+    def __init__(self, device: int, batches, lanes: int, wgs: int, diag: bool = False):
         import torch
         import enethip
         if not torch.cuda.is_available():
             raise SystemExit("bench.py: no GPU visible -- the HIP path has no CPU fallback")
         torch.cuda.set_device(device)
         self.torch = torch
-        self.ctx = enethip.Context(device, lanes, wgs)
+        self.ctx = enethip.Context(device, lanes, wgs, diag=diag)
         self.stream = torch.cuda.Stream()          # dedicated stream: handle != 0
         self.h = self.stream.cuda_stream
         self.streams = [self.stream]
@@ -269,13 +275,23 @@ class GpuEngine:
 
 # ------------------------------------------------------------------ CPU baseline
 
-def cpu_baseline(batch, budget_s: float):
+def host_cores() -> int:
+    """The cores this process may run on (its affinity mask: cgroup / taskset limits
+    included), not the machine's count."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
+def cpu_baseline(batch, budget_s: float, threads: int = 0):
     """The oracle's C restatement of packet.cs:142-160 (kind "port": the C# reference
-    cannot run here), timed on this host on a bounded sample of the same batch."""
+    cannot run here), timed on this host on a bounded sample of the same batch: one
+    thread, and every core of the affinity mask (static packet partition, pthreads)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     lib = oracle.OracleLib()
-    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1))
+    threads = threads or host_cores()
     res = {}
     for label, th in (("1thread", 1), ("all", threads)):
         # sample: the first packets of the batch, sized to ~budget_s of work
@@ -325,22 +341,27 @@ def make_batches(cfg: str, rotate: int, rank: int, world: int = 1):
     return out
 
 
+PRODUCT_PATHS = (0, 1, 2, 13, 17)          # built in libenethip.so (the rest: libenethip_diag.so)
+
+
 def kernel_name(args, list_launch: bool = False) -> str:
-    """The dominant kernel of the measured entry point (as rocprofv3 names it)."""
+    """The dominant kernel of the measured entry point (as rocprofv3 names it:
+    crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT>)."""
     path = getattr(args, "path", 0)
     if list_launch and path == 13 and args.lanes in (0, 4, 8) and not args.binned:
         # batch lists: the lean kernel's list instance, 8 lanes per packet unless set
         return f"crc32_lean_list_kernel<{3 if args.lanes in (0, 8) else 2}, 16, 2>"
-    lanes = args.lanes or 8                       # the library's default (auto_lanes)
+    lanes = args.lanes or (4 if args.binned else 8)   # the library's defaults (auto_lanes / binned)
     lg = {4: 2, 8: 3}.get(lanes)
-    if path and path not in (17, 18):
+    if path and path not in (17, 18, 21):
         return f"kernel path {path}"
     if args.binned:
-        return (f"crc32_vring_kernel<{lg}, 0, 0, 0, 1>" if path in (17, 18)
+        return (f"crc32_vring_kernel<{lg}, 0, 0, 0, 1, 0, 1>" if path == 17
                 else f"crc32_lean_kernel<0, {lg}, 16, 2, 128>")
     if lg is None:
         return "crc32_stream_kernel / crc32_direct_kernel"
-    return f"crc32_vring_kernel<{lg}, 0{', 0, 1' if path == 18 else ''}>"
+    nt, rot = (1 if path == 18 else 0), (0 if path == 21 else 1)
+    return f"crc32_vring_kernel<{lg}, 0, {nt}, 0, 0, 0, {rot}>"
 
 
 def load_traffic(cfg: str):
@@ -359,7 +380,8 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
         args.gpus = ws
     dist = dist_init(ws)
     batches = make_batches(args.config, args.rotate, rank, ws)
-    eng = (engine_factory or GpuEngine)(local, batches, args.lanes, args.wgs)
+    diag = args.path not in PRODUCT_PATHS
+    eng = (engine_factory or GpuEngine)(local, batches, args.lanes, args.wgs, *((diag,) if diag else ()))
     if hasattr(eng, "set_streams"):
         eng.set_streams(args.streams)
     if args.path:
@@ -415,6 +437,15 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
     r_ms = eng.region_ms(lfn, nk)
     k_ms, span_ms = eng.kernel_ms(lfn, nk)
     p_ms = eng.region_ms(eng.probe, nk)
+    # sustained: the same serial launches over a region of --sustain-ms (the burst
+    # value above is a short replay; a box's clocks settle over several ms of load)
+    sus = None
+    if args.sustain_ms > 0 and hasattr(eng, "launch"):
+        nsus = max(nk, int(args.sustain_ms / max(r_ms, 1e-3)))
+        s_ms = eng.region_ms(lambda k: eng.launch(*plan[k % len(plan)]), nsus)
+        sus = {"GiBps": round(float(batches[0].payload_bytes) * sum(plan[k % len(plan)][1] for k in range(nsus)) /
+                              (s_ms * nsus * 1e-3) / GIB, 1),
+               "launches": nsus, "ms": round(s_ms * nsus, 2)}
     per_launch = float(batches[0].payload_bytes) * sum(c for _, c in plan[:nk]) / nk
     probe_bytes = float((batches[0].payload.nbytes // 16) * 16)
     achieved = per_launch / (r_ms * 1e-3) / 1e9
@@ -422,7 +453,7 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
-        cpu = (cpu_factory or cpu_baseline)(batches[0], args.cpu_seconds)
+        cpu = (cpu_factory or cpu_baseline)(batches[0], args.cpu_seconds, args.cpu_threads)
 
     if rank == 0:
         traffic = load_traffic(args.config)
@@ -454,8 +485,9 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
                 "entry": ("enet_hip_crc32_batch_device_binned" if args.binned else
                           "enet_hip_crc32_batch_list_device" if per_launch_steps > 1 else
                           "enet_hip_crc32_batch_device"),
-                "workgroups_per_cu": args.wgs,
+                "workgroups_per_cu": args.wgs or "default (2)",
                 "launch": args.launch,
+                "kernel_path": args.path,
             },
             "hbm_read_frac": round(value * GIB / 1e9 / (HBM_PEAK_GBPS * ws), 4),
             "roofline": {
@@ -472,14 +504,15 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
                 "kernel_ms_bracketed_median": round(k_ms, 5),
                 "read_probe_GBps": round(probe, 1),
             },
+            "sustained": sus,
             "cpu_baseline": None if cpu is None else {
                 "value": round(cpu["all"]["gibps"], 3),
                 "unit": "GiB/s",
                 "cores": cpu["all"]["threads"],
                 "kind": "port",
                 "sample": f"oracle C restatement of packet.cs:142-160, first {cpu['all']['packets']} packets "
-                          f"of the cfg batch x {cpu['all']['reps']} reps; 1 thread: "
-                          f"{cpu['1thread']['gibps']:.3f} GiB/s",
+                          f"of the cfg batch x {cpu['all']['reps']} reps on {cpu['all']['threads']} threads "
+                          f"(the affinity mask's cores); 1 thread: {cpu['1thread']['gibps']:.3f} GiB/s",
             },
         }
         print(json.dumps(line), flush=True)

@@ -7,7 +7,8 @@
 // single 1.4 KB DGRAM is far below what one kernel launch costs, so this entry
 // point never touches the GPU and can never fail (SURVEY.md §8b "Errors").  It is
 // slicing-by-8 over the same register algebra, bit-identical to the reference's
-// byte loop (tests/test_cpu_callback.py checks it against every golden vector).
+// byte loop (tests/test_library_cpu.py checks it against every golden vector and
+// random gather lists; tests/test_sanitizers.py runs it under ASan + UBSan).
 #include <cstddef>
 #include <cstdint>
 #include <cstring>

@@ -402,7 +402,9 @@ __global__ void __launch_bounds__(G::kThreads) crc32_stream_kernel(PacketArgs pa
     while (!done) unroll_slots<G::kNB>(stage);
 }
 
+#ifdef ENET_HIP_DIAG
 // ============================================================ register-stream kernel
+// (diagnostics library only: a comparison point kept for the sweeps)
 //
 // Same per-packet arithmetic as crc32_stream_kernel (strided lanes, advancing
 // tables, rotation, table-driven finish), but each lane loads its own blocks
@@ -709,6 +711,8 @@ __global__ void __launch_bounds__(G::kThreads) crc32_vstream_kernel(PacketArgs p
     }
 }
 
+#endif  // ENET_HIP_DIAG
+
 // ============================================================ direct kernel
 //
 // General direct-load path (every block loaded straight into VGPRs, any P):
@@ -804,6 +808,7 @@ struct GatherArgs {
     const uint32_t* seg_first;
     uint64_t n;
     uint32_t* out;
+    uint64_t segs;      // segments with a CRC in seg_crc (the join's bound; the host's segCount)
 };
 
 // One lane per DGRAM; segments folded in order and joined by the carry-combine.
@@ -844,7 +849,11 @@ __global__ void __launch_bounds__(kThreads) crc32_gather_join_kernel(GatherArgs 
                                                                      KernelTables tb) {
     const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
     for (uint64_t d = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; d < ga.n; d += stride) {
-        const uint32_t s0 = ga.seg_first[d], s1 = ga.seg_first[d + 1];
+        // segFirst lives in device memory, so the host cannot check segFirst[n] ==
+        // segCount: clamp to the segments the binned pass filled (a short segCount
+        // then gives wrong CRCs for the DGRAMs past it, never a read past seg_crc)
+        const uint32_t s1 = static_cast<uint32_t>(min<uint64_t>(ga.seg_first[d + 1], ga.segs));
+        const uint32_t s0 = min(ga.seg_first[d], s1);
         uint32_t reg = 0xFFFFFFFFu;
         bool first = true;
         for (uint32_t q = s0; q < s1; ++q) {
@@ -1062,17 +1071,22 @@ struct StreamVariant {
                        const KernelTables& tb) {
         if (mode == 1)
             hipLaunchKernelGGL((crc32_stream_kernel<1, G>), dim3(grid), dim3(G::kThreads), G::kLds, st, pa, tb);
+#ifdef ENET_HIP_DIAG
         else if (abl == 1)
             hipLaunchKernelGGL((crc32_stream_kernel<0, G, 1>), dim3(grid), dim3(G::kThreads), G::kLds, st, pa, tb);
         else if (abl == 2)
             hipLaunchKernelGGL((crc32_stream_kernel<0, G, 2>), dim3(grid), dim3(G::kThreads), G::kLds, st, pa, tb);
+#endif
         else
             hipLaunchKernelGGL((crc32_stream_kernel<0, G, 0>), dim3(grid), dim3(G::kThreads), G::kLds, st, pa, tb);
+        (void)abl;
     }
     static int setup() {
         const void* fns[] = {reinterpret_cast<const void*>(crc32_stream_kernel<0, G, 0>),
+#ifdef ENET_HIP_DIAG
                              reinterpret_cast<const void*>(crc32_stream_kernel<0, G, 1>),
                              reinterpret_cast<const void*>(crc32_stream_kernel<0, G, 2>),
+#endif
                              reinterpret_cast<const void*>(crc32_stream_kernel<1, G, 0>)};
         for (const void* f : fns) {
             const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, G::kLds);
@@ -1082,11 +1096,21 @@ struct StreamVariant {
     }
 };
 
+// Kernel paths (enet_hip_set_kernel_path): 2 + k = stream geometry k (k < 6), then
+// 5 register-stream geometries, 4 lean geometries, the vring variants.  The product
+// library builds stream geometry 0 (16 lanes per packet) and lean geometry 0; the
+// rest are sweep-only (ENET_HIP_DIAG).
+constexpr int kStreamPaths = 6, kVStreamPaths = 5;
+#ifdef ENET_HIP_DIAG
 using StreamGeoms = std::tuple<StreamGeom<16, 1, 2>, StreamGeom<11, 1, 3>, StreamGeom<8, 1, 4>,
                                StreamGeom<8, 2, 2>, StreamGeom<6, 2, 3>, StreamGeom<10, 1, 3>>;
-constexpr int kNumStreamGeoms = std::tuple_size<StreamGeoms>::value;
+#else
+using StreamGeoms = std::tuple<StreamGeom<16, 1, 2>>;
+#endif
+constexpr int kNumStreamGeoms = kStreamPaths;
 constexpr int kStreamDefault = 0;
 
+#ifdef ENET_HIP_DIAG
 template <class G>
 struct VStreamVariant {
     static void launch(int mode, int abl, unsigned grid, hipStream_t st, const PacketArgs& pa,
@@ -1116,14 +1140,28 @@ struct VStreamVariant {
 
 // register-stream geometries: paths 2 + kNumStreamGeoms + index
 using VStreamGeoms = std::tuple<VGeom<16, 3, 3>, VGeom<16, 2, 3>, VGeom<16, 4, 4>, VGeom<8, 4, 4>, VGeom<8, 6, 6>>;
-constexpr int kNumVStreamGeoms = std::tuple_size<VStreamGeoms>::value;
+static_assert(std::tuple_size<VStreamGeoms>::value == kVStreamPaths, "path numbering");
+static_assert(std::tuple_size<StreamGeoms>::value == kStreamPaths, "path numbering");
+#endif  // ENET_HIP_DIAG
+constexpr int kNumVStreamGeoms = kVStreamPaths;
 // lean kernel geometries (crc32_lean.hip): paths kLeanPath0 + geom; path 0 runs geom 0
 constexpr int kLeanPath0 = 2 + kNumStreamGeoms + kNumVStreamGeoms;
 constexpr int kVringPath = kLeanPath0 + kLeanGeoms;     // crc32_vring.hip (path 0 for checksum batches)
-constexpr int kVringAltPath = kVringPath + 1;           // the same with the other stage-load cache policy
-constexpr bool kVringNt = false;                        // the default policy: nontemporal stage loads
+constexpr int kVringAltPath = kVringPath + 1;           // the same with nontemporal stage loads
 constexpr int kVringWalkPath = kVringAltPath + 1;       // vring, workgroups walking contiguous group ranges
-constexpr int kVringWalkAltPath = kVringWalkPath + 1;   // the same with the other stage-load cache policy
+constexpr int kVringWalkAltPath = kVringWalkPath + 1;   // the same with nontemporal stage loads
+constexpr int kVringInOrderPath = kVringWalkAltPath + 1;   // vring, stages in window order (not tail-first)
+constexpr int kMaxPath = kVringInOrderPath;
+
+// Paths this library builds: all in the diagnostics library; in the product one
+// the default (0), direct (1), stream geometry 0 (2), lean geometry 0 and vring.
+bool path_built(int path) {
+#ifdef ENET_HIP_DIAG
+    return path >= 0 && path <= kMaxPath;
+#else
+    return path == 0 || path == 1 || path == 2 || path == kLeanPath0 || path == kVringPath;
+#endif
+}
 
 template <size_t I = 0>
 void launch_stream(int geom, int mode, int abl, int num_cus, uint64_t groups, hipStream_t st,
@@ -1140,6 +1178,7 @@ void launch_stream(int geom, int mode, int abl, int num_cus, uint64_t groups, hi
     }
 }
 
+#ifdef ENET_HIP_DIAG
 template <size_t I = 0>
 void launch_vstream(int geom, int mode, int abl, int num_cus, uint64_t groups, hipStream_t st,
                     const PacketArgs& pa, const KernelTables& tb) {
@@ -1163,6 +1202,7 @@ int setup_vstream() {
     }
     return 0;
 }
+#endif  // ENET_HIP_DIAG
 
 template <size_t I = 0>
 int setup_stream() {
@@ -1174,15 +1214,21 @@ int setup_stream() {
 }
 
 // vring workgroups per CU of one launch (enet_hip_set_tuning's workgroups_per_cu,
-// at most 2: the LDS and 64-VGPR budget of two 16-wave workgroups)
-int vring_wgs(const enet_hip_context* ctx) { return ctx->wgs_per_cu >= 2 ? 2 : 1; }
+// at most 2: the LDS and 64-VGPR budget of two 16-wave workgroups).  Default (0):
+// two, the configuration bench.py measures (profiles/r02e_*: the 5-batch lists
+// at two workgroups per CU against one).
+int vring_wgs(const enet_hip_context* ctx) { return ctx->wgs_per_cu == 1 ? 1 : 2; }
 bool vring_path(const enet_hip_context* ctx) {
-    return ctx->path == 0 || (ctx->path >= kVringPath && ctx->path <= kVringWalkAltPath);
+    return ctx->path == 0 || (ctx->path >= kVringPath && ctx->path <= kVringInOrderPath);
 }
-bool vring_nt(const enet_hip_context* ctx) {
-    return (ctx->path == kVringAltPath || ctx->path == kVringWalkAltPath) ? !kVringNt : kVringNt;
+VrVariant vring_variant(const enet_hip_context* ctx, bool lists) {
+    VrVariant v;
+    v.nt = ctx->path == kVringAltPath || ctx->path == kVringWalkAltPath;
+    v.walk = (ctx->path == kVringWalkPath || ctx->path == kVringWalkAltPath) && !ctx->trace;
+    v.in_order = ctx->path == kVringInOrderPath;
+    v.abl = lists ? ctx->vr_abl : 0;
+    return v;
 }
-bool vring_walk(const enet_hip_context* ctx) { return ctx->path == kVringWalkPath || ctx->path == kVringWalkAltPath; }
 
 int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStream_t st) {
     if (pa.n == 0) return 0;
@@ -1195,8 +1241,8 @@ int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStr
     // profiles/r02d_cfg3_*; the vring records instance on path 17 / 18)
     if (mode == 0 && (pa.lg == 2 || pa.lg == 3) && ctx->ablation == 0 && vring_path(ctx) &&
         (!pa.meta4 || ctx->path != 0))
-        return vring_launch(pa.lg, ctx->num_cus * (pa.meta4 ? 1 : vring_wgs(ctx)), vring_nt(ctx) && !pa.meta4, st, pa,
-                            tb, ctx->d_basis2, vring_walk(ctx));
+        return vring_launch(pa.lg, ctx->num_cus * (pa.meta4 ? 1 : vring_wgs(ctx)),
+                            pa.meta4 ? VrVariant{} : vring_variant(ctx, false), st, pa, tb, ctx->d_basis2);
     if (ctx->path != 1 && pa.lg >= 2 && pa.lg <= 4) {
         const bool lean_path = (ctx->path >= kLeanPath0 && ctx->path < kVringPath) || (ctx->path == 0 && ctx->ablation == 0);
         if (lean_path && pa.lg <= 3)
@@ -1206,8 +1252,10 @@ int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStr
         const int geom = (ctx->path == 0 || ctx->path >= kLeanPath0) ? kStreamDefault : ctx->path - 2;
         if (geom < kNumStreamGeoms)
             launch_stream(geom, mode, ctx->ablation, ctx->num_cus, groups, st, pa, tb);
+#ifdef ENET_HIP_DIAG
         else
             launch_vstream(geom - kNumStreamGeoms, mode, ctx->ablation, ctx->num_cus, groups, st, pa, tb);
+#endif
     } else {
         const uint64_t tasks = pa.n << pa.lg;
         const unsigned grid = grid_for(ctx, tasks);
@@ -1282,7 +1330,9 @@ int enet_hip_context_create(int device, enet_hip_context** out) {
         if ((rc = herr(hipMemcpy(ctx->d_basis2, ht.basis2.data(), ht.basis2.size() * 4, hipMemcpyHostToDevice)))) break;
         if ((rc = vring_setup())) break;
         if ((rc = setup_stream())) break;
+#ifdef ENET_HIP_DIAG
         if ((rc = setup_vstream())) break;
+#endif
         if ((rc = lean_setup())) break;
         if ((rc = herr(hipFuncSetAttribute(reinterpret_cast<const void*>(crc32_direct_kernel<0>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTableBytes)))) break;
@@ -1329,6 +1379,7 @@ int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgro
     return 0;
 }
 
+#ifdef ENET_HIP_DIAG
 int enet_hip_diag_ablation(enet_hip_context* ctx, int mode) {
     if (!ctx || mode < 0 || mode > 131071) return -static_cast<int>(hipErrorInvalidValue);
     const int prio = (mode & 1024) ? 2 : (mode >> 3) & 1;    // 8: static / 1024: progress priority
@@ -1345,10 +1396,20 @@ int enet_hip_diag_trace(enet_hip_context* ctx, uint64_t* deviceBuffer) {
     return 0;
 }
 
+#endif  // ENET_HIP_DIAG
+
 int enet_hip_set_kernel_path(enet_hip_context* ctx, int path) {
-    if (!ctx || path < 0 || path > kVringWalkAltPath) return -static_cast<int>(hipErrorInvalidValue);
+    if (!ctx || !path_built(path)) return -static_cast<int>(hipErrorInvalidValue);
     ctx->path = path;
     return 0;
+}
+
+int enet_hip_is_diagnostics_build(void) {
+#ifdef ENET_HIP_DIAG
+    return 1;
+#else
+    return 0;
+#endif
 }
 
 int enet_hip_crc32_batch_device(enet_hip_context* ctx, const uint8_t* bytes, const uint64_t* offsets,
@@ -1402,8 +1463,8 @@ int enet_hip_crc32_batch_list_device(enet_hip_context* ctx, const ENetHipBatch* 
             for (size_t b = b0; b < std::min(batchCount, b0 + kVrMaxBatches); ++b)
                 bl.b[bl.count++] = VrBatch{batches[b].bytes, batches[b].offsets, batches[b].lengths, batches[b].out,
                                            static_cast<uint64_t>(batches[b].count), 0u};
-            const int rc = vring_launch_list(lg, ctx->num_cus * vring_wgs(ctx), vring_nt(ctx), ctx->vr_abl, st, bl, tb,
-                                             ctx->d_basis2, ctx->trace, false, vring_walk(ctx) && !ctx->trace);
+            const int rc = vring_launch_list(lg, ctx->num_cus * vring_wgs(ctx), vring_variant(ctx, true), st, bl, tb,
+                                             ctx->d_basis2, ctx->trace);
             if (rc) return rc;
         }
         return 0;
@@ -1546,7 +1607,7 @@ int enet_hip_crc32_gather_device(enet_hip_context* ctx, const uint8_t* bytes, co
     if (dgramCount == 0) return 0;
     if (!bytes || !segOffsets || !segLengths || !segFirst || !out) return -static_cast<int>(hipErrorInvalidValue);
     ENH_CHECK(hipSetDevice(ctx->device));
-    GatherArgs ga{bytes, segOffsets, segLengths, segFirst, dgramCount, out};
+    GatherArgs ga{bytes, segOffsets, segLengths, segFirst, dgramCount, out, ~0ull};
     const unsigned grid = grid_for(ctx, dgramCount);
     hipLaunchKernelGGL(crc32_gather_kernel, dim3(grid), dim3(kThreads), kLdsTableBytes,
                        stream ? static_cast<hipStream_t>(stream) : ctx->stream, ga, tables_of(ctx));
@@ -1576,7 +1637,7 @@ int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* by
                                                           workspace, bws, st);
         if (rc) return rc;
     }
-    GatherArgs ga{bytes, segOffsets, segLengths, segFirst, dgramCount, out};
+    GatherArgs ga{bytes, segOffsets, segLengths, segFirst, dgramCount, out, segCount};
     const unsigned grid = grid_for(ctx, dgramCount);
     hipLaunchKernelGGL(crc32_gather_join_kernel, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx));
     return herr(hipGetLastError());
@@ -1604,6 +1665,12 @@ int enet_hip_fragment_reassemble_device(enet_hip_context* ctx, const uint8_t* by
     // frag_copy_kernel / frag_serial_kernel)
     const size_t claims = std::max<size_t>(1, slotCount * wordsPerMsg * 32u);
     const size_t need = claims + slotCount + 1;
+    // Refill on any layout change that could expose words not in the filled state.
+    // d_claim_cap is the END OF THE FILLED LAYOUT (set to `need` at each fill, not
+    // the allocation size): with the same claim-word count, a call whose winner
+    // counts and flag fit in [claims, d_claim_cap) reads words the last fill zeroed
+    // and every call since restored to zero; a larger slotCount refills
+    // (tests/test_gpu_fragments.py test_fragments_scratch_layout_changes).
     if (need > ctx->d_claim_cap || claims != ctx->d_claim_words) {
         ENH_CHECK(hipStreamSynchronize(st));
         if (need > ctx->d_claim_cap) {

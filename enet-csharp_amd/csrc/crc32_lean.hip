@@ -615,6 +615,7 @@ struct LeanVariant {
     }
     static void launch(int mode, int lg, int abl, int num_cus, hipStream_t st, const PacketArgs& pa,
                        const KernelTables& tb) {
+#ifdef ENET_HIP_DIAG
         if (mode == 0 && abl) {
             switch (abl) {                                   // diagnostics: 8-lane packets only
                 case 1: go_abl<3, 1>(num_cus, st, pa, tb); break;
@@ -631,6 +632,8 @@ struct LeanVariant {
             }
             return;
         }
+#endif
+        (void)abl;
         if (mode == 0) {
             if (lg == 2) go<0, 2>(num_cus, st, pa, tb);
             else go<0, 3>(num_cus, st, pa, tb);
@@ -697,17 +700,24 @@ int lean_launch_vlist(int lg, int num_cus, hipStream_t st, const ENetHipVerifyBa
 
 int lean_setup() {
     int rc = LeanVariant<16, 2>::setup();
-    return rc ? rc : LeanVariant<12, 3>::setup();
+#ifdef ENET_HIP_DIAG
+    if (!rc) rc = LeanVariant<12, 3>::setup();
+#endif
+    return rc;
 }
 
 int lean_launch(int mode, int lg, int geom, int abl, int num_cus, hipStream_t st, const PacketArgs& pa,
                 const KernelTables& tb) {
     if (lg != 2 && lg != 3) return -static_cast<int>(hipErrorInvalidValue);
+#ifdef ENET_HIP_DIAG
     // geoms 2, 3 (tuning sweeps): checksum mode, 8 lanes per packet only
     if (geom == 2 && mode == 0 && lg == 3) LeanVariant<14, 3>::go_abl<3, 0>(num_cus, st, pa, tb);
     else if (geom == 3 && mode == 0 && lg == 3) LeanVariant<10, 4>::go_abl<3, 0>(num_cus, st, pa, tb);
     else if (geom == 1) LeanVariant<12, 3>::launch(mode, lg, 0, num_cus, st, pa, tb);
-    else LeanVariant<16, 2>::launch(mode, lg, abl, num_cus, st, pa, tb);
+    else
+#endif
+        LeanVariant<16, 2>::launch(mode, lg, abl, num_cus, st, pa, tb);
+    (void)geom;
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : -static_cast<int>(e);
 }

@@ -333,14 +333,38 @@ struct VrIt {
 // BIN = 1: the batch's metadata are length-binned records (VrBatch::off points at
 // them, 4 dwords per packet), read in record order; packet r's CRC goes to
 // out[record r's index] (enet_hip_crc32_batch_device_binned).  One workgroup per CU.
-template <int LG, int TR = 0, int NT = 0, int ABL = 0, int BIN = 0, int WK = 0>
+// ROT = 1: the tail-first stage order (below); 0 = stages in order (kernel path 17).
+template <int LG, int TR = 0, int NT = 0, int ABL = 0, int BIN = 0, int WK = 0, int ROT = 1>
 __global__ void __launch_bounds__(64 * kVrW) __attribute__((amdgpu_waves_per_eu(8, 8), amdgpu_num_vgpr(24)))
 crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_t* trace) {
     constexpr uint32_t P = 1u << LG, kPk = 64u >> LG;
-    // The lane id and everything derived from it (k, p, the fold's lane constants)
-    // is recomputed in every ring iteration from a fresh v_mbcnt (asm volatile, so
-    // not hoisted): held across the loop, those ten values were what pushed the
-    // kernel past 64 VGPRs.
+    // Tail-first stage order.  A group of S > 1 stages runs its last stage first,
+    // then stages 0 .. S-2.  Packed packets share a 128-byte line at every packet
+    // boundary: packet j's last stage reads it, packet j+1's first stage too.  In
+    // order, those two reads are S-1 stages apart, long enough for the XCD's L2 to
+    // evict the line (FETCH_SIZE 1.105 x the payload on cfg2); tail first, they are
+    // adjacent steps.  Lane k folds its last-stage block from a zero register into
+    // rt, the other stages as before into reg; fold(b ^ r) = fold(b) ^ adv(r), so
+    // the packet's lane register is rt ^ adv(reg), adv(r) = r x^(256 P) = four
+    // lookups in the advancing tables T'_31 .. T'_28 (tests/kernel_model.py,
+    // vring_packet(rotate=True)).  Binned records are not neighbours in memory: no
+    // gain there, so the records instance keeps the plain order.
+    constexpr bool kRot = ROT && !BIN && !(ABL & 8);
+    // the window stage of step j of a group of S stages
+    auto stage_of = [](uint32_t j, uint32_t S) __attribute__((always_inline)) -> uint32_t {
+        if constexpr (!kRot) return j;
+        return S > 1u ? (j == 0u ? S - 1u : j - 1u) : 0u;
+    };
+    // ... and its inverse (~0u stays ~0u)
+    auto step_of = [](uint32_t a, uint32_t S) __attribute__((always_inline)) -> uint32_t {
+        if constexpr (!kRot) return a;
+        return (S <= 1u || a == ~0u) ? a : (a == S - 1u ? 0u : a + 1u);
+    };
+    // The lane id and everything derived from it (k, p, the fold's lane constants):
+    // kept live across the ring loop in the in-order instances; the tail-first and
+    // records instances recompute the lane id every iteration from a fresh v_mbcnt
+    // (asm volatile, so not hoisted) -- their rt / record register needs the VGPR
+    // room, and held across the loop those values made hipcc spill.
     uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t wv = static_cast<uint64_t>(blockIdx.x) * kVrW + wave;
@@ -479,7 +503,7 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
                 pe = 0;
             }
         }
-        const uint32_t q0 = 32u * (lane_k() + P * pst);
+        const uint32_t q0 = 32u * (lane_k() + P * stage_of(pst, pstages));
         const uint32_t hs16 = lane & 16u;                    // this lane takes the block's halves swapped
         // (ABL & 8, diagnostics: instruction j of a stage reads bytes 16 P j + 16 k)
         const uint32_t a0 = (ABL & 8) ? 32u * P * pst + 16u * lane_k() : q0 + hs16;
@@ -544,6 +568,7 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
 
     // ---- consumer
     uint32_t reg = 0, clz = 0, ce = 0, cs = 0, cstages = 0, nedge = ~0u;
+    uint32_t rt = 0;                                         // kRot: the last stage's fold
     uint32_t* cout = nullptr;                                // the CRCs of the group's packets (BIN: the batch's)
     uint32_t cidx = 0;                                       // BIN: the caller index of the lane's packet
     uint64_t crem = 0;                                       // packets of its batch from the group's first
@@ -553,6 +578,8 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
         const uint32_t wh = clz >> 5, wl = (ce - 1u) >> 5;
         uint32_t h = (live && (clz & 15u) && (wh & (P - 1u)) == lane_k()) ? wh >> LG : ~0u;
         uint32_t t = (live && (ce & 15u) && (wl & (P - 1u)) == lane_k()) ? wl >> LG : ~0u;
+        h = step_of(h, cstages);
+        t = step_of(t, cstages);
         h = h >= from ? h : ~0u;
         t = t >= from ? t : ~0u;
         return wave_min_u(min(h, t));
@@ -581,27 +608,42 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
     bool done = false;
     auto iteration = [&](auto sc) __attribute__((always_inline)) {
         constexpr uint32_t S = decltype(sc)::value;
-        if constexpr (kVrLaneRecompute || BIN) lane = vr_lane();   // (BIN: its record register needs the room)
+        if constexpr (kVrLaneRecompute || BIN || kRot) lane = vr_lane();   // (BIN: its record register needs the room; kRot: rt)
         produce(std::integral_constant<uint32_t, S ^ 1u>{}, std::integral_constant<int, static_cast<int>(S)>{});
+        const uint32_t cst = stage_of(cs, cstages);          // the window stage this step folds
+        const bool tail_first = kRot && cs == 0u && cstages > 1u;   // (wave-uniform)
+        const uint32_t rin = tail_first ? 0u : reg;
         uint32_t d[8];
         if (cs == nedge) {                                   // head / tail pieces: keep [clz, ce) only
             u32x4 A, B;
             vr_read_stage<S>(A, B);
-            const uint32_t q0 = 32u * (lane_k() + P * cs);               // windows < 2 GiB: differences fit int32
+            const uint32_t q0 = 32u * (lane_k() + P * cst);              // windows < 2 GiB: differences fit int32
             if constexpr (!(ABL & 1))
                 vr_edge_mask(A, B, make_vr_sched(lane).hs, static_cast<int32_t>(clz - q0), static_cast<int32_t>(ce - q0));
             nedge = next_edge(cs + 1u);
-            vr_shuffle(reg, lane, A, B, d);
+            vr_shuffle(rin, lane, A, B, d);
         } else {
-            vr_shuffle_slot<S>(reg, lane, d);
+            vr_shuffle_slot<S>(rin, lane, d);
         }
         uint32_t nr;
         if constexpr (ABL & 2)
             nr = xor3(xor3(d[0], d[1], d[2]), xor3(d[3], d[4], d[5]), d[6] ^ d[7]);
         else
             nr = vr_lookups(d, make_vr_sched(lane));
-        reg = 32u * (lane_k() + P * cs) < ce ? nr : reg;            // the lane's block k + P cs is in the window
+        const bool inw = 32u * (lane_k() + P * cst) < ce;           // the lane's block k + P cst is in the window
+        if (tail_first) rt = inw ? nr : 0u;
+        else reg = inw ? nr : reg;
         if (++cs == cstages) {
+            if (kRot && cstages > 1u && 32u * (lane_k() + P * (cstages - 1u)) < ce) {
+                // the last-stage block came first: reg = rt ^ reg x^(256 P)
+                uint32_t x[4];
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const uint32_t sel = 0x0C0C0000u | ((4u + b) << 8);      // byte1 = byte b of reg, byte0 = column
+                    x[b] = lds_load(__builtin_amdgcn_perm(reg, col_byte(31u - b), sel));
+                }
+                reg = xor3(x[0], x[1], x[2]) ^ x[3] ^ rt;
+            }
             // lane k is o = (k - nb) mod P blocks past the window end: x^(-256 o)
             const uint32_t nb = (ce + 31u) >> 5;
             const uint32_t o = (lane_k() - nb) & (P - 1u);
@@ -651,57 +693,89 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
 
 // ---------------------------------------------------------------- host side
 
-template <int LG, int TR = 0, int NT = 0, int ABL = 0, int BIN = 0, int WK = 0>
+template <int LG, int TR = 0, int NT = 0, int ABL = 0, int BIN = 0, int WK = 0, int ROT = 1>
 const void* vring_fn() {
-    return reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK>);
+    return reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT>);
 }
 const void* vring_pick_bin(int lg) { return lg == 2 ? vring_fn<2, 0, 0, 0, 1>() : vring_fn<3, 0, 0, 0, 1>(); }
 
-// The product instances: 64 VGPRs (WPE 8), one or two workgroups per CU.  With a
-// trace buffer: the same kernel writing per-wave timestamps.  nt: the stage loads
-// with the nontemporal cache policy.  Measured and not kept: 3 and 4 ring slots and
-// a binned-records variant (its record register was copied by hipcc between load
-// and wait: tools/isa_inflight_check.py).
-const void* vring_pick(int lg, bool trace, bool nt, int abl, bool walk) {
-    if (walk && !trace && !abl)
+// The product instances: 64 VGPRs (WPE 8), one or two workgroups per CU, tail-first
+// stage order.  The diagnostics library (ENET_HIP_DIAG) adds the sweep variants: a
+// trace buffer (per-wave timestamps), nt stage loads, workgroup walks, the in-order
+// stage schedule and the ablations (wrong CRCs by design).  Null = not built here.
+// Measured and not kept: 3 and 4 ring slots and a binned-records variant (its
+// record register was copied by hipcc between load and wait).
+const void* vring_pick(int lg, bool trace, const VrVariant& v) {
+    if (lg != 2 && lg != 3) return nullptr;
+    const bool plain = !trace && !v.nt && !v.abl && !v.walk && !v.in_order;
+    if (plain) return lg == 2 ? vring_fn<2>() : vring_fn<3>();
+#ifdef ENET_HIP_DIAG
+    const bool nt = v.nt;
+    const int abl = v.abl;
+    if (v.in_order) {
+        if (trace || abl || v.walk) return nullptr;
+        return lg == 2 ? (nt ? vring_fn<2, 0, 1, 0, 0, 0, 0>() : vring_fn<2, 0, 0, 0, 0, 0, 0>())
+                       : (nt ? vring_fn<3, 0, 1, 0, 0, 0, 0>() : vring_fn<3, 0, 0, 0, 0, 0, 0>());
+    }
+    if (v.walk) {
+        if (trace || abl) return nullptr;
         return lg == 2 ? (nt ? vring_fn<2, 0, 1, 0, 0, 1>() : vring_fn<2, 0, 0, 0, 0, 1>())
                        : (nt ? vring_fn<3, 0, 1, 0, 0, 1>() : vring_fn<3, 0, 0, 0, 0, 1>());
-    if (abl == 8 && lg == 3 && !trace) return nt ? vring_fn<3, 0, 1, 8>() : vring_fn<3, 0, 0, 8>();
-    if (abl == 19 && lg == 2 && !trace && !nt) return vring_fn<2, 0, 0, 19>();
-    if (abl == 27 && lg == 3 && !trace) return nt ? vring_fn<3, 0, 1, 27>() : vring_fn<3, 0, 0, 27>();
-    if (abl == 19 && lg == 3 && !trace && !nt) return vring_fn<3, 0, 0, 19>();
-    if (abl == 32 && lg == 2 && !trace) return nt ? vring_fn<2, 0, 3>() : vring_fn<2, 0, 2>();   // sc1 / sc0 sc1
-    if (abl && lg == 2 && !trace && !nt)
-        return abl == 1 ? vring_fn<2, 0, 0, 1>() : abl == 2 ? vring_fn<2, 0, 0, 2>() : abl == 3 ? vring_fn<2, 0, 0, 3>()
-               : abl == 4 ? vring_fn<2, 0, 0, 4>() : vring_fn<2, 0, 0, 6>();
-    if (trace) return lg == 2 ? (nt ? vring_fn<2, 1, 1>() : vring_fn<2, 1>()) : (nt ? vring_fn<3, 1, 1>() : vring_fn<3, 1>());
-    return lg == 2 ? (nt ? vring_fn<2, 0, 1>() : vring_fn<2>()) : (nt ? vring_fn<3, 0, 1>() : vring_fn<3>());
+    }
+    if (trace) {
+        if (abl) return nullptr;
+        return lg == 2 ? (nt ? vring_fn<2, 1, 1>() : vring_fn<2, 1>()) : (nt ? vring_fn<3, 1, 1>() : vring_fn<3, 1>());
+    }
+    if (!abl) return lg == 2 ? vring_fn<2, 0, 1>() : vring_fn<3, 0, 1>();
+    if (abl == 8 && lg == 3) return nt ? vring_fn<3, 0, 1, 8>() : vring_fn<3, 0, 0, 8>();
+    if (abl == 27 && lg == 3) return nt ? vring_fn<3, 0, 1, 27>() : vring_fn<3, 0, 0, 27>();
+    if (abl == 19 && !nt) return lg == 2 ? vring_fn<2, 0, 0, 19>() : vring_fn<3, 0, 0, 19>();
+    if (abl == 32 && lg == 2) return nt ? vring_fn<2, 0, 3>() : vring_fn<2, 0, 2>();   // sc1 / sc0 sc1
+    if (lg == 2 && !nt) {
+        switch (abl) {
+            case 1: return vring_fn<2, 0, 0, 1>();
+            case 2: return vring_fn<2, 0, 0, 2>();
+            case 3: return vring_fn<2, 0, 0, 3>();
+            case 4: return vring_fn<2, 0, 0, 4>();
+            case 6: return vring_fn<2, 0, 0, 6>();
+            default: break;
+        }
+    }
+#endif
+    return nullptr;
 }
 
 int vring_setup() {
-    for (int lg = 2; lg <= 3; ++lg)
-        for (int t = 0; t < 256; ++t) {
-            const hipError_t e = hipFuncSetAttribute(vring_pick(lg, t & 1, (t >> 1) & 1, t >> 2, false),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, kVrLds);
-            if (e != hipSuccess) return -static_cast<int>(e);
-        }
-    for (int lg = 2; lg <= 3; ++lg)
-        for (int nt = 0; nt < 2; ++nt) {
-            const hipError_t e = hipFuncSetAttribute(vring_pick(lg, false, nt != 0, 0, true),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, kVrLds);
-            if (e != hipSuccess) return -static_cast<int>(e);
-        }
+    auto set = [](const void* fn, int lds) -> int {
+        if (!fn) return 0;
+        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        return e == hipSuccess ? 0 : -static_cast<int>(e);
+    };
+    static const int kAbl[] = {0, 1, 2, 3, 4, 6, 8, 19, 27, 32};
     for (int lg = 2; lg <= 3; ++lg) {
-        const hipError_t e = hipFuncSetAttribute(vring_pick_bin(lg), hipFuncAttributeMaxDynamicSharedMemorySize, kVrLdsBin);
-        if (e != hipSuccess) return -static_cast<int>(e);
+        int rc;
+        if ((rc = set(vring_pick_bin(lg), kVrLdsBin))) return rc;
+        for (int t = 0; t < 2; ++t)
+            for (int nt = 0; nt < 2; ++nt)
+                for (int abl : kAbl)
+                    for (int w = 0; w < 4; ++w) {
+                        VrVariant v;
+                        v.nt = nt != 0;
+                        v.abl = abl;
+                        v.walk = (w & 1) != 0;
+                        v.in_order = (w & 2) != 0;
+                        if ((rc = set(vring_pick(lg, t != 0, v), kVrLds))) return rc;
+                    }
     }
     return 0;
 }
 
-int vring_launch_list(int lg, int max_wgs, bool nt, int abl, hipStream_t st, const VrBatches& bl, const KernelTables& tb,
-                      const uint32_t* basis2, uint64_t* trace, bool bin, bool walk) {
+int vring_launch_list(int lg, int max_wgs, const VrVariant& v, hipStream_t st, const VrBatches& bl,
+                      const KernelTables& tb, const uint32_t* basis2, uint64_t* trace, bool bin) {
     if ((lg != 2 && lg != 3) || bl.count > static_cast<uint32_t>(kVrMaxBatches))
         return -static_cast<int>(hipErrorInvalidValue);
+    const void* fn = bin ? vring_pick_bin(lg) : vring_pick(lg, trace != nullptr, v);
+    if (!fn) return -static_cast<int>(hipErrorInvalidValue);   // a variant this library does not build
     // empty batches dropped: the kernel may then read any batch's packet n - 1
     VrBatches a{};
     for (uint32_t b = 0; b < bl.count; ++b)
@@ -718,21 +792,19 @@ int vring_launch_list(int lg, int max_wgs, bool nt, int abl, hipStream_t st, con
     if ((a.groups / (static_cast<uint64_t>(grid) * kVrW) + 2u) * kVrW > 0xFFFFFFF0ull)
         return -static_cast<int>(hipErrorInvalidValue);
     void* args[] = {&a, const_cast<KernelTables*>(&tb), const_cast<const uint32_t**>(&basis2), &trace};
-    const void* fn = bin ? vring_pick_bin(lg) : vring_pick(lg, trace != nullptr, nt, abl, walk);
     const hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(64 * kVrW), args, bin ? kVrLdsBin : kVrLds, st);
     return e == hipSuccess ? 0 : -static_cast<int>(e);
 }
 
-int vring_launch(int lg, int max_wgs, bool nt, hipStream_t st, const PacketArgs& pa, const KernelTables& tb,
-                 const uint32_t* basis2, bool walk) {
+int vring_launch(int lg, int max_wgs, const VrVariant& v, hipStream_t st, const PacketArgs& pa, const KernelTables& tb,
+                 const uint32_t* basis2) {
     if (pa.n == 0) return 0;
     VrBatches bl{};
     bl.count = 1;
     // binned records: the record array rides in the offsets field (BIN instance)
     bl.b[0] = pa.meta4 ? VrBatch{pa.bytes, reinterpret_cast<const uint64_t*>(pa.meta4), nullptr, pa.out, pa.n, 0u}
                        : VrBatch{pa.bytes, pa.off, pa.len, pa.out, pa.n, 0u};
-    return vring_launch_list(lg, max_wgs, nt, 0, st, bl, tb, basis2, pa.meta4 ? nullptr : pa.trace, pa.meta4 != nullptr,
-                             walk && !pa.meta4);
+    return vring_launch_list(lg, max_wgs, v, st, bl, tb, basis2, pa.meta4 ? nullptr : pa.trace, pa.meta4 != nullptr);
 }
 
 }  // namespace enethip

@@ -35,25 +35,36 @@ struct VrBatches {
 };
 static_assert(sizeof(VrBatches) <= 3072, "kernel arguments");
 
-// Set the dynamic-LDS attribute of every vring kernel instance (once per context).
+// Kernel variants.  The product library builds the default alone (all fields at
+// their defaults); the diagnostics library (ENET_HIP_DIAG) also builds the sweep
+// variants: nt = nontemporal stage loads, abl = ablations (crc32_vring.hip; most
+// give wrong CRCs by design), walk = each workgroup takes a contiguous range of the
+// launch's groups in order, in_order = stages in window order (not tail-first).
+struct VrVariant {
+    bool nt = false;
+    int abl = 0;
+    bool walk = false;
+    bool in_order = false;
+};
+
+// Set the dynamic-LDS attribute of every vring kernel instance built (once per context).
 int vring_setup();
 
 // Launch over a list of batches (bl.count <= kVrMaxBatches): one launch, each batch
 // spread over the whole chip in turn, at most max_wgs 16-wave workgroups (the CU
-// count: one per CU; twice that: two); nt = nontemporal stage loads;
-// abl = diagnostics ablation (0 in the product, crc32_vring.hip).  trace = per-wave timestamps or null.
-int vring_launch_list(int lg, int max_wgs, bool nt, int abl, hipStream_t st, const VrBatches& bl, const KernelTables& tb,
-                      const uint32_t* basis2, uint64_t* trace, bool bin = false, bool walk = false);
-// walk = each workgroup takes a contiguous range of the launch's groups in order
-// (its waves walk one region of the arena) instead of rounds spread over the chip.
+// count: one per CU; twice that: two).  trace = per-wave timestamps (diagnostics
+// library) or null.  bin = the batches' metadata are length-binned records {len,
+// off_lo, off_hi, index} (VrBatch::off points at them, len unused): results go to
+// out[index]; 82.5 KiB of LDS, so at most one workgroup per CU (max_wgs = the CU
+// count).  Returns 0 or -hipError_t (-hipErrorInvalidValue for a variant this
+// library does not build).
+int vring_launch_list(int lg, int max_wgs, const VrVariant& v, hipStream_t st, const VrBatches& bl,
+                      const KernelTables& tb, const uint32_t* basis2, uint64_t* trace, bool bin = false);
 
-// bin = the batches' metadata are length-binned records {len, off_lo, off_hi,
-// index} (VrBatch::off points at them, len unused): results go to out[index];
-// 82.5 KiB of LDS, so at most one workgroup per CU (max_wgs = the CU count).
 // Launch the vring kernel over one batch: checksum mode, lanes per packet 2^lg
-// (lg = 2 or 3), at most max_wgs workgroups; pa.meta4 set = binned records.  basis2 = kVrBasisDwords per image (images for
-// P = 1, 4, 8, 16 in that order).  Returns 0 or -hipError_t.
-int vring_launch(int lg, int max_wgs, bool nt, hipStream_t st, const PacketArgs& pa, const KernelTables& tb,
-                 const uint32_t* basis2, bool walk = false);
+// (lg = 2 or 3), at most max_wgs workgroups; pa.meta4 set = binned records.
+// basis2 = kVrBasisDwords per image (images for P = 1, 4, 8, 16 in that order).
+int vring_launch(int lg, int max_wgs, const VrVariant& v, hipStream_t st, const PacketArgs& pa, const KernelTables& tb,
+                 const uint32_t* basis2);
 
 }  // namespace enethip

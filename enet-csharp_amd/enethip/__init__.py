@@ -11,6 +11,11 @@ bench harness:
 
 The GPU path has no fallback: if libenethip.so is missing or the HIP runtime
 reports an error, these calls raise ``ENetHipError``.
+
+``load(diag=True)`` / ``Context(..., diag=True)`` bind libenethip_diag.so instead:
+the same library built with -DENET_HIP_DIAG, which adds the sweep-only kernel
+paths and the diagnostics entry points (``diag_ablation``: WRONG checksums by
+design; ``diag_trace``).  Only tools/ and the sweep tests use it.
 """
 from __future__ import annotations
 
@@ -22,6 +27,7 @@ import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_ROOT, "libenethip.so")
+DIAG_LIB_PATH = os.path.join(PKG_ROOT, "libenethip_diag.so")
 
 # Every symbol include/enet_hip.h declares (tests check the .so exports them all).
 EXPORTED_SYMBOLS = (
@@ -34,9 +40,11 @@ EXPORTED_SYMBOLS = (
     "enet_hip_crc32_batch_multi", "enet_hip_device_alloc",
     "enet_hip_device_free", "enet_hip_host_alloc", "enet_hip_host_free", "enet_hip_memcpy_h2d",
     "enet_hip_memcpy_d2h", "enet_hip_synchronize", "enet_hip_read_probe_device", "enet_hip_set_kernel_path",
-    "enet_hip_diag_ablation", "enet_hip_diag_trace", "enet_hip_fragment_reassemble_device",
+    "enet_hip_is_diagnostics_build", "enet_hip_fragment_reassemble_device",
     "enet_hip_range_compress_device", "enet_hip_range_decompress_device",
 )
+# Declared under #ifdef ENET_HIP_DIAG: exported by libenethip_diag.so only.
+DIAG_SYMBOLS = ("enet_hip_diag_ablation", "enet_hip_diag_trace")
 
 
 class ENetHipBatch(ctypes.Structure):
@@ -63,14 +71,15 @@ class ENetBuffer(ctypes.Structure):
     _fields_ = [("dataLength", ctypes.c_size_t), ("data", ctypes.c_void_p)]
 
 
-_lib = None
+_libs: dict = {}
 
 
-def load(path: str | None = None) -> ctypes.CDLL:
-    global _lib
-    if _lib is not None and path is None:
-        return _lib
-    p = path or LIB_PATH
+def load(path: str | None = None, diag: bool = False) -> ctypes.CDLL:
+    """The product library (or, diag=True, the diagnostics build)."""
+    key = path or (DIAG_LIB_PATH if diag else LIB_PATH)
+    if key in _libs:
+        return _libs[key]
+    p = key
     if not os.path.exists(p):
         raise ENetHipError(f"load {p} (run __graft_entry__.build())", -1)
     L = ctypes.CDLL(p)
@@ -89,10 +98,11 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.enet_hip_error_string.argtypes = [i32]
     L.enet_hip_set_tuning.restype = i32
     L.enet_hip_set_tuning.argtypes = [vp, i32, i32]
-    L.enet_hip_diag_ablation.restype = i32
-    L.enet_hip_diag_ablation.argtypes = [vp, i32]
-    L.enet_hip_diag_trace.restype = i32
-    L.enet_hip_diag_trace.argtypes = [vp, vp]
+    if L.enet_hip_is_diagnostics_build():
+        L.enet_hip_diag_ablation.restype = i32
+        L.enet_hip_diag_ablation.argtypes = [vp, i32]
+        L.enet_hip_diag_trace.restype = i32
+        L.enet_hip_diag_trace.argtypes = [vp, vp]
     L.enet_hip_set_kernel_path.restype = i32
     L.enet_hip_set_kernel_path.argtypes = [vp, i32]
     L.enet_hip_crc32_batch_device.restype = i32
@@ -143,8 +153,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
     L.enet_hip_fragment_reassemble_device.restype = i32
     L.enet_hip_fragment_reassemble_device.argtypes = [vp, vp, vp, vp, vp, sz, u32, vp, vp, vp, vp, vp, u32, vp, sz,
                                                       vp, vp]
-    if path is None:
-        _lib = L
+    _libs[key] = L
     return L
 
 
@@ -194,8 +203,9 @@ def device_count() -> int:
 class Context:
     """One GPU.  Device pointers may be passed as torch tensors or ints."""
 
-    def __init__(self, device: int = 0, lanes_per_packet: int = 0, workgroups_per_cu: int = 0):
-        self.lib = load()
+    def __init__(self, device: int = 0, lanes_per_packet: int = 0, workgroups_per_cu: int = 0, diag: bool = False):
+        self.lib = load(diag=diag)
+        self.diag = diag
         h = ctypes.c_void_p()
         _check("enet_hip_context_create", self.lib.enet_hip_context_create(int(device), ctypes.byref(h)))
         self.handle = h
@@ -207,7 +217,8 @@ class Context:
         _check("enet_hip_set_tuning", self.lib.enet_hip_set_tuning(self.handle, lanes_per_packet, workgroups_per_cu))
 
     def set_kernel_path(self, path: int) -> None:
-        """0 = LDS-staged (default), 1 = direct loads."""
+        """0 = default; 1 = direct loads, 2 = LDS stream kernel, 13 = lean kernel, 17 = vring
+        kernel; the other paths (tuning sweeps) exist in the diagnostics library only."""
         _check("enet_hip_set_kernel_path", self.lib.enet_hip_set_kernel_path(self.handle, int(path)))
 
     def diag_ablation(self, mode: int) -> None:

@@ -72,19 +72,26 @@ ENET_HIP_API const char* enet_hip_error_string(int code);
 
 /* Tuning knobs (0 = automatic).  lanes_per_packet: 1,2,4,...,64 lanes share one
  * packet (a power of two; default 8, and 4 for the length-binned entries);
- * workgroups_per_cu: resident workgroups per CU the direct / gather grids are
- * sized for. */
+ * workgroups_per_cu: resident workgroups per CU (the VGPR-ring kernel runs 1 or
+ * 2, default 2; the direct / gather grids are sized for it). */
 ENET_HIP_API int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgroups_per_cu);
 
 /* Kernel path for the packet batch entry points (0 = default): checksum batches
  * at 4 or 8 lanes per packet run the VGPR-ring kernel (crc32_vring.hip), receive
  * verify and the length-binned entries the lean LDS-DMA kernel (crc32_lean.hip),
  * 16 lanes the LDS-ring stream kernel, other lane counts the direct kernel.
- * Tuning sweeps: 1 = direct loads only, 2 + k = stream kernel geometry k (k < 11),
- * 13 + g = lean kernel geometry g (g < 4), 17 = the vring kernel, 18 = the same
- * with the other stage-load cache policy, 19 / 20 = the vring kernel with each
- * workgroup walking a contiguous range of groups (plain / nontemporal loads). */
+ * Every path gives the same (correct) checksums.  Built in every library: 1 =
+ * direct loads only, 2 = the stream kernel, 13 = the lean kernel, 17 = the vring
+ * kernel (for the length-binned entries: its records instance).  Tuning sweeps,
+ * libenethip_diag.so only (-1 elsewhere): 2 + k = stream kernel geometry k
+ * (k < 11), 13 + g = lean kernel geometry g (g < 4), 18 = vring with nontemporal
+ * stage loads, 19 / 20 = vring with each workgroup walking a contiguous range of
+ * groups (plain / nontemporal loads), 21 = vring with its stages in window order
+ * (the schedule before the tail-first order). */
 ENET_HIP_API int enet_hip_set_kernel_path(enet_hip_context* ctx, int path);
+
+/* 1 in libenethip_diag.so (built with -DENET_HIP_DIAG), 0 in libenethip.so. */
+ENET_HIP_API int enet_hip_is_diagnostics_build(void);
 
 /* ---- batched checksum, device-resident ----
  * Packet i is bytes[offsets[i] .. offsets[i]+lengths[i]).  All pointers are
@@ -270,6 +277,9 @@ ENET_HIP_API int enet_hip_crc32_batch_multi(enet_hip_context* const* contexts, i
 ENET_HIP_API int enet_hip_read_probe_device(enet_hip_context* ctx, const uint8_t* bytes, size_t byteCount,
                                             uint32_t* sink, void* stream);
 
+#ifdef ENET_HIP_DIAG
+/* ==== diagnostics: exported by libenethip_diag.so only ==== */
+
 /* ---- diagnostics: roofline ablation of the stream kernel ----
  * 0 = normal; 1 = skip the table lookups (memory path alone); 2 = skip the
  * LDS-DMA (compute path alone).  Modes 1 and 2 produce WRONG checksums by
@@ -292,6 +302,7 @@ ENET_HIP_API int enet_hip_diag_ablation(enet_hip_context* ctx, int mode);
  * landed, end, HW_ID | XCC_ID << 32, groups.  NULL turns it off.  Checksums are
  * unaffected. */
 ENET_HIP_API int enet_hip_diag_trace(enet_hip_context* ctx, uint64_t* deviceBuffer);
+#endif /* ENET_HIP_DIAG */
 
 /* ---- small memory helpers (so C#/ctypes hosts need no HIP binding) ---- */
 ENET_HIP_API int enet_hip_device_alloc(enet_hip_context* ctx, size_t bytes, void** out);

@@ -26,6 +26,7 @@
  */
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 /* include/win32.cs:25-29 -- Win32 WSABUF order: length first, then pointer. */
@@ -133,14 +134,22 @@ void oracle_crc32_gather(const uint8_t* bytes, const uint64_t* seg_off, const ui
 /* Batched receive verify (protocol.cs:1052-1068): desired = slot; slot = connectID
  * (or 0 when there is no peer); crc over the whole DGRAM; drop on mismatch.  The
  * slot sits at slot_off[i] bytes into DGRAM i.  `bytes` is NOT modified: the
- * substitution is applied on a private copy.  ok[i] = 1 keep / 0 drop. */
+ * substitution is applied on a private copy (heap, as long as the longest DGRAM:
+ * no length limit beyond the reference's).  A slot that does not lie wholly inside
+ * the DGRAM (slot_off + 4 > L) is dropped (ok = 0, computed = 0): the reference
+ * reads those bytes from past receivedDataLength in its 4096-byte receive buffer
+ * (protocol.cs:1001-1014 check only L >= 2), which a batch API has no content for. */
 void oracle_verify_batch(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
                          const uint32_t* slot_off, const uint32_t* connect_id, size_t n,
                          uint8_t* ok, uint32_t* computed) {
-    static __thread uint8_t tmp[65536 + 8];
+    uint32_t maxL = 8;
+    for (size_t i = 0; i < n; ++i)
+        if (len[i] > maxL) maxL = len[i];
+    uint8_t* tmp = (uint8_t*)malloc(maxL);
+    if (!tmp) abort();
     for (size_t i = 0; i < n; ++i) {
         uint32_t L = len[i];
-        if (L > 65536 || slot_off[i] + 4u > L) { ok[i] = 0; if (computed) computed[i] = 0; continue; }
+        if ((uint64_t)slot_off[i] + 4u > L) { ok[i] = 0; if (computed) computed[i] = 0; continue; }
         memcpy(tmp, bytes + off[i], L);
         uint32_t desired;
         memcpy(&desired, tmp + slot_off[i], 4);
@@ -151,6 +160,7 @@ void oracle_verify_batch(const uint8_t* bytes, const uint64_t* off, const uint32
         if (computed) computed[i] = c;
         ok[i] = (c == desired) ? 1 : 0;
     }
+    free(tmp);
 }
 
 /* Batched fragment reassembly, sequential, as c/protocol.cs:529-637

@@ -576,19 +576,43 @@ def vring_window(addr: int, L: int):
     return addr - lz, lz, e, nb
 
 
-def vring_packet(arena: bytes, addr: int, L: int, P: int, lane_base: int = 0) -> int:
+def vring_stage_order(S: int, rotate: bool):
+    """crc32_vring.hip's stage order of a group of S stages: in order, or (rotate,
+    the tail-first schedule) the last stage first, then 0 .. S-2."""
+    if not rotate or S <= 1:
+        return list(range(S))
+    return [S - 1] + list(range(S - 1))
+
+
+def vring_adv(img, reg: int) -> int:
+    """reg * x^(256 P): the fold of a block holding reg in its first 4 bytes and
+    zeros elsewhere, four lookups in the advancing tables T'_31 .. T'_28."""
+    acc = 0
+    for m in range(4):
+        acc ^= img[(((reg >> (8 * m)) & 0xFF) * 256 + col_byte(31 - m)) // 4]
+    return acc
+
+
+def vring_packet(arena: bytes, addr: int, L: int, P: int, lane_base: int = 0, rotate: bool = False,
+                 group_stages: int = 0) -> int:
     """What crc32_vring_kernel's P lanes (lanes lane_base .. lane_base+P-1) compute
-    for the packet arena[addr:addr+L]; returns the wire CRC."""
+    for the packet arena[addr:addr+L]; returns the wire CRC.  rotate: the
+    tail-first stage order (the group's last stage first, folded from a zero
+    register into rt; rt ^ adv(reg) joins it at the end); group_stages: the
+    group's stage count (>= this packet's own)."""
     img = vring_image(P)
     ws, lz, e, nb = vring_window(addr, L)
-    stages = (nb + P - 1) // P
+    stages = max((nb + P - 1) // P, group_stages)
+    order = vring_stage_order(stages, rotate)
     total = 0
     for k in range(P):
         lane = lane_base + k
         col, sel, sw1, sw2, hs = make_sched(lane)
         reg = (img[init_addr(lz) // 4] if nb else 0xFFFFFFFF) if k == 0 else 0
+        rt = 0
         cnt = (nb - 1 - k) // P + 1 if nb > k else 0
-        for st in range(stages):
+        for step, st in enumerate(order):
+            tail_first = rotate and stages > 1 and step == 0
             q0 = 32 * (k + P * st)
             pieces = []
             for po in ((q0 + 16, q0) if hs else (q0, q0 + 16)):   # lane order A, B
@@ -604,11 +628,16 @@ def vring_packet(arena: bytes, addr: int, L: int, P: int, lane_base: int = 0) ->
             if st >= cnt:
                 continue
             w = [int.from_bytes(blk[4 * q:4 * q + 4], "little") for q in range(8)]
-            w[0] ^= reg
+            w[0] ^= 0 if tail_first else reg
             acc = 0
             for a in lookup_addresses(lane, w):
                 acc ^= img[a // 4]
-            reg = acc
+            if tail_first:
+                rt = acc
+            else:
+                reg = acc
+        if rotate and stages > 1 and stages - 1 < cnt:
+            reg = rt ^ vring_adv(img, reg)
         o = (k - nb) % P
         if o:
             reg = (img[corr_addr(o, 0, reg & 0xFF) // 4] ^ img[corr_addr(o, 1, (reg >> 8) & 0xFF) // 4] ^

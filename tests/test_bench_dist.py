@@ -45,7 +45,7 @@ class FakeEngine:
         return self.lib.batch(b.payload, b.off, b.lens, threads=2)
 
 
-def fake_cpu(batch, budget):
+def fake_cpu(batch, budget, threads=0):
     one = {"gibps": 0.5, "threads": 1, "packets": batch.n, "reps": 1}
     return {"1thread": one, "all": dict(one, gibps=2.0, threads=2)}
 
@@ -92,6 +92,18 @@ def test_two_rank_gloo_harness():
     assert d["value"] == pytest.approx(2 * per_rank / (d["ms_per_step"] * 6e-3) / 2**30, rel=0.02)
     assert d["roofline"]["bound"] == "hbm" and d["roofline"]["peak"] == 8000.0
     assert d["cpu_baseline"]["cores"] == 2 and d["cpu_baseline"]["kind"] == "port"
+    assert d["config"]["workgroups_per_cu"] == "default (2)" and d["config"]["kernel_path"] == 0
+
+
+def test_cpu_baseline_uses_the_affinity_cores():
+    """The CPU baseline runs on every core of the process's affinity mask (the box's
+    CPU share, cgroup / taskset limits included) and says how many."""
+    import bench
+    assert bench.host_cores() == len(os.sched_getaffinity(0))
+    from enethip import workloads
+    b = workloads.fixed(512, 1200, seed=1, name="t")
+    r = bench.cpu_baseline(b, 0.05)
+    assert r["all"]["threads"] == len(os.sched_getaffinity(0)) and r["1thread"]["threads"] == 1
 
 
 def test_cfg4_shards_partition_the_million_packets():

@@ -120,3 +120,18 @@ def test_fragments_overlapping_ranges(ctx, oracle_lib, words):  # noqa: F811
             assert (run_gpu(ctx, fb, sg, sel) == run_oracle(oracle_lib, fb, so, sel)).all()
         for k in ("msg_bytes", "fragments", "remaining"):
             assert (so[k] == sg[k]).all(), k
+
+
+def test_fragments_scratch_layout_changes(ctx, oracle_lib):  # noqa: F811
+    """The context's claim scratch (claim words, then per-slot winner counts and the
+    deferred flag) across calls whose (slots, bitmap words) layouts differ -- more
+    slots with the same claim-word count, fewer, then more again -- each a small
+    batch of overlapping fragments against a large claim space (the atomic decide
+    path, where winner counts defer overlapping slots)."""
+    for i, (slots, words) in enumerate(((4000, 1), (2500, 2), (5000, 1), (2500, 2), (4000, 1), (1000, 2))):
+        fb = workloads.overlapping_fragments(slots, seed=50 + i)
+        so, sg = state(fb, words), state(fb, words)
+        sel = np.arange(min(fb.n, 2000))                  # 8 n + 65536 < slots x 32 x words: atomic
+        assert (run_gpu(ctx, fb, sg, sel) == run_oracle(oracle_lib, fb, so, sel)).all(), (slots, words)
+        for k in ("msg_bytes", "fragments", "remaining"):
+            assert (so[k] == sg[k]).all(), (slots, words, k)

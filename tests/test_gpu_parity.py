@@ -25,6 +25,28 @@ def ctx():
     c.close()
 
 
+@pytest.fixture(scope="module")
+def dctx():
+    """The diagnostics library (libenethip_diag.so): the sweep-only kernel paths."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.init()
+    c = enethip.Context(0, diag=True)
+    yield c
+    c.close()
+
+
+PRODUCT_PATHS = (0, 1, 2, 13, 17)   # built in libenethip.so; every other path: libenethip_diag.so only
+
+
+def on(ctx, dctx, path):
+    """The context whose library builds kernel path `path`."""
+    return ctx if path in PRODUCT_PATHS else dctx
+
+
+WGS = (0, 1, 2)    # workgroups per CU of the vring kernel: the default (2), one, two
+
+
 def dev(a: np.ndarray):
     a = np.ascontiguousarray(a)
     view = {np.dtype(np.uint64): np.int64, np.dtype(np.uint32): np.int32, np.dtype(np.uint8): np.uint8}[a.dtype]
@@ -230,7 +252,7 @@ LEAN_PATHS = (13, 14)        # crc32_lean.hip geometries (path 0 runs the first 
 
 
 @pytest.mark.parametrize("geom", range(N_STREAM_GEOMS))
-def test_stream_geometries(ctx, golden, oracle_lib, geom):
+def test_stream_geometries(ctx, dctx, golden, oracle_lib, geom):
     """Every stream-kernel geometry (path 2 + k) x 4/8/16 lanes: golden vectors,
     unaligned mixed sizes (empty packets included) and many groups per wave."""
     payload, off, lens, exp = golden_batch(golden)
@@ -238,6 +260,7 @@ def test_stream_geometries(ctx, golden, oracle_lib, geom):
     exp_b = oracle_lib.batch(b.payload, b.off, b.lens, threads=16)
     small = workloads.mixed(200000, 1, 100, seed=7, len_seed=8)
     exp_s = oracle_lib.batch(small.payload, small.off, small.lens, threads=16)
+    ctx = on(ctx, dctx, 2 + geom)
     try:
         ctx.set_kernel_path(2 + geom)
         for lanes in (4, 8, 16):
@@ -253,7 +276,7 @@ def _verify_expect(oracle_lib, payload, off, lens, slot, conn):
 
 
 @pytest.mark.parametrize("path", LEAN_PATHS)
-def test_lean_many_chunks(ctx, oracle_lib, path):
+def test_lean_many_chunks(ctx, dctx, oracle_lib, path):
     """Many metadata chunks per wave (tiny packets: one-stage groups, so the
     producer runs into chunks the consumer has not prefetched yet) and long
     packets (many stages per group), crc and verify, 4 and 8 lanes."""
@@ -264,6 +287,7 @@ def test_lean_many_chunks(ctx, oracle_lib, path):
     rng = np.random.default_rng(81)
     vp, vo, vl, vs, vc = _verify_inputs(rng, 300_000)
     exp_ok, exp_comp = oracle_lib.verify(vp, vo, vl, vs, vc)
+    ctx = on(ctx, dctx, path)
     try:
         ctx.set_kernel_path(path)
         for lanes in (4, 8):
@@ -521,23 +545,38 @@ def test_bad_tuning_raises(ctx):
         ctx.set_tuning(3, 0)
 
 
-def test_vring_many_groups(ctx, oracle_lib):
-    """The default VGPR-ring kernel (4 and 8 lanes): tiny packets (one-stage groups,
-    the producer switching group every stage, empty packets among them) and long
-    ones (many stages per group), each against the oracle."""
+@pytest.mark.parametrize("wgs", WGS)
+@pytest.mark.parametrize("path", (0, 17, 18, 19, 20, 21))
+def test_vring_many_groups(ctx, dctx, oracle_lib, path, wgs):
+    """The default VGPR-ring kernel (4 and 8 lanes, one or two workgroups per CU):
+    tiny packets (one-stage groups, the producer switching group every stage, empty
+    packets among them), long ones (many stages per group, the tail-first order's
+    last stage far from the rest) and cfg2-shaped packed MTU packets, each against
+    the oracle.  18: nontemporal stage loads; 19, 20: walks; 21: stages in order."""
     tiny = workloads.mixed(1_200_000, 0, 40, seed=177, len_seed=178)
     exp_t = oracle_lib.batch(tiny.payload, tiny.off, tiny.lens, threads=16)
     big = workloads.mixed(40_000, 2000, 9000, seed=179, len_seed=180)
     exp_b = oracle_lib.batch(big.payload, big.off, big.lens, threads=16)
+    mtu = workloads.mixed(100_000, 1200, 1200, seed=181, len_seed=182)
+    exp_m = oracle_lib.batch(mtu.payload, mtu.off, mtu.lens, threads=16)
+    ctx = on(ctx, dctx, path)
     try:
-        for path in (0, 17, 18, 19, 20):       # 18: the other stage-load cache policy; 19, 20: walks
-            ctx.set_kernel_path(path)
-            for lanes in (4, 8):
-                assert (run_batch(ctx, tiny.payload, tiny.off, tiny.lens, lanes) == exp_t).all(), ("tiny", path, lanes)
-                assert (run_batch(ctx, big.payload, big.off, big.lens, lanes) == exp_b).all(), ("big", path, lanes)
+        ctx.set_kernel_path(path)
+        for lanes in (4, 8):
+            assert (run_batch(ctx, tiny.payload, tiny.off, tiny.lens, lanes, wgs) == exp_t).all(), ("tiny", lanes)
+            assert (run_batch(ctx, big.payload, big.off, big.lens, lanes, wgs) == exp_b).all(), ("big", lanes)
+            assert (run_batch(ctx, mtu.payload, mtu.off, mtu.lens, lanes, wgs) == exp_m).all(), ("mtu", lanes)
     finally:
         ctx.set_kernel_path(0)
         ctx.set_tuning(0, 0)
+
+
+def test_product_library_rejects_sweep_paths(ctx):
+    """libenethip.so builds no sweep path (they exist in libenethip_diag.so only)."""
+    for path in (3, 8, 14, 18, 19, 20, 21, 22):
+        with pytest.raises(enethip.ENetHipError):
+            ctx.set_kernel_path(path)
+    ctx.set_kernel_path(0)
 
 
 def _batch_list_cases(oracle_lib):
@@ -571,20 +610,23 @@ def _run_list(ctx, cases):
     return [o.cpu().numpy().view(np.uint32)[:len(c[1])] for o, c in zip(outs, cases)]
 
 
-LIST_PATHS = (0, 13, 19, 20)  # 0: the vring kernel (default), 13: the lean kernel's list instance,
-                              # 19 / 20: the vring kernel with workgroups walking contiguous ranges
+LIST_PATHS = (0, 13, 19, 20, 21)  # 0: the vring kernel (default), 13: the lean kernel's list instance,
+                                  # 19 / 20: vring with workgroups walking contiguous ranges, 21: in order
 
 
+@pytest.mark.parametrize("wgs", WGS)
 @pytest.mark.parametrize("path", LIST_PATHS)
-def test_batch_list(ctx, oracle_lib, path):
+def test_batch_list(ctx, dctx, oracle_lib, path, wgs):
     """enet_hip_crc32_batch_list_device: batches of every shape in one launch,
     each against the oracle; vring (path 0) or lean (13) lists at the default, 4 and
-    8 lanes; 16 lanes (one launch per batch on the stream kernel)."""
+    8 lanes, one or two workgroups per CU; 16 lanes (one launch per batch on the
+    stream kernel)."""
     cases = _batch_list_cases(oracle_lib)
+    ctx = on(ctx, dctx, path)
     try:
         ctx.set_kernel_path(path)
         for lanes in (0, 4, 8, 16):
-            ctx.set_tuning(lanes, 0)
+            ctx.set_tuning(lanes, wgs)
             for i, (got, c) in enumerate(zip(_run_list(ctx, cases), cases)):
                 assert (got == c[3]).all(), (path, lanes, i, np.nonzero(got != c[3])[0][:5])
     finally:
@@ -592,8 +634,9 @@ def test_batch_list(ctx, oracle_lib, path):
         ctx.set_tuning(0, 0)
 
 
+@pytest.mark.parametrize("wgs", WGS)
 @pytest.mark.parametrize("path", LIST_PATHS)
-def test_batch_list_many_launches(ctx, oracle_lib, path):
+def test_batch_list_many_launches(ctx, dctx, oracle_lib, path, wgs):
     """More batches than one launch takes (48): 110 small batches of varied sizes,
     plus the reverse order (the grid is sized by the largest batch)."""
     rng = np.random.default_rng(55)
@@ -606,18 +649,22 @@ def test_batch_list_many_launches(ctx, oracle_lib, path):
                           np.zeros(0, np.uint32)))
         else:
             cases.append((b.payload, b.off, b.lens, oracle_lib.batch(b.payload, b.off, b.lens, threads=16)))
+    ctx = on(ctx, dctx, path)
     try:
         ctx.set_kernel_path(path)
+        ctx.set_tuning(0, wgs)
         for order in (cases, cases[::-1]):
             for i, (got, c) in enumerate(zip(_run_list(ctx, order), order)):
                 assert (got == c[3]).all(), (path, i, len(c[1]))
     finally:
         ctx.set_kernel_path(0)
+        ctx.set_tuning(0, 0)
 
 
-def test_vring_trace_instance(ctx, oracle_lib):
+def test_vring_trace_instance(dctx, oracle_lib):
     """The diagnostics (trace) instance of the vring kernel computes the same CRCs
     and fills one 8 x u64 record per wave."""
+    ctx = dctx
     b = workloads.mixed(100_000, 0, 3000, seed=91, len_seed=92)
     exp = oracle_lib.batch(b.payload, b.off, b.lens, threads=16)
     tr = torch.zeros(256 * 16 * 8, dtype=torch.int64, device="cuda")
@@ -635,7 +682,8 @@ def test_vring_trace_instance(ctx, oracle_lib):
         ctx.set_tuning(0, 0)
 
 
-def test_all_empty_groups_every_path(ctx, oracle_lib):
+@pytest.mark.parametrize("wgs", WGS)
+def test_all_empty_groups_every_path(ctx, dctx, oracle_lib, wgs):
     """Groups whose packets are all empty (a stage count of zero before the
     clamp): a lone empty packet, a batch of empty packets, and runs of empty
     packets amid others -- every lane count, the default and direct paths, and
@@ -652,13 +700,59 @@ def test_all_empty_groups_every_path(ctx, oracle_lib):
     cases = [(np.zeros(16, np.uint8), np.zeros(1, np.uint64), np.zeros(1, np.uint32), np.zeros(1, np.uint32)),
              (np.zeros(16, np.uint8), np.zeros(64, np.uint64), np.zeros(64, np.uint32), np.zeros(64, np.uint32)),
              (payload, off, lens, exp)]
-    try:
-        for path in [0, 1] + [2 + g for g in range(N_STREAM_GEOMS)] + [17, 18]:
-            ctx.set_kernel_path(path)
+    paths = [0, 1, 17] if wgs else [0, 1] + [2 + g for g in range(N_STREAM_GEOMS)] + [17, 18, 21]
+    for path in paths:
+        c = on(ctx, dctx, path)
+        try:
+            c.set_kernel_path(path)
             for lanes in (1, 2, 4, 8, 16, 32, 64):
                 for i, (p, o, l, e) in enumerate(cases):
-                    got = run_batch(ctx, p, o, l, lanes)
+                    got = run_batch(c, p, o, l, lanes, wgs)
                     assert (got == e).all(), (path, lanes, i, np.nonzero(got != e)[0][:5])
-    finally:
-        ctx.set_kernel_path(0)
-        ctx.set_tuning(0, 0)
+        finally:
+            c.set_kernel_path(0)
+            c.set_tuning(0, 0)
+
+
+def test_verify_dgrams_over_64k(ctx, oracle_lib):
+    """Receive verify has no length limit of its own (protocol.cs:1052-1068 CRCs
+    receivedDataLength bytes): DGRAMs of 64 KiB - 1 .. 200 000 B, stamped and
+    corrupted, through the single-batch, list and binned entries, against the
+    oracle's verify (which holds no 64 KiB limit either)."""
+    rng = np.random.default_rng(65)
+    lens = np.array([65535, 65536, 65537, 70000, 131072, 200000, 100, 65540], np.uint32)
+    n = len(lens)
+    slot = np.array([4, 2, 4, 4, 2, 4, 4, 2], np.uint32)
+    conn = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    off = np.zeros(n, np.uint64)
+    np.cumsum(lens[:-1].astype(np.uint64) + np.uint64(3), out=off[1:])
+    payload = rng.integers(0, 256, size=int(off[-1] + lens[-1]) + 16, dtype=np.uint8)
+    for i in range(n):
+        o, s = int(off[i]), int(slot[i])
+        payload[o + s:o + s + 4] = np.frombuffer(np.uint32(conn[i]).tobytes(), np.uint8)
+    stamped = oracle_lib.batch(payload, off, lens, threads=8)
+    for i in range(n):
+        o, s = int(off[i]), int(slot[i])
+        payload[o + s:o + s + 4] = np.frombuffer(np.uint32(stamped[i]).tobytes(), np.uint8)
+    payload[int(off[3]) + 66000] ^= np.uint8(4)              # corrupt one long DGRAM
+    exp_ok, exp_comp = oracle_lib.verify(payload, off, lens, slot, conn)
+    assert exp_ok.tolist() == [1, 1, 1, 0, 1, 1, 1, 1]
+    for lanes in (0, 4, 8):
+        ctx.set_tuning(lanes, 0)
+        d_ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        d_comp = torch.zeros(n, dtype=torch.int32, device="cuda")
+        ctx.verify_batch_device(dev(payload), dev(off), dev(lens), dev(slot), dev(conn), n, d_ok, d_comp,
+                                stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert (d_ok.cpu().numpy() == exp_ok).all(), lanes
+        assert (d_comp.cpu().numpy().view(np.uint32) == exp_comp).all(), lanes
+        (ok_l, comp_l), = _run_verify_list(ctx, [(payload, off, lens, slot, conn, exp_ok, exp_comp)])
+        assert (ok_l == exp_ok).all() and (comp_l == exp_comp).all(), ("list", lanes)
+        wsb = ctx.verify_binned_workspace_size(n)
+        ws = torch.zeros(wsb, dtype=torch.uint8, device="cuda")
+        d_ok.zero_()
+        ctx.verify_batch_device_binned(dev(payload), dev(off), dev(lens), dev(slot), dev(conn), n, d_ok, ws, wsb,
+                                       d_comp, stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert (d_ok.cpu().numpy() == exp_ok).all(), ("binned", lanes)
+    ctx.set_tuning(0, 0)

@@ -7,8 +7,11 @@ checked here on the gfx950 ISA hipcc emits with the Makefile's flags:
     would need vmcnt(0);
   * no instruction reads or overwrites a register while a load into it may be in
     flight, on any path of the control-flow graph (tools/isa_inflight_check.py);
+  * no compiler instruction writes a ring register (v48-v63: the allocator limit
+    amdgpu_num_vgpr(24) is what keeps it out of them);
   * at most 64 VGPRs: a launch runs one 16-wave workgroup per CU, and the next
     launch's workgroup (another stream) can share the CU as this one drains.
+Both builds are checked: the product library and the diagnostics one (-DENET_HIP_DIAG).
 """
 import os
 import re
@@ -23,14 +26,16 @@ PKG = os.path.join(ROOT, "enet-csharp_amd")
 HIPCC = "/opt/rocm/bin/hipcc"
 
 
-@pytest.fixture(scope="module")
-def vring_isa(tmp_path_factory):
+@pytest.fixture(scope="module", params=["product", "diag"])
+def vring_isa(tmp_path_factory, request):
     if not os.path.exists(HIPCC):
         pytest.skip("hipcc not available")
-    out = tmp_path_factory.mktemp("isa") / "vring.s"
+    out = tmp_path_factory.mktemp("isa") / f"vring_{request.param}.s"
     cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-mllvm", "-simplifycfg-sink-common=false",
            "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(PKG, "csrc"), "--cuda-device-only", "-S",
            os.path.join(PKG, "csrc", "crc32_vring.hip"), "-o", str(out)]
+    if request.param == "diag":
+        cmd.insert(1, "-DENET_HIP_DIAG")
     subprocess.run(cmd, check=True, capture_output=True)
     return str(out)
 
@@ -58,3 +63,15 @@ def test_vring_loads_not_touched_before_wait(vring_isa):
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import isa_inflight_check as chk
     assert chk.main(vring_isa) == 0
+
+
+def test_ring_write_check_catches_a_compiler_write():
+    """The checker flags a compiler instruction that writes a ring register (it
+    would corrupt a landed slot before its fold), and passes the asm loads."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import isa_inflight_check as chk
+    body = [";;#ASMSTART", "global_load_dwordx4 v[48:51], v[0:1], off", ";;#ASMEND",
+            "s_waitcnt vmcnt(0)", "v_xor_b32_e32 v1, v48, v2", "s_endpgm"]
+    assert chk.check(body, "k") == []
+    bad = body[:-1] + ["v_mov_b32_e32 v52, 0", "s_endpgm"]
+    assert any("writes ring" in e for e in chk.check(bad, "k"))

@@ -249,6 +249,27 @@ def test_vring_model_matches_oracle(P):
         assert got == exp, (a, L, P, hex(got), hex(exp))
 
 
+@pytest.mark.parametrize("P", [4, 8])
+def test_vring_tail_first_model_matches_oracle(P):
+    """The vring kernel's tail-first stage order (the group's last stage folded
+    first, from a zero register into rt; the others in order; then rt ^ adv(reg),
+    adv = four lookups in T'_31 .. T'_28): equal to packet.cs:142-160 for every
+    start alignment, lengths across stage boundaries, empty packets, and packets
+    shorter than their group (whose own last stage is not the group's)."""
+    rng = random.Random(0x5254 + P)
+    arena = bytes(rng.getrandbits(8) for _ in range(16384))
+    ol = oracle.OracleLib()
+    cases = [(a, L, 0) for a in range(0, 64, 7) for L in (0, 1, 17, 32, 33, 255, 256, 257, 511, 1200, 1400)]
+    cases += [(rng.randrange(0, 2048), rng.randrange(0, 3000), rng.randrange(0, 14)) for _ in range(40)]
+    cases += [(1200 * i, 1200, 0) for i in range(8)]        # cfg2 shapes
+    assert km.vring_stage_order(5, True) == [4, 0, 1, 2, 3] and km.vring_stage_order(1, True) == [0]
+    for a, L, gs in cases:
+        lane_base = P * rng.randrange(0, 64 // P)
+        got = km.vring_packet(arena, 128 + a, L, P, lane_base, rotate=True, group_stages=gs)
+        exp = ol.crc32(arena[128 + a:128 + a + L])
+        assert got == exp, (a, L, P, gs, hex(got), hex(exp))
+
+
 @pytest.mark.parametrize("batch_groups,grid", [([4096] * 5, 512), ([1], 1), ([0, 3, 0, 17], 2),
                                                ([5000, 1, 70, 2, 800], 300), ([33] * 48, 7)])
 def test_vring_dynamic_slots_cover_every_group_once(batch_groups, grid):

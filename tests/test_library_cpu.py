@@ -4,6 +4,7 @@ No GPU compute is attempted here."""
 import ctypes
 import os
 import re
+import subprocess
 import zlib
 
 import numpy as np
@@ -14,13 +15,26 @@ import oracle
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _header_symbols():
+SYM = r"ENET_HIP_API\s+[\w\s\*]+?\b(enet_hip_\w+)\s*\("
+
+
+def _header_symbols(diag_section: bool = False):
+    """Declarations outside (or, diag_section, inside) the #ifdef ENET_HIP_DIAG block."""
     text = open(os.path.join(ROOT, "include", "enet_hip.h")).read()
-    return sorted(set(re.findall(r"ENET_HIP_API\s+[\w\s\*]+?\b(enet_hip_\w+)\s*\(", text)))
+    m = re.search(r"#ifdef ENET_HIP_DIAG(.*?)#endif /\* ENET_HIP_DIAG \*/", text, re.S)
+    assert m, "the header's diagnostics section"
+    part = m.group(1) if diag_section else text[:m.start()] + text[m.end():]
+    return sorted(set(re.findall(SYM, part)))
 
 
 def test_header_lists_match_binding():
     assert _header_symbols() == sorted(enethip.EXPORTED_SYMBOLS)
+    assert _header_symbols(True) == sorted(enethip.DIAG_SYMBOLS)
+
+
+def _exported(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", path], check=True, capture_output=True, text=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.split()[-1].startswith("enet_hip_")}
 
 
 def test_library_loads_and_exports_everything():
@@ -28,6 +42,17 @@ def test_library_loads_and_exports_everything():
     for name in _header_symbols():
         assert hasattr(lib, name), name
         assert ctypes.cast(getattr(lib, name), ctypes.c_void_p).value
+    assert lib.enet_hip_is_diagnostics_build() == 0
+
+
+def test_product_library_has_no_diagnostics():
+    """The library a C# host loads cannot emit a wrong CRC: the ablation switch
+    (wrong checksums by design) and the trace exist only in libenethip_diag.so,
+    and the exports are exactly the header's product section."""
+    assert _exported(enethip.LIB_PATH) == set(_header_symbols())
+    diag = enethip.load(diag=True)
+    assert diag.enet_hip_is_diagnostics_build() == 1
+    assert _exported(enethip.DIAG_LIB_PATH) == set(_header_symbols()) | set(_header_symbols(True))
 
 
 def test_callback_path_golden(golden):

@@ -101,3 +101,22 @@ def test_c_verify(golden, oracle_lib):
 def test_python_vs_zlib_lengths(n):
     data = bytes((i * 131 + 7) & 0xFF for i in range(n))
     assert oracle.enet_crc32_py([data]) == oracle.host_to_net_32(zlib.crc32(data))
+
+
+def test_oracle_verify_has_no_length_limit(oracle_lib):
+    """oracle_verify_batch follows protocol.cs:1052-1068 for any DGRAM length (no
+    64 KiB cap): a 200 000-byte DGRAM stamped with its CRC verifies, one flipped
+    bit drops it; a slot that does not fit the DGRAM drops (documented rule)."""
+    rng = np.random.default_rng(3)
+    L = 200_000
+    buf = rng.integers(0, 256, size=L, dtype=np.uint8)
+    conn = 0x1234ABCD
+    buf[4:8] = np.frombuffer(np.uint32(conn).tobytes(), np.uint8)
+    crc = oracle.host_to_net_32(zlib.crc32(buf.tobytes()))
+    buf[4:8] = np.frombuffer(np.uint32(crc).tobytes(), np.uint8)
+    off = np.array([0, 0, 0], np.uint64)
+    lens = np.array([L, L, 6], np.uint32)
+    slot = np.array([4, 4, 4], np.uint32)
+    cid = np.array([conn, conn ^ 1, conn], np.uint32)
+    ok, comp = oracle_lib.verify(buf, off, lens, slot, cid)
+    assert ok.tolist() == [1, 0, 0] and int(comp[0]) == crc and int(comp[2]) == 0

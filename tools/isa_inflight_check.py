@@ -35,6 +35,27 @@ def regs(text):
     return frozenset(out)
 
 
+RING = frozenset(range(48, 64))
+
+
+def writes(line, op):
+    """VGPRs an instruction writes: the first operand of a VALU op, a load or an LDS
+    read / returning atomic (stores, DS writes and scalar ops write no VGPR)."""
+    rest = line[len(op):]
+    if not rest.strip():
+        return frozenset()
+    first = rest.split(",", 1)[0]
+    if op.startswith("v_") and not op.startswith(("v_cmp_", "v_cmpx_", "v_readlane", "v_readfirstlane")):
+        return regs(first)
+    if op.startswith(("global_load", "buffer_load", "scratch_load", "flat_load")) and "lds" not in op:
+        return regs(first)
+    if op.startswith("ds_") and ("read" in op or "_rtn" in op or "bpermute" in op or "permute" in op):
+        return regs(first)
+    if "atomic" in op and " glc" in line + " ":
+        return regs(first)
+    return frozenset()
+
+
 def parse(lines):
     """-> list of instructions (kind, text, regs, target, lineno) and label -> index."""
     insts, labels = [], {}
@@ -128,6 +149,16 @@ def check(lines, name):
                 state_in[j] = m
                 work.append(j)
     errors = []
+    # the ring registers v48-v63 are written only by the asm stage loads: a compiler
+    # instruction writing one (a temporary the allocator placed there) would corrupt
+    # a slot between its wait and its fold, and the in-flight pass cannot see that
+    for i, inst in enumerate(insts):
+        kind, line, op, _, no = inst
+        if kind == "aload":
+            continue
+        hit = writes(line, op) & RING
+        if hit:
+            errors.append(f"{name}:{no + 1}: '{line}' writes ring register(s) v{sorted(hit)}")
     for i, inst in enumerate(insts):
         kind, line, op, _, no = inst
         st = state_in[i]

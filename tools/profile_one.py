@@ -29,11 +29,13 @@ def main():
     ap.add_argument("--wgs", type=int, default=0)
     a = ap.parse_args()
     batches = bench.make_batches(a.config, a.rotate, 0)
-    eng = bench.GpuEngine(0, batches, a.lanes, a.wgs)
+    diag = a.ablate != 0 or a.path not in bench.PRODUCT_PATHS   # sweep paths: libenethip_diag.so
+    eng = bench.GpuEngine(0, batches, a.lanes, a.wgs, diag=diag)
     if a.list:
         eng.set_list(a.list)
     eng.ctx.set_kernel_path(a.path)
-    eng.ctx.diag_ablation(a.ablate)
+    if diag:
+        eng.ctx.diag_ablation(a.ablate)
     for first, count in eng.launch_plan(a.reps):          # --reps batches, --list per launch
         eng.launch(first, count)
     if a.probe:
