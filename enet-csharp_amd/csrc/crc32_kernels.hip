@@ -32,6 +32,7 @@
 #include "crc32_lean.hpp"
 #include "crc32_vring.hpp"
 #include "crc32_stream_common.hpp"
+#include "context.hpp"
 #include "enet_hip.h"
 #include "fragment_kernels.hpp"
 #include "range_coder.hpp"
@@ -889,48 +890,7 @@ __global__ void __launch_bounds__(kThreads) read_probe_kernel(const uint8_t* byt
 
 using namespace enethip;
 
-struct enet_hip_context {
-    int device = 0;
-    int num_cus = 256;
-    hipStream_t stream = nullptr;
-    uint32_t* d_image = nullptr;
-    uint32_t* d_xn = nullptr;    // lo[65536] | hi[65536]
-    uint32_t* d_init = nullptr;  // 32
-    uint8_t* d_zero = nullptr;   // 256 zero bytes
-    uint32_t* d_basis = nullptr; // lean-kernel table basis, kBasisDwords per image
-    uint32_t* d_basis2 = nullptr; // vring-kernel table basis, kVrBasisDwords per image
-    int lanes_per_packet = 0;    // 0 = auto
-    int wgs_per_cu = 0;          // 0 = auto (direct / gather kernels)
-    int path = 0;                // 0 = stream (default geometry), 1 = direct, 2+k = stream geometry k
-    uint64_t* trace = nullptr;   // diagnostics: lean-kernel per-wave timeline
-    int ablation_prio = 0;       // tuning: lean-kernel lagging-wave priority (diag_ablation mode 8)
-    int ablation = 0;            // diagnostics: 1 = no lookups, 2 = no DMA (wrong CRCs by design)
-    int vr_abl = 0;              // diagnostics, vring batch lists: 1 = no edge masks, 2 = no lookups
-    // staging for the host-memory entry points
-    std::mutex mu;
-    uint8_t* d_bytes = nullptr;
-    size_t d_bytes_cap = 0;
-    uint8_t* d_meta = nullptr;  // off | len | out
-    size_t d_meta_cap = 0;
-    // fragment reassembly claim words (all ~0 between calls)
-    uint32_t* d_claim = nullptr;
-    size_t d_claim_cap = 0;     // words (claim words + per-slot winner counts + deferred flag)
-    size_t d_claim_words = 0;   // claim words of the current layout (slots x bitmap bits)
-    uint8_t* d_frag_desc = nullptr;   // copy descriptors, 28 B per command
-    size_t d_frag_desc_cap = 0;
-    uint8_t* d_rc_scratch = nullptr;  // range coder models, kRangeModelBytes per thread
-    size_t d_rc_scratch_cap = 0;
-};
-
 namespace {
-
-int herr(hipError_t e) { return e == hipSuccess ? 0 : -static_cast<int>(e); }
-
-#define ENH_CHECK(expr)                 \
-    do {                                \
-        hipError_t e_ = (expr);         \
-        if (e_ != hipSuccess) return herr(e_); \
-    } while (0)
 
 // x^-1 mod p = (p(x) + 1) / x in the reflected representation (bit 31-i <-> x^i).
 constexpr uint32_t x_inverse() {
@@ -1241,7 +1201,7 @@ int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStr
     // profiles/r02d_cfg3_*; the vring records instance on path 17 / 18)
     if (mode == 0 && (pa.lg == 2 || pa.lg == 3) && ctx->ablation == 0 && vring_path(ctx) &&
         (!pa.meta4 || ctx->path != 0))
-        return vring_launch(pa.lg, ctx->num_cus * (pa.meta4 ? 1 : vring_wgs(ctx)),
+        return vring_launch(pa.lg, ctx->num_cus * vring_wgs(ctx),
                             pa.meta4 ? VrVariant{} : vring_variant(ctx, false), st, pa, tb, ctx->d_basis2);
     if (ctx->path != 1 && pa.lg >= 2 && pa.lg <= 4) {
         const bool lean_path = (ctx->path >= kLeanPath0 && ctx->path < kVringPath) || (ctx->path == 0 && ctx->ablation == 0);
@@ -1267,16 +1227,7 @@ int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStr
     return herr(hipGetLastError());
 }
 
-int ensure(uint8_t** p, size_t* cap, size_t need) {
-    if (*cap >= need) return 0;
-    if (*p) ENH_CHECK(hipFree(*p));
-    *p = nullptr;
-    *cap = 0;
-    size_t sz = std::max<size_t>(need, 1 << 20);
-    ENH_CHECK(hipMalloc(reinterpret_cast<void**>(p), sz));
-    *cap = sz;
-    return 0;
-}
+int ensure(uint8_t** p, size_t* cap, size_t need) { return ensure_device(p, cap, need); }
 
 }  // namespace
 
@@ -1293,6 +1244,7 @@ int enet_hip_device_count(int* count) {
 const char* enet_hip_error_string(int code) {
     if (code == 0) return "success";
     if (code > 0) return "unknown";
+    if (-code >= ENET_HIP_ERRNO_BASE) return strerror(-code - ENET_HIP_ERRNO_BASE);   // a failed system call
     return hipGetErrorString(static_cast<hipError_t>(-code));
 }
 
@@ -1359,8 +1311,7 @@ int enet_hip_context_destroy(enet_hip_context* ctx) {
     (void)hipFree(ctx->d_zero);
     (void)hipFree(ctx->d_basis);
     (void)hipFree(ctx->d_basis2);
-    (void)hipFree(ctx->d_bytes);
-    (void)hipFree(ctx->d_meta);
+    pipeline_release(ctx);
     (void)hipFree(ctx->d_claim);
     (void)hipFree(ctx->d_frag_desc);
     (void)hipFree(ctx->d_rc_scratch);
@@ -1735,73 +1686,6 @@ int enet_hip_range_decompress_device(enet_hip_context* ctx, const uint8_t* in, c
                                      void* stream) {
     return range_coder_call(ctx, true, in, inOffsets, inLengths, count, out, outOffsets, outLimits, outLengths,
                             stream);
-}
-
-int enet_hip_crc32_batch_host(enet_hip_context* ctx, const uint8_t* bytes, size_t byteCount,
-                              const uint64_t* offsets, const uint32_t* lengths, size_t count, uint32_t* out) {
-    if (!ctx) return -static_cast<int>(hipErrorInvalidValue);
-    if (count == 0) return 0;
-    if (!bytes || !offsets || !lengths || !out) return -static_cast<int>(hipErrorInvalidValue);
-    for (size_t i = 0; i < count; ++i)  // host-side shape check before any launch
-        if (offsets[i] > byteCount || lengths[i] > byteCount - offsets[i]) return -static_cast<int>(hipErrorInvalidValue);
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    ENH_CHECK(hipSetDevice(ctx->device));
-    int rc;
-    if ((rc = ensure(&ctx->d_bytes, &ctx->d_bytes_cap, byteCount + 16))) return rc;
-    const size_t meta = count * (8 + 4 + 4) + 64;
-    if ((rc = ensure(&ctx->d_meta, &ctx->d_meta_cap, meta))) return rc;
-    uint64_t* d_off = reinterpret_cast<uint64_t*>(ctx->d_meta);
-    uint32_t* d_len = reinterpret_cast<uint32_t*>(ctx->d_meta + count * 8);
-    uint32_t* d_out = reinterpret_cast<uint32_t*>(ctx->d_meta + count * 12);
-    hipStream_t st = ctx->stream;
-    ENH_CHECK(hipMemcpyAsync(ctx->d_bytes, bytes, byteCount, hipMemcpyHostToDevice, st));
-    ENH_CHECK(hipMemcpyAsync(d_off, offsets, count * 8, hipMemcpyHostToDevice, st));
-    ENH_CHECK(hipMemcpyAsync(d_len, lengths, count * 4, hipMemcpyHostToDevice, st));
-    PacketArgs pa{};
-    pa.bytes = ctx->d_bytes;
-    pa.off = d_off;
-    pa.len = d_len;
-    pa.n = count;
-    pa.lg = static_cast<uint32_t>(log2i(auto_lanes(ctx)));
-    pa.out = d_out;
-    if ((rc = launch_packets(ctx, 0, pa, st))) return rc;
-    ENH_CHECK(hipMemcpyAsync(out, d_out, count * 4, hipMemcpyDeviceToHost, st));
-    ENH_CHECK(hipStreamSynchronize(st));
-    return 0;
-}
-
-int enet_hip_crc32_batch_multi(enet_hip_context* const* contexts, int contextCount, const uint8_t* bytes,
-                               size_t byteCount, const uint64_t* offsets, const uint32_t* lengths, size_t count,
-                               uint32_t* out) {
-    if (!contexts || contextCount <= 0) return -static_cast<int>(hipErrorInvalidValue);
-    if (count == 0) return 0;
-    if (!bytes || !offsets || !lengths || !out) return -static_cast<int>(hipErrorInvalidValue);
-    for (int i = 0; i < contextCount; ++i)
-        if (!contexts[i]) return -static_cast<int>(hipErrorInvalidValue);
-    std::vector<int> rcs(contextCount, 0);
-    std::vector<std::thread> th;
-    for (int i = 0; i < contextCount; ++i) {
-        th.emplace_back([&, i]() {
-            const size_t lo = count * static_cast<size_t>(i) / contextCount;
-            const size_t hi = count * static_cast<size_t>(i + 1) / contextCount;
-            if (hi == lo) return;
-            // rebase this shard's offsets onto the byte span it touches
-            uint64_t bmin = UINT64_MAX, bmax = 0;
-            for (size_t p = lo; p < hi; ++p) {
-                bmin = std::min<uint64_t>(bmin, offsets[p]);
-                bmax = std::max<uint64_t>(bmax, offsets[p] + lengths[p]);
-            }
-            if (bmax > byteCount) { rcs[i] = -static_cast<int>(hipErrorInvalidValue); return; }
-            std::vector<uint64_t> off(hi - lo);
-            for (size_t p = lo; p < hi; ++p) off[p - lo] = offsets[p] - bmin;
-            rcs[i] = enet_hip_crc32_batch_host(contexts[i], bytes + bmin, bmax - bmin, off.data(), lengths + lo,
-                                               hi - lo, out + lo);
-        });
-    }
-    for (auto& t : th) t.join();
-    for (int rc : rcs)
-        if (rc) return rc;
-    return 0;
 }
 
 int enet_hip_read_probe_device(enet_hip_context* ctx, const uint8_t* bytes, size_t byteCount, uint32_t* sink,

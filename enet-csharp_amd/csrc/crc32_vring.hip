@@ -41,17 +41,22 @@ namespace enethip {
 
 constexpr int kVrW = 16;                                        // waves per workgroup
 constexpr uint32_t kVrStaging = kLdsTableBytes;                 // basis rows land after the image
-// per wave, the metadata of the next group (LDS-DMA): 3 x 256 B -- lengths, then
-// the offsets' low and high dwords, lane l's at +4l
+// per wave, the metadata of the next group: ONE LDS-DMA instruction whose 64 lanes
+// load the group's fields, field f of packet p (of the group's kPk) at +4 (f kPk + p):
+// f = 0 the length, 1 / 2 the offset's low / high dword (BIN: the record's dwords
+// {len, off_lo, off_hi, index}, f = 3 the index).  3 x 8 fields at 8 lanes per
+// packet, 3 x 16 or 4 x 16 at 4; the remaining lanes repeat field 0.  (Round 2 used
+// one instruction per field, each lane loading its own packet's copy: 3 or 4 VMEM
+// instructions and 768 / 1024 B of LDS per wave, against 1 and 256 B here.)
 constexpr uint32_t kVrMeta = kVrStaging + kVrBasisRows * 256;
-constexpr uint32_t kVrMetaWave = 3 * 256;
+constexpr uint32_t kVrMetaWave = 256;
 constexpr uint32_t kVrCtr = kVrMeta + kVrW * kVrMetaWave;       // the workgroup's slot counter (16 B)
-constexpr int kVrLds = kVrCtr + 16;                              // 79.5 KiB: two workgroups per CU
+constexpr int kVrLds = kVrCtr + 16;                              // 70.5 KiB: two workgroups per CU
 static_assert(2 * kVrLds <= 160 * 1024, "two workgroups per CU");
-// length-binned records (BIN): the 4 dwords {len, off_lo, off_hi, index} per lane
-constexpr uint32_t kVrMetaWaveBin = 4 * 256;
-constexpr uint32_t kVrCtrBin = kVrMeta + kVrW * kVrMetaWaveBin;
-constexpr int kVrLdsBin = kVrCtrBin + 16;                        // 82.5 KiB: one workgroup per CU
+// length-binned records (BIN): the same area and layout
+constexpr uint32_t kVrMetaWaveBin = kVrMetaWave;
+constexpr uint32_t kVrCtrBin = kVrCtr;
+constexpr int kVrLdsBin = kVrLds;                                // two workgroups per CU as well
 
 // Global loads as inline asm, waited for by explicit counted vmcnt.  The
 // compiler's own wait insertion loses count across the loop's group-switch
@@ -104,44 +109,25 @@ __device__ __forceinline__ void vr_read_stage(u32x4& a, u32x4& b) {
     else
         asm volatile("" : "={v[56:59]}"(a), "={v[60:63]}"(b));
 }
-// the lane's metadata, 3 dwords, into the wave's LDS area at `base` (M0-relative
-// LDS-DMA, lane l's dword at +4l); the LDS reads of the previous group's metadata
-// are complete first (lgkmcnt(0)), so the DMA cannot overtake them
-__device__ __forceinline__ void vr_issue_meta(uint64_t len_addr, uint64_t off_addr, uint32_t base) {
+// the group's metadata into the wave's LDS area at `base`: one M0-relative LDS-DMA
+// (lane l's dword at base + 4 l, from the lane's own address); the LDS reads of the
+// previous group's metadata are complete first (lgkmcnt(0)), so the DMA cannot
+// overtake them
+__device__ __forceinline__ void vr_issue_meta(uint64_t addr, uint32_t base) {
     asm volatile("s_waitcnt lgkmcnt(0)\n\t"
-                 "s_mov_b32 m0, %2\n\t"
-                 "global_load_lds_dword %0, off\n\t"
-                 "s_add_u32 m0, m0, 0x100\n\t"
-                 "global_load_lds_dword %1, off\n\t"
-                 "s_add_u32 m0, m0, 0x100\n\t"
-                 "global_load_lds_dword %3, off"             // (an instruction offset would move the LDS address too)
-                 :: "v"(len_addr), "v"(off_addr), "s"(base), "v"(off_addr + 4u) : "m0", "scc", "memory");
+                 "s_mov_b32 m0, %1\n\t"
+                 "global_load_lds_dword %0, off"
+                 :: "v"(addr), "s"(base) : "m0", "memory");
 }
-// a length-binned record {len, off_lo, off_hi, index} (crc32_kernels.hip
-// length_bin), dword f into the wave's area at base + 256 f: four LDS-DMA loads
-__device__ __forceinline__ void vr_issue_rec(uint64_t rec_addr, uint32_t base) {
-    asm volatile("s_waitcnt lgkmcnt(0)\n\t"
-                 "s_mov_b32 m0, %4\n\t"
-                 "global_load_lds_dword %0, off\n\t"
-                 "s_add_u32 m0, m0, 0x100\n\t"
-                 "global_load_lds_dword %1, off\n\t"
-                 "s_add_u32 m0, m0, 0x100\n\t"
-                 "global_load_lds_dword %2, off\n\t"
-                 "s_add_u32 m0, m0, 0x100\n\t"
-                 "global_load_lds_dword %3, off"
-                 :: "v"(rec_addr), "v"(rec_addr + 4u), "v"(rec_addr + 8u), "v"(rec_addr + 12u), "s"(base)
-                 : "m0", "scc", "memory");
-}
-// the metadata once at most N younger loads are in flight (BIN: and the record's
-// caller index, dword 3)
-template <int N, int BIN>
-__device__ __forceinline__ void vr_wait_meta(uint32_t base, uint32_t lane, uint32_t& L, uint64_t& off,
-                                             uint32_t& idx) {
+// the metadata of the lane's packet p (of kPk) once at most N younger loads are in
+// flight (BIN: and the record's caller index)
+template <int N, int BIN, uint32_t kPk>
+__device__ __forceinline__ void vr_wait_meta(uint32_t base, uint32_t p, uint32_t& L, uint64_t& off, uint32_t& idx) {
     asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
-    L = lds_load(base + 4u * lane);
-    off = static_cast<uint64_t>(lds_load(base + 256u + 4u * lane)) |
-          (static_cast<uint64_t>(lds_load(base + 512u + 4u * lane)) << 32);
-    if constexpr (BIN) idx = lds_load(base + 768u + 4u * lane);
+    L = lds_load(base + 4u * p);
+    off = static_cast<uint64_t>(lds_load(base + 4u * (kPk + p))) |
+          (static_cast<uint64_t>(lds_load(base + 4u * (2u * kPk + p))) << 32);
+    if constexpr (BIN) idx = lds_load(base + 4u * (3u * kPk + p));
 }
 // every load retired (the wave's exit: no load may land after it has ended)
 __device__ __forceinline__ void vr_drain() {
@@ -440,19 +426,26 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
     uint32_t midx = 0;                                       // BIN: the record's caller index
     auto load_meta = [&](const VrIt& it) __attribute__((always_inline)) {
         const VrBatch& B = bl.b[it.b];
-        // the lane's packet, clamped to the batch's last (always a valid address; the
+        // lane l loads field f = l / kPk of packet l % kPk (lanes past the fields: field
+        // 0), the packet clamped to the batch's last (always a valid address; the
         // prologue of a wave with no group at all loads batch 0's last packet)
         const uint64_t base = min<uint64_t>(group_base(it), B.n - 1u);
         const uint64_t left = B.n - 1u - base;               // (uniform: scalar select, no VALU)
-        const uint32_t q = min(lane_p(), left < 63u ? static_cast<uint32_t>(left) : 63u);
-        if constexpr (BIN)
-            vr_issue_rec(reinterpret_cast<uint64_t>(B.off) + 16u * (base + q), mbase);
-        else
-            vr_issue_meta(reinterpret_cast<uint64_t>(B.len + base) + 4u * q,
-                          reinterpret_cast<uint64_t>(B.off + base) + 8u * q, mbase);
+        const uint32_t l = vr_lane();                       // (recomputed: not a register held across the loop)
+        uint32_t f = l / kPk;
+        const uint32_t q = min(l & (kPk - 1u), left < 63u ? static_cast<uint32_t>(left) : 63u);
+        if constexpr (BIN) {
+            f = f < 4u ? f : 0u;
+            vr_issue_meta(reinterpret_cast<uint64_t>(B.off) + 16u * (base + q) + 4u * f, mbase);
+        } else {
+            f = f < 3u ? f : 0u;
+            const uint64_t la = reinterpret_cast<uint64_t>(B.len + base) + 4u * q;
+            const uint64_t oa = reinterpret_cast<uint64_t>(B.off + base) + 8u * q + 4u * (f - 1u);
+            vr_issue_meta(f ? oa : la, mbase);
+        }
     };
     load_meta(any ? pit : VrIt{0u, 0u});                     // (batch 0 exists: count >= 1)
-    vr_wait_meta<0, BIN>(mbase, lane, mL, moff, midx);       // basis row and metadata have landed
+    vr_wait_meta<0, BIN, kPk>(mbase, lane_p(), mL, moff, midx);   // basis row and metadata have landed
     mark(1);
 
     // ---- producer: window of the group it loads, one stage ahead of the consumer
@@ -480,9 +473,9 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
         pst = 0;
     };
     // A produce issues the stage's two pieces, preceded -- on a group's first stage,
-    // when a next group exists -- by that group's metadata (three LDS-DMA loads), a whole
+    // when a next group exists -- by that group's metadata (one LDS-DMA load), a whole
     // group ahead of its use.  The wait for the previous stage (slot WS, WS < 0:
-    // none) follows in the same branch, counting the loads just issued (2, or 5
+    // none) follows in the same branch, counting the loads just issued (2, or 3
     // with metadata): one issue-and-wait sequence per path, so the in-flight check
     // sees each path's own count.
     auto produce = [&](auto slot_c, auto ws_c) __attribute__((always_inline)) {
@@ -493,7 +486,7 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
                 // group qit's metadata was issued before the last produce's two stage
                 // loads (on this group's first stage, or at the prologue): retired
                 // once at most those two are in flight (stores do not count: older)
-                vr_wait_meta<2, BIN>(mbase, lane, mL, moff, midx);
+                vr_wait_meta<2, BIN, kPk>(mbase, lane_p(), mL, moff, midx);
                 pit = qit;
                 qlive = advance(qit);
                 producer_enter();
@@ -516,7 +509,7 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
         if (meta) {
             load_meta(qit);
             vr_issue_stage<slot, NT>(s0, s1);
-            if constexpr (WS >= 0) vr_wait_stage<(ABL & 4) ? 0 : (BIN ? 6 : 5)>();   // 3 (BIN: 4) metadata + 2 stage loads younger
+            if constexpr (WS >= 0) vr_wait_stage<(ABL & 4) ? 0 : 3>();   // the metadata load + 2 stage loads younger
         } else {
             vr_issue_stage<slot, NT>(s0, s1);
             if constexpr (WS >= 0) vr_wait_stage<(ABL & 4) ? 0 : 2>();

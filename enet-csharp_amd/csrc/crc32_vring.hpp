@@ -55,9 +55,8 @@ int vring_setup();
 // count: one per CU; twice that: two).  trace = per-wave timestamps (diagnostics
 // library) or null.  bin = the batches' metadata are length-binned records {len,
 // off_lo, off_hi, index} (VrBatch::off points at them, len unused): results go to
-// out[index]; 82.5 KiB of LDS, so at most one workgroup per CU (max_wgs = the CU
-// count).  Returns 0 or -hipError_t (-hipErrorInvalidValue for a variant this
-// library does not build).
+// out[index].  70.5 KiB of LDS either way: one or two workgroups per CU.  Returns 0
+// or -hipError_t (-hipErrorInvalidValue for a variant this library does not build).
 int vring_launch_list(int lg, int max_wgs, const VrVariant& v, hipStream_t st, const VrBatches& bl,
                       const KernelTables& tb, const uint32_t* basis2, uint64_t* trace, bool bin = false);
 

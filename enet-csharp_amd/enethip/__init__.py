@@ -42,7 +42,14 @@ EXPORTED_SYMBOLS = (
     "enet_hip_memcpy_d2h", "enet_hip_synchronize", "enet_hip_read_probe_device", "enet_hip_set_kernel_path",
     "enet_hip_is_diagnostics_build", "enet_hip_fragment_reassemble_device",
     "enet_hip_range_compress_device", "enet_hip_range_decompress_device",
+    "enet_hip_crc32_gather_binned_host", "enet_hip_udp_receive", "enet_hip_parse_headers", "enet_hip_udp_send",
+    "enet_hip_stamp_callback", "enet_hip_verify_callback", "enet_hip_udp_receive_verify", "enet_hip_udp_stamp_send",
 )
+
+# include/enet_hip.h socket-harness constants
+ERRNO_BASE = 100000
+DGRAM_TRUNCATED = 0xFFFFFFFF
+DGRAM_CHECKSUM, DROP_SHORT, DROP_PEER, DROP_COMPRESSED, DROP_TRUNCATED = 0, 1, 2, 3, 4
 # Declared under #ifdef ENET_HIP_DIAG: exported by libenethip_diag.so only.
 DIAG_SYMBOLS = ("enet_hip_diag_ablation", "enet_hip_diag_trace")
 
@@ -150,6 +157,25 @@ def load(path: str | None = None, diag: bool = False) -> ctypes.CDLL:
     for f in ("enet_hip_range_compress_device", "enet_hip_range_decompress_device"):
         getattr(L, f).restype = i32
         getattr(L, f).argtypes = [vp, vp, vp, vp, sz, vp, vp, vp, vp, vp]
+    szp = ctypes.POINTER(sz)
+    L.enet_hip_crc32_gather_binned_host.restype = i32
+    L.enet_hip_crc32_gather_binned_host.argtypes = [vp, vp, sz, vp, vp, sz, vp, sz, vp]
+    L.enet_hip_udp_receive.restype = i32
+    L.enet_hip_udp_receive.argtypes = [i32, vp, sz, sz, vp, vp, vp, i32, szp]
+    L.enet_hip_parse_headers.restype = i32
+    L.enet_hip_parse_headers.argtypes = [vp, sz, vp, sz, vp, sz, vp, vp, vp]
+    L.enet_hip_udp_send.restype = i32
+    L.enet_hip_udp_send.argtypes = [i32, vp, vp, vp, vp, sz, u32, ctypes.c_uint16, szp]
+    L.enet_hip_stamp_callback.restype = i32
+    L.enet_hip_stamp_callback.argtypes = [vp, vp, vp, vp, vp, sz]
+    L.enet_hip_verify_callback.restype = i32
+    L.enet_hip_verify_callback.argtypes = [vp, sz, vp, vp, vp, vp, sz, vp]
+    L.enet_hip_udp_receive_verify.restype = i32
+    L.enet_hip_udp_receive_verify.argtypes = [vp, i32, vp, sz, sz, vp, sz, i32, vp, vp, szp]
+    L.enet_hip_udp_stamp_send.restype = i32
+    L.enet_hip_udp_stamp_send.argtypes = [vp, i32, vp, sz, vp, vp, sz, vp, vp, sz, u32, ctypes.c_uint16, szp]
+    L.enet_hip_is_diagnostics_build.restype = i32
+    L.enet_hip_is_diagnostics_build.argtypes = []
     L.enet_hip_fragment_reassemble_device.restype = i32
     L.enet_hip_fragment_reassemble_device.argtypes = [vp, vp, vp, vp, vp, sz, u32, vp, vp, vp, vp, vp, u32, vp, sz,
                                                       vp, vp]
@@ -335,6 +361,40 @@ class Context:
     def synchronize(self) -> None:
         _check("enet_hip_synchronize", self.lib.enet_hip_synchronize(self.handle))
 
+    # --- host-memory entry points and the GPU socket pipelines (synchronous) ---
+    def gather_binned_host(self, payload: np.ndarray, seg_off, seg_len, seg_first) -> np.ndarray:
+        payload = np.ascontiguousarray(payload, dtype=np.uint8)
+        seg_off, seg_len, seg_first = _u(seg_off, np.uint64), _u(seg_len, np.uint32), _u(seg_first, np.uint32)
+        n = len(seg_first) - 1
+        out = np.zeros(max(1, n), dtype=np.uint32)
+        _check("enet_hip_crc32_gather_binned_host", self.lib.enet_hip_crc32_gather_binned_host(
+            self.handle, _ptr(payload), payload.nbytes, _ptr(seg_off) if len(seg_off) else None,
+            _ptr(seg_len) if len(seg_len) else None, len(seg_off), _ptr(seg_first), n, _ptr(out)))
+        return out[:n]
+
+    def udp_receive_verify(self, fd: int, arena, stride: int, max_dgrams: int, peer_connect_ids,
+                           timeout_ms: int = 0):
+        """-> (count, lengths[count], ok[count]): socket -> header stage -> GPU verify -> keep mask."""
+        peers = _u(peer_connect_ids, np.uint32)
+        lens = np.zeros(max(1, max_dgrams), np.uint32)
+        ok = np.zeros(max(1, max_dgrams), np.uint8)
+        got = ctypes.c_size_t(0)
+        _check("enet_hip_udp_receive_verify", self.lib.enet_hip_udp_receive_verify(
+            self.handle, int(fd), _ptr(arena), int(stride), int(max_dgrams), _ptr(peers) if len(peers) else None,
+            len(peers), int(timeout_ms), _ptr(lens), _ptr(ok), ctypes.byref(got)))
+        n = got.value
+        return n, lens[:n], ok[:n]
+
+    def udp_stamp_send(self, fd: int, payload, seg_off, seg_len, seg_first, slot_off, addr: int, port: int) -> int:
+        """GPU stamp of the gather-list DGRAMs (payload modified in place), then sendmmsg."""
+        seg_off, seg_len, seg_first, slot_off = (_u(seg_off, np.uint64), _u(seg_len, np.uint32),
+                                                 _u(seg_first, np.uint32), _u(slot_off, np.uint32))
+        sent = ctypes.c_size_t(0)
+        _check("enet_hip_udp_stamp_send", self.lib.enet_hip_udp_stamp_send(
+            self.handle, int(fd), _ptr(payload), int(payload.nbytes), _ptr(seg_off), _ptr(seg_len), len(seg_off),
+            _ptr(seg_first), _ptr(slot_off), len(seg_first) - 1, int(addr), int(port), ctypes.byref(sent)))
+        return sent.value
+
     # --- host-memory entry point (synchronous) ---
     def crc32_batch_host(self, payload: np.ndarray, off: np.ndarray, lens: np.ndarray) -> np.ndarray:
         payload = np.ascontiguousarray(payload, dtype=np.uint8)
@@ -344,6 +404,74 @@ class Context:
         _check("enet_hip_crc32_batch_host", self.lib.enet_hip_crc32_batch_host(
             self.handle, _ptr(payload), payload.nbytes, _ptr(off), _ptr(lens), len(off), _ptr(out)))
         return out
+
+
+def _u(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+# ------------------------------------------------------------------ socket harness
+# (include/enet_hip.h "UDP socket batching harness"; fd = socket.fileno() of a bound
+# IPv4 UDP socket, addresses as host-order ints)
+
+def udp_receive(fd: int, arena: np.ndarray, stride: int, max_dgrams: int, timeout_ms: int = 0):
+    """-> (count, lengths[count], src_addr[count], src_port[count]); DGRAM i at arena[i*stride:]."""
+    L = load()
+    lens = np.zeros(max(1, max_dgrams), np.uint32)
+    addr = np.zeros(max(1, max_dgrams), np.uint32)
+    port = np.zeros(max(1, max_dgrams), np.uint16)
+    got = ctypes.c_size_t(0)
+    _check("enet_hip_udp_receive", L.enet_hip_udp_receive(int(fd), _ptr(arena), int(stride), int(max_dgrams),
+                                                          _ptr(lens), _ptr(addr), _ptr(port), int(timeout_ms),
+                                                          ctypes.byref(got)))
+    n = got.value
+    return n, lens[:n], addr[:n], port[:n]
+
+
+def parse_headers(arena: np.ndarray, stride: int, lengths: np.ndarray, peer_connect_ids: np.ndarray):
+    """ENet's receive header stage (c/protocol.cs:1001-1030) -> (slot_off, connect_id, verdict)."""
+    L = load()
+    n = len(lengths)
+    lengths = _u(lengths, np.uint32)
+    peers = _u(peer_connect_ids, np.uint32)
+    slot, conn, verdict = np.zeros(max(1, n), np.uint32), np.zeros(max(1, n), np.uint32), np.zeros(max(1, n), np.uint8)
+    _check("enet_hip_parse_headers", L.enet_hip_parse_headers(_ptr(arena), int(stride), _ptr(lengths), n,
+                                                              _ptr(peers) if len(peers) else None, len(peers),
+                                                              _ptr(slot), _ptr(conn), _ptr(verdict)))
+    return slot[:n], conn[:n], verdict[:n]
+
+
+def udp_send(fd: int, payload: np.ndarray, seg_off, seg_len, seg_first, addr: int, port: int) -> int:
+    """sendmmsg of the gather-list DGRAMs; returns how many the socket accepted."""
+    L = load()
+    seg_off, seg_len, seg_first = _u(seg_off, np.uint64), _u(seg_len, np.uint32), _u(seg_first, np.uint32)
+    sent = ctypes.c_size_t(0)
+    _check("enet_hip_udp_send", L.enet_hip_udp_send(int(fd), _ptr(payload), _ptr(seg_off), _ptr(seg_len),
+                                                    _ptr(seg_first), len(seg_first) - 1, int(addr), int(port),
+                                                    ctypes.byref(sent)))
+    return sent.value
+
+
+def stamp_callback(payload: np.ndarray, seg_off, seg_len, seg_first, slot_off) -> None:
+    """Per-DGRAM callback stamp (protocol.cs:1690-1698), in place, on the CPU."""
+    L = load()
+    seg_off, seg_len, seg_first, slot_off = (_u(seg_off, np.uint64), _u(seg_len, np.uint32),
+                                             _u(seg_first, np.uint32), _u(slot_off, np.uint32))
+    _check("enet_hip_stamp_callback", L.enet_hip_stamp_callback(_ptr(payload), _ptr(seg_off), _ptr(seg_len),
+                                                                _ptr(seg_first), _ptr(slot_off), len(seg_first) - 1))
+
+
+def verify_callback(arena: np.ndarray, stride: int, lengths, slot_off, connect_ids, verdict=None) -> np.ndarray:
+    """Per-DGRAM callback verify (protocol.cs:1052-1068) on the CPU, slot replaced in place."""
+    L = load()
+    n = len(lengths)
+    lengths, slot_off, connect_ids = _u(lengths, np.uint32), _u(slot_off, np.uint32), _u(connect_ids, np.uint32)
+    vd = None if verdict is None else _u(verdict, np.uint8)
+    ok = np.zeros(max(1, n), np.uint8)
+    _check("enet_hip_verify_callback", L.enet_hip_verify_callback(_ptr(arena), int(stride), _ptr(lengths),
+                                                                  _ptr(slot_off), _ptr(connect_ids),
+                                                                  _ptr(vd) if vd is not None else None, n, _ptr(ok)))
+    return ok[:n]
 
 
 def crc32_batch_multi(contexts: Sequence[Context], payload: np.ndarray, off: np.ndarray,

@@ -250,3 +250,56 @@ def overlapping_fragments(messages: int, seed: int = SEED_PAYLOAD, max_count: in
         slots[i] = m
     return FragmentBatch(arena, cmd_off, cmd_avail, slots, np.array(lens, dtype=np.uint32),
                          np.array(counts, dtype=np.uint32), [], 0, name)
+
+
+@dataclass
+class SendBatch:
+    """DGRAMs as an ENet host sends them with a checksum (c/protocol.cs:1640-1698): a
+    gather list of [ENetProtocolHeader: peerID | flags | session (big endian), sentTime
+    if SENT_TIME][4-B checksum slot = the peer's connectID, or 0 for peerID 0xFFF]
+    [12-B command][body].  peers[p] = connectID of outgoing peer p (the receiver's
+    table for incoming peer p); slot_off[d] = the slot's offset in DGRAM d's first
+    buffer; seq[d] = a 4-byte sequence number at the start of the command."""
+    gather: GatherBatch
+    slot_off: np.ndarray   # uint32
+    peer: np.ndarray       # uint32 (0xFFF = no peer)
+    peers: np.ndarray      # uint32 connectIDs
+
+    @property
+    def n(self) -> int:
+        return self.gather.n
+
+
+def send_batch(n: int, n_peers: int = 7, body: tuple = (0, 1360), seed: int = SEED_PAYLOAD) -> SendBatch:
+    rng = np.random.default_rng(seed)
+    peers = rng.integers(1, 2**32, size=n_peers, dtype=np.uint64).astype(np.uint32)
+    peer = rng.integers(0, n_peers + 1, size=n).astype(np.uint32)
+    peer[peer == n_peers] = 0xFFF                           # connect requests: no peer yet
+    sent_time = rng.integers(0, 2, size=n).astype(bool)
+    hdr_len = np.where(sent_time, 8, 6).astype(np.uint32)   # header (2 or 4 B) + 4-B slot
+    body_len = rng.integers(body[0], body[1] + 1, size=n).astype(np.uint32)
+    hdr_off = np.zeros(n, np.uint64)
+    np.cumsum(np.full(n, 8, np.uint64)[:-1], out=hdr_off[1:])
+    cmd_base = np.uint64(8 * n)
+    body_base = cmd_base + np.uint64(12 * n)
+    body_off = body_base + np.concatenate([[0], np.cumsum(body_len.astype(np.uint64))[:-1]]).astype(np.uint64)
+    payload = payload_bytes(int(body_base) + int(body_len.astype(np.uint64).sum()) + 16, seed)
+    session = rng.integers(0, 4, size=n).astype(np.uint32)
+    word = (peer | (sent_time.astype(np.uint32) << 15) | np.where(peer == 0xFFF, 0, session << 12)).astype(np.uint32)
+    for d in range(n):
+        o = int(hdr_off[d])
+        payload[o:o + 2] = np.frombuffer(int(word[d]).to_bytes(2, "big"), np.uint8)
+        s = o + int(hdr_len[d]) - 4
+        cid = 0 if peer[d] == 0xFFF else int(peers[peer[d]])
+        payload[s:s + 4] = np.frombuffer(np.uint32(cid).tobytes(), np.uint8)
+        c = int(cmd_base) + 12 * d
+        payload[c:c + 4] = np.frombuffer(np.uint32(d).tobytes(), np.uint8)   # sequence number
+    seg_off = np.zeros(3 * n, np.uint64)
+    seg_len = np.zeros(3 * n, np.uint32)
+    seg_off[0::3], seg_len[0::3] = hdr_off, hdr_len
+    seg_off[1::3], seg_len[1::3] = cmd_base + np.arange(n, dtype=np.uint64) * np.uint64(12), 12
+    seg_off[2::3], seg_len[2::3] = body_off, body_len
+    first = (np.arange(n + 1, dtype=np.uint64) * np.uint64(3)).astype(np.uint32)
+    g = GatherBatch(payload, seg_off, seg_len, first, int(seg_len.astype(np.uint64).sum()),
+                    f"send batch: {n} DGRAMs")
+    return SendBatch(g, (hdr_len - 4).astype(np.uint32), peer, peers)

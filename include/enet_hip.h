@@ -139,9 +139,12 @@ ENET_HIP_API int enet_hip_crc32_batch_device_binned(enet_hip_context* ctx, const
                                                     size_t workspaceBytes, void* stream);
 
 /* ---- batched checksum from/to host memory ----
- * bytes[0 .. byteCount) is copied H2D, the batch is checksummed on the GPU and
- * out[] is copied back; synchronous.  Host buffers allocated with
- * enet_hip_host_alloc are pinned and give full PCIe rate. */
+ * Packets in host memory, CRCs back to host memory; synchronous.  Pipelined: the
+ * batch is cut into chunks of consecutive packets (about 16 MiB of payload each)
+ * on two streams -- H2D of a chunk's byte span and metadata, the checksum kernel,
+ * D2H of its CRCs -- so one chunk's copy overlaps the previous chunk's kernel.
+ * Host buffers allocated with enet_hip_host_alloc are pinned and give the full
+ * PCIe rate. */
 ENET_HIP_API int enet_hip_crc32_batch_host(enet_hip_context* ctx, const uint8_t* bytes, size_t byteCount,
                                            const uint64_t* offsets, const uint32_t* lengths,
                                            size_t count, uint32_t* out);
@@ -262,10 +265,101 @@ ENET_HIP_API int enet_hip_range_decompress_device(enet_hip_context* ctx, const u
                                                   uint8_t* out, const uint64_t* outOffsets, const uint32_t* outLimits,
                                                   uint32_t* outLengths, void* stream);
 
+/* ---- host-memory gather lists (send side, c/protocol.cs:1690-1698) ----
+ * enet_hip_crc32_gather_binned_device with HOST arrays: bytes[0 .. byteCount) and
+ * the segment metadata are copied H2D (the arena in two halves on two streams),
+ * the binned gather CRC runs on the GPU, out[] is copied back.  The DGRAMs use
+ * segments segFirst[0] .. segFirst[dgramCount]-1 of the segCount given (a send
+ * batch may be a slice of a longer list; checked).  Synchronous; pinned host
+ * memory (enet_hip_host_alloc) gives the full PCIe rate. */
+ENET_HIP_API int enet_hip_crc32_gather_binned_host(enet_hip_context* ctx, const uint8_t* bytes, size_t byteCount,
+                                                   const uint64_t* segOffsets, const uint32_t* segLengths,
+                                                   size_t segCount, const uint32_t* segFirst, size_t dgramCount,
+                                                   uint32_t* out);
+
+/* ---- UDP socket batching harness (Linux recvmmsg / sendmmsg) ----
+ * The path's host ends: DGRAMs arrive from a UDP socket buffer and leave through
+ * one.  These batch the system calls and the per-DGRAM steps ENet runs around
+ * host->checksum:
+ *   receive  c/protocol.cs:1209-1240 (up to 256 DGRAMs of <= 4096 B per service
+ *            pass, one recvmsg each: plugins/NativeSockets/Unix/Linux/c/
+ *            LinuxSocketPal.cs:407-449, a truncated DGRAM returns -1);
+ *   header   c/protocol.cs:1001-1030;  verify c/protocol.cs:1052-1068;
+ *   stamp    c/protocol.cs:1690-1698;  send LinuxSocketPal.cs:315-349 (sendmsg
+ *            with the gather list as iovecs, <= 65 buffers).
+ * fd is a bound IPv4 UDP socket; addresses and ports are in host order.  Socket
+ * functions return 0, -1 for a bad argument, or -(ENET_HIP_ERRNO_BASE + errno) for
+ * a failed system call; the GPU pipelines also -hipError_t. */
+#define ENET_HIP_ERRNO_BASE 100000
+#define ENET_HIP_DGRAM_TRUNCATED 0xFFFFFFFFu   /* lengths[i] of a DGRAM longer than the slot */
+/* enet_hip_parse_headers verdicts: 0 = the DGRAM goes on to the checksum; else the
+ * reason the reference returns before it (the DGRAM is dropped). */
+#define ENET_HIP_DGRAM_CHECKSUM 0
+#define ENET_HIP_DROP_SHORT 1       /* < 2 B (protocol.cs:1001), or no room for the slot */
+#define ENET_HIP_DROP_PEER 2        /* peerID >= peerCount (protocol.cs:1017-1018) */
+#define ENET_HIP_DROP_COMPRESSED 3  /* compressed, no decompressor here (protocol.cs:1033-1036) */
+#define ENET_HIP_DROP_TRUNCATED 4   /* did not fit its receive slot (LinuxSocketPal.cs:425-426) */
+
+/* Receive up to maxDgrams DGRAMs, DGRAM i into arena + i*stride (stride >= 4096 =
+ * ENet's receive buffer), lengths[i] its length (ENET_HIP_DGRAM_TRUNCATED if it did
+ * not fit).  Waits up to timeoutMs for the first DGRAM (0 = no wait, < 0 = forever),
+ * then takes what is queued without blocking, 256 per recvmmsg.  srcAddr / srcPort
+ * may be NULL.  *received = the count. */
+ENET_HIP_API int enet_hip_udp_receive(int fd, uint8_t* arena, size_t stride, size_t maxDgrams, uint32_t* lengths,
+                                      uint32_t* srcAddr, uint16_t* srcPort, int timeoutMs, size_t* received);
+
+/* ENet's header stage for received DGRAMs (c/protocol.cs:1001-1030): from each
+ * ENetProtocolHeader, slotOffsets[i] = the checksum slot's offset (2, or 4 with
+ * ENET_PROTOCOL_HEADER_FLAG_SENT_TIME), connectIds[i] = peerConnectIds[peerID] (0
+ * for peerID 0xFFF, "no peer"), verdict[i] = ENET_HIP_DGRAM_CHECKSUM or a drop
+ * reason.  (Peer state, address and session checks are ENet's, out of scope.) */
+ENET_HIP_API int enet_hip_parse_headers(const uint8_t* arena, size_t stride, const uint32_t* lengths, size_t count,
+                                        const uint32_t* peerConnectIds, size_t peerCount, uint32_t* slotOffsets,
+                                        uint32_t* connectIds, uint8_t* verdict);
+
+/* Send DGRAM d = the gather list of segments segFirst[d] .. segFirst[d+1]-1
+ * (bytes + segOffsets[s], segLengths[s]; at most 65) to dstAddr:dstPort, 256 per
+ * sendmmsg.  *sent = the DGRAMs the socket accepted (a full socket buffer ends the
+ * call early with 0). */
+ENET_HIP_API int enet_hip_udp_send(int fd, const uint8_t* bytes, const uint64_t* segOffsets,
+                                   const uint32_t* segLengths, const uint32_t* segFirst, size_t dgramCount,
+                                   uint32_t dstAddr, uint16_t dstPort, size_t* sent);
+
+/* The reference's per-DGRAM callback engine, batched, on the CPU (the path ENet
+ * runs today, one enet_hip_crc32 call per DGRAM; the GPU pipelines below are
+ * checked and timed against it).  stamp: the 4 bytes at slotOffsets[d] of DGRAM d's
+ * first segment hold connectID (or 0) on entry and its CRC on return
+ * (protocol.cs:1694-1697).  verify: ok[i] as protocol.cs:1054-1067 decides, with
+ * the slot replaced by connectIds[i] IN PLACE in the arena as the reference does;
+ * DGRAMs whose verdict (may be NULL) is not ENET_HIP_DGRAM_CHECKSUM get ok = 0. */
+ENET_HIP_API int enet_hip_stamp_callback(uint8_t* bytes, const uint64_t* segOffsets, const uint32_t* segLengths,
+                                         const uint32_t* segFirst, const uint32_t* slotOffsets, size_t dgramCount);
+ENET_HIP_API int enet_hip_verify_callback(uint8_t* arena, size_t stride, const uint32_t* lengths,
+                                          const uint32_t* slotOffsets, const uint32_t* connectIds,
+                                          const uint8_t* verdict, size_t count, uint8_t* ok);
+
+/* Receive side on the GPU, socket to keep mask: enet_hip_udp_receive into `arena`
+ * (pinned: enet_hip_host_alloc), the header stage, one pitched H2D (only each slot's
+ * first maxLen bytes cross PCIe), receive verify of the whole batch
+ * (enet_hip_verify_batch_device) and D2H: ok[i] = 1 where ENet keeps DGRAM i.  The
+ * arena is not modified.  Synchronous. */
+ENET_HIP_API int enet_hip_udp_receive_verify(enet_hip_context* ctx, int fd, uint8_t* arena, size_t stride,
+                                             size_t maxDgrams, const uint32_t* peerConnectIds, size_t peerCount,
+                                             int timeoutMs, uint32_t* lengths, uint8_t* ok, size_t* received);
+
+/* Send side on the GPU: every DGRAM's CRC over its gather list
+ * (enet_hip_crc32_gather_binned_host), written into its slot as protocol.cs:1697
+ * does (slot bytes hold connectID or 0 on entry; `bytes` is modified), then
+ * enet_hip_udp_send.  Synchronous. */
+ENET_HIP_API int enet_hip_udp_stamp_send(enet_hip_context* ctx, int fd, uint8_t* bytes, size_t byteCount,
+                                         const uint64_t* segOffsets, const uint32_t* segLengths, size_t segCount,
+                                         const uint32_t* segFirst, const uint32_t* slotOffsets, size_t dgramCount,
+                                         uint32_t dstAddr, uint16_t dstPort, size_t* sent);
+
 /* ---- multi-GPU: independent contiguous shards, no collective ----
- * Packets [i*count/k, (i+1)*count/k) go to contexts[i]; each shard's bytes are
- * copied to its device, checksummed and the CRCs copied back into out[].
- * Synchronous; one host thread per device. */
+ * Packets [i*count/k, (i+1)*count/k) go to contexts[i], each through the pipelined
+ * enet_hip_crc32_batch_host of its device (its own streams, PCIe link and HBM), the
+ * CRCs into out[].  Synchronous; one host thread per device. */
 ENET_HIP_API int enet_hip_crc32_batch_multi(enet_hip_context* const* contexts, int contextCount,
                                             const uint8_t* bytes, size_t byteCount, const uint64_t* offsets,
                                             const uint32_t* lengths, size_t count, uint32_t* out);

@@ -1,0 +1,157 @@
+"""GPU parity of the host-memory entry points and the socket pipelines
+(csrc/host_pipeline.hip) against the oracle: the pipelined checksum of host
+batches (cfg2 in full, many chunks, offsets out of order, multi-context shards),
+the host gather lists at full cfg5 size (4096 x 64 KiB messages = 200 704
+DGRAMs), and the GPU stamp / receive-verify over a loopback socket."""
+import socket
+
+import numpy as np
+import pytest
+
+import enethip
+from enethip import workloads
+from test_gpu_parity import ctx  # noqa: F401  (fixture)
+from test_udp_harness import (LOOPBACK, STRIDE, expected_keep, odd_dgrams, oracle_stamps, slots_of,  # noqa: F401
+                              sockets)
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def pinned(n):
+    """Host memory from enet_hip_host_alloc (pinned), as a numpy view; (array, pointer)."""
+    import ctypes
+    lib = enethip.load()
+    p = ctypes.c_void_p()
+    assert lib.enet_hip_host_alloc(n, ctypes.byref(p)) == 0
+    buf = (ctypes.c_uint8 * n).from_address(p.value)
+    return np.frombuffer(buf, dtype=np.uint8), p
+
+
+def free_pinned(p):
+    enethip.load().enet_hip_host_free(p)
+
+
+def test_batch_host_cfg2_pipelined(ctx, oracle_lib):  # noqa: F811
+    """cfg2 (75 MiB: five 16-MiB chunks over two streams) from pinned host memory."""
+    b = workloads.cfg2()
+    exp = oracle_lib.batch(b.payload, b.off, b.lens, threads=16)
+    arr, p = pinned(b.payload.nbytes)
+    try:
+        arr[:] = b.payload
+        assert (ctx.crc32_batch_host(arr, b.off, b.lens) == exp).all()
+    finally:
+        free_pinned(p)
+
+
+def test_batch_host_chunks_and_orders(ctx, oracle_lib):  # noqa: F811
+    """Many chunks (300 K mixed packets, pageable memory), packets in arbitrary order
+    (the one-span fallback), a single packet and empty packets."""
+    b = workloads.mixed(300_000, 0, 1400, seed=61, len_seed=62)
+    exp = oracle_lib.batch(b.payload, b.off, b.lens, threads=16)
+    assert (ctx.crc32_batch_host(b.payload, b.off, b.lens) == exp).all()
+    perm = np.random.default_rng(63).permutation(b.n)
+    assert (ctx.crc32_batch_host(b.payload, b.off[perm], b.lens[perm]) == exp[perm]).all()
+    assert (ctx.crc32_batch_host(b.payload, b.off[7:8], b.lens[7:8]) == exp[7:8]).all()
+    with pytest.raises(enethip.ENetHipError):                # a packet past the arena: rejected
+        ctx.crc32_batch_host(b.payload[:100], b.off[:2], np.array([50, 60], np.uint32) + 50)
+
+
+def test_batch_multi_contexts(oracle_lib):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    b = workloads.mixed(400_001, 64, 1400, seed=64, len_seed=65)
+    ctxs = [enethip.Context(i % max(1, enethip.device_count())) for i in range(3)]
+    try:
+        got = enethip.crc32_batch_multi(ctxs, b.payload, b.off, b.lens)
+    finally:
+        for c in ctxs:
+            c.close()
+    assert (got == oracle_lib.batch(b.payload, b.off, b.lens, threads=16)).all()
+
+
+def test_gather_binned_host_full_cfg5(ctx, oracle_lib):  # noqa: F811
+    """cfg5 at full size: 4096 messages x 64 KiB -> 200 704 three-buffer DGRAMs
+    (274.9 MB) from pinned host memory, against the oracle's gather."""
+    g = workloads.cfg5()
+    assert g.n == 200_704
+    exp = oracle_lib.gather(g.payload, g.seg_off, g.seg_len, g.seg_first)
+    arr, p = pinned(g.payload.nbytes)
+    try:
+        arr[:] = g.payload
+        got = ctx.gather_binned_host(arr, g.seg_off, g.seg_len, g.seg_first)
+    finally:
+        free_pinned(p)
+    assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
+    # random gather lists (0-65 buffers, empty buffers and DGRAMs), pageable memory
+    rng = np.random.default_rng(66)
+    payload = rng.integers(0, 256, size=1 << 20, dtype=np.uint8)
+    cnt = rng.integers(0, 66, size=500)
+    sf = np.zeros(501, np.uint32)
+    np.cumsum(cnt, out=sf[1:])
+    ns = int(sf[-1])
+    lens = np.where(rng.integers(0, 6, size=ns) == 0, 0, rng.integers(1, 1400, size=ns)).astype(np.uint32)
+    offs = rng.integers(0, len(payload) - 1400, size=ns).astype(np.uint64)
+    assert (ctx.gather_binned_host(payload, offs, lens, sf) == oracle_lib.gather(payload, offs, lens, sf)).all()
+    with pytest.raises(enethip.ENetHipError):                # segFirst[n] > segCount: rejected
+        ctx.gather_binned_host(payload, offs, lens, np.concatenate([sf[:-1], [ns + 1]]).astype(np.uint32))
+    sl = sf[100:301]                                         # a slice of the list (segFirst[0] > 0)
+    exp = oracle_lib.gather(payload, offs, lens, sf)
+    assert (ctx.gather_binned_host(payload, offs, lens, sl) == exp[100:300]).all()
+
+
+@pytest.mark.parametrize("corrupt", [0, 61])
+def test_gpu_stamp_send_and_receive_verify(ctx, oracle_lib, corrupt):  # noqa: F811
+    """The socket harness around the GPU: enet_hip_udp_stamp_send (GPU stamp,
+    protocol.cs:1690-1698, then sendmmsg) and enet_hip_udp_receive_verify (recvmmsg,
+    header stage, pitched H2D, GPU verify, protocol.cs:1052-1068): stamps and keep
+    mask equal to the oracle's, header-stage drops included."""
+    sb = workloads.send_batch(3000, seed=70 + corrupt)
+    g = sb.gather
+    exp_stamp = oracle_stamps(oracle_lib, sb)
+    rx, tx, port = sockets()
+    arena, p = pinned(STRIDE * 512)
+    try:
+        rng = np.random.default_rng(corrupt)
+        recv_rows, recv_lens, oks = [], [], []
+        for a in range(0, sb.n, 400):
+            b = min(sb.n, a + 400)
+            sf = g.seg_first[a:b + 1]
+            sent = ctx.udp_stamp_send(tx.fileno(), g.payload, g.seg_off, g.seg_len, sf, sb.slot_off[a:b],
+                                      LOOPBACK, port)
+            assert sent == b - a
+            n, lens, ok = ctx.udp_receive_verify(rx.fileno(), arena, STRIDE, 512, sb.peers, timeout_ms=2000)
+            assert n == b - a
+            recv_rows.append(arena[:n * STRIDE].copy())
+            recv_lens.append(lens.copy())
+            oks.append(ok.copy())
+        assert (slots_of(sb) == exp_stamp).all()
+        ok = np.concatenate(oks)
+        assert ok.sum() == sb.n                                   # every stamped DGRAM kept
+        # corrupted re-sends and the odd DGRAMs: drops decided as the oracle decides
+        if corrupt:
+            for d in rng.choice(sb.n, corrupt, replace=False):
+                s = int(g.seg_first[d]) + int(rng.integers(0, 3))
+                if g.seg_len[s]:
+                    g.payload[int(g.seg_off[s]) + int(rng.integers(0, int(g.seg_len[s])))] ^= np.uint8(2)
+        sent = enethip.udp_send(tx.fileno(), g.payload, g.seg_off, g.seg_len, g.seg_first[:401], LOOPBACK, port)
+        assert sent == 400
+        for dg in odd_dgrams(sb.peers):
+            tx.sendto(dg, ("127.0.0.1", port))
+        got = 0
+        rows, lens_l, oks2 = [], [], []
+        while got < 405:
+            n, lens, okb = ctx.udp_receive_verify(rx.fileno(), arena, STRIDE, 512, sb.peers, timeout_ms=2000)
+            assert n > 0
+            rows.append(arena[:n * STRIDE].copy())
+            lens_l.append(lens.copy())
+            oks2.append(okb.copy())
+            got += n
+        recv, lens, ok2 = np.concatenate(rows), np.concatenate(lens_l), np.concatenate(oks2)
+        exp = expected_keep(oracle_lib, recv, STRIDE, lens, sb.peers)
+        assert (ok2 == exp).all(), np.nonzero(ok2 != exp)[0][:10]
+        assert exp[-5:].sum() == 0
+    finally:
+        free_pinned(p)
+        rx.close()
+        tx.close()

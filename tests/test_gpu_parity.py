@@ -667,7 +667,9 @@ def test_vring_trace_instance(dctx, oracle_lib):
     ctx = dctx
     b = workloads.mixed(100_000, 0, 3000, seed=91, len_seed=92)
     exp = oracle_lib.batch(b.payload, b.off, b.lens, threads=16)
-    tr = torch.zeros(256 * 16 * 8, dtype=torch.int64, device="cuda")
+    # 8 x u64 per wave: up to 2 workgroups per CU (the default) x 16 waves
+    props = torch.cuda.get_device_properties(0)
+    tr = torch.zeros(2 * props.multi_processor_count * 16 * 8, dtype=torch.int64, device="cuda")
     ctx.diag_trace(tr)
     try:
         for lanes in (4, 8):

@@ -71,7 +71,8 @@ static uint32_t stamp(Checksum cb, Dgram* d, uint32_t connect) {
     /* the socket layer sends the buffers back to back (c/win32.cs:168-194) */
     memcpy(d->wire, d->hdr, HDR + SLOT);
     memcpy(d->wire + HDR + SLOT, d->cmd, d->cmd_len);
-    memcpy(d->wire + HDR + SLOT + d->cmd_len, d->payload, d->payload_len);
+    if (d->payload_len) /* (an ack carries no payload: payload may be NULL) */
+        memcpy(d->wire + HDR + SLOT + d->cmd_len, d->payload, d->payload_len);
     d->wire_len = HDR + SLOT + d->cmd_len + d->payload_len;
     return crc;
 }
@@ -88,7 +89,7 @@ static int verify(Checksum cb, Dgram* d, uint32_t connect, uint32_t* computed) {
 }
 
 static void make_reliable(Dgram* d, uint16_t peer, uint16_t seq, const uint8_t* payload, size_t n) {
-    const uint16_t pid = (uint16_t)(peer | 0x4000u); /* ENET_PROTOCOL_HEADER_FLAG_SENT_TIME */
+    const uint16_t pid = (uint16_t)(peer | 0x8000u); /* ENET_PROTOCOL_HEADER_FLAG_SENT_TIME = 1 << 15 */
     const uint16_t sent = (uint16_t)(seq * 7u);
     d->hdr[0] = (uint8_t)(pid >> 8), d->hdr[1] = (uint8_t)pid; /* network order */
     d->hdr[2] = (uint8_t)(sent >> 8), d->hdr[3] = (uint8_t)sent;
@@ -102,7 +103,7 @@ static void make_reliable(Dgram* d, uint16_t peer, uint16_t seq, const uint8_t* 
 }
 
 static void make_ack(Dgram* d, uint16_t peer, uint16_t seq) {
-    const uint16_t pid = (uint16_t)(peer | 0x4000u);
+    const uint16_t pid = (uint16_t)(peer | 0x8000u); /* SENT_TIME */
     const uint16_t sent = (uint16_t)(seq * 7u + 1u);
     d->hdr[0] = (uint8_t)(pid >> 8), d->hdr[1] = (uint8_t)pid;
     d->hdr[2] = (uint8_t)(sent >> 8), d->hdr[3] = (uint8_t)sent;

@@ -35,7 +35,7 @@ def main():
     from enethip import workloads
     import oracle as orc
     g = workloads.cfg5(a.messages)
-    ctx = enethip.Context(0, a.lanes, 0)
+    ctx = enethip.Context(0, a.lanes, 0, diag=a.path not in (0, 1, 2, 13, 17))
     if a.path:
         ctx.set_kernel_path(a.path)
     st = torch.cuda.Stream()

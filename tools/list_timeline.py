@@ -26,7 +26,7 @@ def main():
     lens = torch.full((65536,), 1200, dtype=torch.int32, device="cuda")
     outs = [torch.zeros(65536, dtype=torch.int32, device="cuda") for _ in range(L)]
     descs = [(big[j * BATCH:], off, lens, 65536, outs[j]) for j in range(L)]
-    ctx = enethip.Context(0, 4, wgs)
+    ctx = enethip.Context(0, 4, wgs, diag=True)
     nw = 256 * wgs * 16
     tr = torch.zeros(nw * 8, dtype=torch.int64, device="cuda")
     ctx.diag_trace(tr)

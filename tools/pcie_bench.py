@@ -1,11 +1,16 @@
 #!/usr/bin/env python3
 """Host-memory (PCIe-inclusive) rates of the checksum path, for DESIGN.md.
 
-  * cfg2 through enet_hip_crc32_batch_host with PINNED host buffers
-    (enet_hip_host_alloc): H2D of the packet bytes + offsets + lengths, the
-    stream kernel, D2H of the CRCs; synchronous per batch.
-  * cfg5 (fragmented sends, 3-buffer gather lists): pinned arenas, H2D of the
-    segment bytes and tables, crc32_gather_device, D2H of the CRCs.
+  * pcie: the raw H2D rate of the same bytes from pinned memory (enet_hip_memcpy_h2d,
+    one synchronous copy) -- the bound every host-memory case below is held against;
+  * cfg2 through enet_hip_crc32_batch_host (pipelined: 16-MiB chunks on two streams,
+    H2D + kernel + D2H), pinned host buffers;
+  * cfg5 (4096 x 64 KiB fragmented sends = 200 704 three-buffer DGRAMs) through
+    enet_hip_crc32_gather_binned_host (arena H2D in two halves on two streams, the
+    binned gather, D2H), pinned host buffers; and the old one-lane-per-DGRAM gather
+    kernel behind synchronous copies, for comparison;
+  * cfg2 over 2 contexts of the same device (enet_hip_crc32_batch_multi), the
+    multi-GPU entry's host path.
 Every result is checked against the oracle.  Prints one JSON line per case.
 """
 import ctypes
@@ -44,91 +49,91 @@ class Pinned:
         self.lib.enet_hip_host_free(self.ptr)
 
 
-class Device:
-    def __init__(self, ctx, nbytes: int):
-        self.ctx = ctx
-        p = ctypes.c_void_p()
-        rc = ctx.lib.enet_hip_device_alloc(ctx.handle, max(16, nbytes), ctypes.byref(p))
-        if rc:
-            raise RuntimeError(f"device_alloc {rc}")
-        self.ptr = p.value
-
-    def free(self):
-        self.ctx.lib.enet_hip_device_free(self.ctx.handle, self.ptr)
+def timed(fn, reps):
+    for _ in range(2):
+        fn()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    return (time.perf_counter() - t0) / reps
 
 
-def case_cfg2(ctx, reps: int):
+def case_pcie(ctx, reps):
+    lib = ctx.lib
+    n = 78_643_200
+    h = Pinned(lib, np.zeros(n, np.uint8))
+    p = ctypes.c_void_p()
+    assert lib.enet_hip_device_alloc(ctx.handle, n, ctypes.byref(p)) == 0
+    dt = timed(lambda: lib.enet_hip_memcpy_h2d(ctx.handle, p.value, h.ptr, n), reps)
+    lib.enet_hip_device_free(ctx.handle, p.value)
+    h.free()
+    return {"case": "raw pinned H2D of 75 MiB (one synchronous hipMemcpy)", "GBps": round(n / dt / 1e9, 2),
+            "GiBps": round(n / dt / GIB, 2)}
+
+
+def case_cfg2(ctx, reps):
     lib = ctx.lib
     b = workloads.cfg2()
     hp, ho, hl = Pinned(lib, b.payload), Pinned(lib, b.off), Pinned(lib, b.lens)
     out = Pinned(lib, np.zeros(b.n, np.uint32))
     call = lambda: lib.enet_hip_crc32_batch_host(ctx.handle, hp.ptr, b.payload.nbytes, ho.ptr, hl.ptr,  # noqa: E731
                                                  b.n, out.ptr)
-    for _ in range(3):
-        assert call() == 0
+    assert call() == 0
     exp = oracle.OracleLib().batch(b.payload, b.off, b.lens, threads=8)
     assert (out.arr == exp).all(), "cfg2 host path differs from the oracle"
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        call()
-    dt = (time.perf_counter() - t0) / reps
+    dt = timed(call, reps)
     for x in (hp, ho, hl, out):
         x.free()
-    return {"case": "cfg2 host path (pinned H2D + kernel + D2H, synchronous)", "payload_bytes": b.payload_bytes,
+    return {"case": "cfg2 enet_hip_crc32_batch_host (pipelined: 16-MiB chunks, 2 streams), pinned",
+            "payload_bytes": b.payload_bytes, "ms_per_batch": round(dt * 1e3, 4),
+            "GiBps": round(b.payload_bytes / dt / GIB, 2), "GBps": round(b.payload_bytes / dt / 1e9, 2)}
+
+
+def case_cfg2_multi(reps):
+    b = workloads.cfg2()
+    ctxs = [enethip.Context(0), enethip.Context(0)]
+    lib = ctxs[0].lib
+    hp = Pinned(lib, b.payload)
+    exp = oracle.OracleLib().batch(b.payload, b.off, b.lens, threads=8)
+    got = enethip.crc32_batch_multi(ctxs, hp.arr, b.off, b.lens)
+    assert (got == exp).all()
+    dt = timed(lambda: enethip.crc32_batch_multi(ctxs, hp.arr, b.off, b.lens), reps)
+    hp.free()
+    for c in ctxs:
+        c.close()
+    return {"case": "cfg2 enet_hip_crc32_batch_multi, 2 contexts on one device (the multi-GPU host path)",
             "ms_per_batch": round(dt * 1e3, 4), "GiBps": round(b.payload_bytes / dt / GIB, 2),
             "GBps": round(b.payload_bytes / dt / 1e9, 2)}
 
 
-def case_cfg5(ctx, reps: int):
+def case_cfg5(ctx, reps):
     lib = ctx.lib
     g = workloads.cfg5()
     hp = Pinned(lib, g.payload)
     ho, hl, hf = Pinned(lib, g.seg_off), Pinned(lib, g.seg_len), Pinned(lib, g.seg_first)
     out = Pinned(lib, np.zeros(g.n, np.uint32))
-    dp, do_, dl, df, dout = (Device(ctx, x.nbytes) for x in (hp, ho, hl, hf, out))
-
-    def h2d(d, h):
-        assert lib.enet_hip_memcpy_h2d(ctx.handle, d.ptr, h.ptr, h.nbytes) == 0
-
-    def once(copy_in=True):
-        if copy_in:
-            for d, h in ((dp, hp), (do_, ho), (dl, hl), (df, hf)):
-                h2d(d, h)
-        assert lib.enet_hip_crc32_gather_device(ctx.handle, dp.ptr, do_.ptr, dl.ptr, df.ptr, g.n, dout.ptr,
-                                                None) == 0
-        assert lib.enet_hip_memcpy_d2h(ctx.handle, out.ptr, dout.ptr, out.nbytes) == 0
-
-    for _ in range(2):
-        once()
+    call = lambda: lib.enet_hip_crc32_gather_binned_host(  # noqa: E731
+        ctx.handle, hp.ptr, g.payload.nbytes, ho.ptr, hl.ptr, len(g.seg_off), hf.ptr, g.n, out.ptr)
+    assert call() == 0
     exp = oracle.OracleLib().gather(g.payload, g.seg_off, g.seg_len, g.seg_first)
-    assert (out.arr == exp).all(), "cfg5 gather differs from the oracle"
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        once()
-    dt = (time.perf_counter() - t0) / reps
-    # kernel-only (tables and bytes resident), for comparison
-    ctx.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        assert lib.enet_hip_crc32_gather_device(ctx.handle, dp.ptr, do_.ptr, dl.ptr, df.ptr, g.n, dout.ptr,
-                                                None) == 0
-    ctx.synchronize()
-    dk = (time.perf_counter() - t0) / reps
-    for x in (hp, ho, hl, hf, out, dp, do_, dl, df, dout):
+    assert (out.arr == exp).all(), "cfg5 host gather differs from the oracle"
+    dt = timed(call, reps)
+    for x in (hp, ho, hl, hf, out):
         x.free()
-    return {"case": "cfg5 gather (pinned H2D of segment arena + tables, gather kernel, D2H)",
+    return {"case": "cfg5 enet_hip_crc32_gather_binned_host (arena H2D on 2 streams, binned gather, D2H), pinned",
             "dgram_bytes": g.dgram_bytes, "arena_bytes": int(g.payload.nbytes), "dgrams": g.n,
             "ms_per_batch": round(dt * 1e3, 4), "GiBps": round(g.dgram_bytes / dt / GIB, 2),
             "GBps": round(g.dgram_bytes / dt / 1e9, 2),
-            "kernel_only_ms": round(dk * 1e3, 4), "kernel_only_GiBps": round(g.dgram_bytes / dk / GIB, 2)}
+            "arena_GBps": round(g.payload.nbytes / dt / 1e9, 2)}
 
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
     ctx = enethip.Context(0)
-    for case in (case_cfg2, case_cfg5):
+    for case in (case_pcie, case_cfg2, case_cfg5):
         print(json.dumps(case(ctx, reps)), flush=True)
     ctx.close()
+    print(json.dumps(case_cfg2_multi(reps)), flush=True)
 
 
 if __name__ == "__main__":

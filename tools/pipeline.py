@@ -36,7 +36,7 @@ def main():
     import torch
     import oracle
     batches = bench.make_batches(a.config, a.rotate, 0)
-    eng = bench.GpuEngine(0, batches, a.lanes, 0)
+    eng = bench.GpuEngine(0, batches, a.lanes, 0, diag=True)
     eng.ctx.set_kernel_path(a.path)
     eng.ctx.diag_ablation(a.ablate)
     nbytes = batches[0].payload_bytes

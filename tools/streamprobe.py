@@ -98,7 +98,8 @@ def main():
         if what == "abl":
             combos = [(w, 17, a) for w in (2, 1) for a in (0, 4096, 2048 + 4096 + 32768)]
         for wgs, path, abl in combos:
-            ctx = enethip.Context(0, (8 if lanes == 4 else lanes) if (path == 13 and what == "list") else lanes, wgs)
+            ctx = enethip.Context(0, (8 if lanes == 4 else lanes) if (path == 13 and what == "list") else lanes, wgs,
+                                  diag=True)
             ctx.set_kernel_path(path)
             ctx.diag_ablation(abl)
             off = torch.arange(65536, dtype=torch.int64, device="cuda") * 1200
@@ -123,7 +124,7 @@ def main():
         lens = torch.full((n,), 1200, dtype=torch.int32, device="cuda")
         out = torch.zeros(n, dtype=torch.int32, device="cuda")
         for path, lanes, wgs in ((17, 4, 2), (17, 4, 1), (17, 8, 2), (13, 8, 0), (13, 4, 0), (14, 8, 0), (14, 4, 0)):
-            ctx = enethip.Context(0, lanes, wgs)
+            ctx = enethip.Context(0, lanes, wgs, diag=True)
             ctx.set_kernel_path(path)
 
             def fn(i, ctx=ctx):

@@ -1,55 +1,166 @@
 #!/usr/bin/env python3
-"""Measurement only: per-launch duration of back-to-back batch-list launches over a
-long serial run (HIP events between launches), to see whether the rate drops once
-the chip has streamed for a while (power / clock management).
-    python tools/sustain.py [launches=400] [list=5] [path=0]"""
+"""Sustained streaming rate of a kernel against time, with the GPU's clocks and
+power sampled beside it (VERDICT r2 "settle the sustained-rate gap with evidence").
+
+    python tools/sustain.py --kernel vring|probe [--launches N] [--list L]
+
+vring: N back-to-back enet_hip_crc32_batch_list_device launches of L resident
+cfg2-shaped batches (1200-B packets), the bench's default entry; probe: N launches
+of the read probe (enet_hip_read_probe_device: 16-B coalesced loads, every byte
+once, no compute) over the same L x 75 MiB of bytes.  Every launch is bracketed by
+HIP events on one stream (a spin kernel heads the queue, so the host never starves
+it).  A thread samples amdsmi's GPU metrics (current gfx / memory clocks, socket
+power, PPT and thermal residency counters, throttle status) as fast as the library
+answers.  Output: one JSON line per time bucket (1 ms buckets over the first 40 ms,
+then 20 ms) with the streaming rate and the metric samples that fall in it, then a
+summary line.
+"""
+import argparse
 import json
 import os
 import sys
+import threading
+import time
+
+import numpy as np
+import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "enet-csharp_amd"))
-
-import numpy as np  # noqa: E402
-import torch  # noqa: E402
-
 import enethip  # noqa: E402
 
 BATCH = 65536 * 1200
 
 
+class Sampler(threading.Thread):
+    """amdsmi GPU metrics, sampled in a loop; t = perf_counter seconds."""
+
+    FIELDS = ("current_gfxclk", "current_uclk", "current_socket_power", "average_socket_power",
+              "ppt_residency_acc", "socket_thm_residency_acc", "hbm_thm_residency_acc", "throttle_status",
+              "average_gfx_activity", "average_umc_activity", "firmware_timestamp")
+
+    def __init__(self):
+        super().__init__(daemon=True)
+        self.samples, self.stop, self.error = [], False, None
+        try:
+            import amdsmi
+            amdsmi.amdsmi_init()
+            self.amdsmi = amdsmi
+            self.h = amdsmi.amdsmi_get_processor_handles()[0]
+        except Exception as e:  # noqa: BLE001 -- report, keep timing
+            self.amdsmi, self.error = None, repr(e)
+
+    def run(self):
+        if self.amdsmi is None:
+            return
+        while not self.stop:
+            try:
+                m = self.amdsmi.amdsmi_get_gpu_metrics_info(self.h)
+            except Exception as e:  # noqa: BLE001
+                self.error = repr(e)
+                return
+            self.samples.append((time.perf_counter(), {k: m.get(k) for k in self.FIELDS}))
+
+
 def main():
-    launches = int(sys.argv[1]) if len(sys.argv) > 1 else 400
-    L = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-    path = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kernel", choices=["vring", "probe"], default="vring")
+    ap.add_argument("--launches", type=int, default=3000)
+    ap.add_argument("--list", type=int, default=5)
+    a = ap.parse_args()
     nb = 10
     big = torch.randint(0, 255, (nb * BATCH + 4096,), dtype=torch.uint8, device="cuda")
     off = torch.arange(65536, dtype=torch.int64, device="cuda") * 1200
     lens = torch.full((65536,), 1200, dtype=torch.int32, device="cuda")
     outs = [torch.zeros(65536, dtype=torch.int32, device="cuda") for _ in range(nb)]
     descs = [(big[j * BATCH:], off, lens, 65536, outs[j]) for j in range(nb)]
-    ctx = enethip.Context(0, 0, 2)
-    ctx.set_kernel_path(path)
+    sink = torch.zeros(4, dtype=torch.int32, device="cuda")
+    ctx = enethip.Context(0)
     st = torch.cuda.Stream()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(launches + 1)]
-    for i in range(5):
-        ctx.crc32_batch_list_device([descs[(i * L + t) % nb] for t in range(L)], st.cuda_stream)
-    torch.cuda.synchronize()
-    with torch.cuda.stream(st):
-        torch.cuda._sleep(int(4e8))
-        ev[0].record(st)
-        for i in range(launches):
+    L = a.list
+
+    def launch(i):
+        if a.kernel == "vring":
             ctx.crc32_batch_list_device([descs[(i * L + t) % nb] for t in range(L)], st.cuda_stream)
-            ev[i + 1].record(st)
+        else:
+            j = (i * L) % (nb - L + 1)
+            ctx.read_probe_device(big[j * BATCH:], L * BATCH, sink, st.cuda_stream)
+
+    for i in range(5):
+        launch(i)
     torch.cuda.synchronize()
-    us = np.array([ev[i].elapsed_time(ev[i + 1]) * 1e3 for i in range(launches)])
-    t = np.cumsum(us)
-    for k in range(0, launches, max(1, launches // 20)):
-        sl = us[k:k + max(1, launches // 20)]
-        print(json.dumps({"from_us": round(float(t[k] - us[k]), 1), "launches": len(sl),
-                          "us_per_launch": round(float(sl.mean()), 2),
-                          "TBps": round(L * BATCH / float(sl.mean()) / 1e6, 3)}), flush=True)
-    print(json.dumps({"total_us": round(float(t[-1]), 1), "mean_TBps": round(L * BATCH * launches / float(t[-1]) / 1e6, 3)}))
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(a.launches + 1)]
+    smp = Sampler()
+    smp.start()
+    time.sleep(0.05)
+    with torch.cuda.stream(st):
+        torch.cuda._sleep(int(2e9))                    # ~1 s of spin: every launch is queued before it ends
+        ev[0].record(st)
+        for i in range(a.launches):
+            launch(i)
+            ev[i + 1].record(st)
+    ev[0].synchronize()
+    t_gpu0 = time.perf_counter()                       # host time the GPU reached ev[0] (+ poll latency)
+    torch.cuda.synchronize()
+    t_end = time.perf_counter()
+    time.sleep(0.05)
+    smp.stop = True
+    smp.join()
+    ends = np.array([ev[0].elapsed_time(ev[i + 1]) for i in range(a.launches)])      # ms since ev[0]
+    starts = np.concatenate([[0.0], ends[:-1]])
+    nbytes = L * BATCH
+    edges = list(np.arange(0, 40, 1.0)) + list(np.arange(40, ends[-1] + 20, 20.0))
+    early = []                                          # 1-ms bucket rates over the first 40 ms
+    for lo, hi in zip(edges[:-1], edges[1:]):
+        sel = (starts >= lo) & (starts < hi)
+        if not sel.any():
+            continue
+        dur = (ends[sel] - starts[sel]).sum()
+        ss = [m for t, m in smp.samples if lo <= (t - t_gpu0) * 1e3 < hi]
+        row = {"t_ms": [round(lo, 1), round(hi, 1)], "launches": int(sel.sum()),
+               "TBps": round(nbytes * int(sel.sum()) / (dur * 1e-3) / 1e12, 3), "smi_samples": len(ss)}
+        if hi <= 40:
+            early.append(row["TBps"])
+        for k in ("current_gfxclk", "current_uclk", "current_socket_power"):
+            v = [m[k] for m in ss if isinstance(m.get(k), (int, float))]
+            if v:
+                row[k] = round(float(np.mean(v)), 1)
+        print(json.dumps(row))
+    idle = [m for t, m in smp.samples if t < t_gpu0 - 0.9]                 # during the spin / before
+    run = [m for t, m in smp.samples if t_gpu0 <= t <= t_end]
+    first, last = (run[0], run[-1]) if run else ({}, {})
+
+    def delta(k):
+        try:
+            return last[k] - first[k]
+        except Exception:  # noqa: BLE001
+            return None
+    print(json.dumps({"summary": a.kernel, "launches": a.launches, "bytes_per_launch": nbytes,
+                      "span_ms": round(float(ends[-1]), 2),
+                      "TBps_first_2ms": round(nbytes * int((starts < 2).sum()) /
+                                              (ends[starts < 2][-1] * 1e-3) / 1e12, 3),
+                      "TBps_whole": round(nbytes * a.launches / (ends[-1] * 1e-3) / 1e12, 3),
+                      "TBps_1ms_buckets_first_40ms": [min(early, default=None), max(early, default=None)],
+                      "smi_samples_run": len(run), "smi_error": smp.error,
+                      "ppt_residency_delta": delta("ppt_residency_acc"),
+                      "socket_thm_residency_delta": delta("socket_thm_residency_acc"),
+                      "hbm_thm_residency_delta": delta("hbm_thm_residency_acc"),
+                      "throttle_status_seen": sorted({str(m.get("throttle_status")) for m in run}),
+                      "gfxclk_run": [min((m["current_gfxclk"] for m in run if isinstance(m.get("current_gfxclk"), int)),
+                                         default=None),
+                                     max((m["current_gfxclk"] for m in run if isinstance(m.get("current_gfxclk"), int)),
+                                         default=None)],
+                      "uclk_run": [min((m["current_uclk"] for m in run if isinstance(m.get("current_uclk"), int)),
+                                       default=None),
+                                   max((m["current_uclk"] for m in run if isinstance(m.get("current_uclk"), int)),
+                                       default=None)],
+                      "power_run_W": [min((m["current_socket_power"] for m in run
+                                           if isinstance(m.get("current_socket_power"), int)), default=None),
+                                      max((m["current_socket_power"] for m in run
+                                           if isinstance(m.get("current_socket_power"), int)), default=None)],
+                      "gfxclk_idle": idle[-1].get("current_gfxclk") if idle else None,
+                      "power_idle_W": idle[-1].get("current_socket_power") if idle else None}))
+    ctx.close()
 
 
 if __name__ == "__main__":

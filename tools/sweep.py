@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--ablate", default="0", help="staged-kernel ablations to run: 0,1,2")
     a = ap.parse_args()
     batches = bench.make_batches(a.config, a.rotate, 0)
-    eng = bench.GpuEngine(0, batches, 0, 0)
+    eng = bench.GpuEngine(0, batches, 0, 0, diag=True)
     nbytes = batches[0].payload_bytes
     exp = None
     if a.check:

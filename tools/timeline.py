@@ -30,7 +30,7 @@ def main():
     a = ap.parse_args()
     import torch
     batches = bench.make_batches(a.config, 5, 0)
-    eng = bench.GpuEngine(0, batches, a.lanes, 0)
+    eng = bench.GpuEngine(0, batches, a.lanes, 0, diag=True)
     eng.ctx.set_kernel_path(a.path)
     eng.ctx.diag_ablation(a.ablate)
     nw = 256 * a.waves
