@@ -1186,8 +1186,35 @@ VrVariant vring_variant(const enet_hip_context* ctx, bool lists) {
     v.nt = ctx->path == kVringAltPath || ctx->path == kVringWalkAltPath;
     v.walk = (ctx->path == kVringWalkPath || ctx->path == kVringWalkAltPath) && !ctx->trace;
     v.in_order = ctx->path == kVringInOrderPath;
-    v.abl = lists ? ctx->vr_abl : 0;
+    v.abl = (lists || ctx->vr_abl == 128) ? ctx->vr_abl : 0;   // (128: the end-record trace instance)
     return v;
+}
+
+// Receive verify on the vring kernel (8 lanes per packet, VF instance): the default
+// (path 0) and the vring paths 17 / 21; the lean kernel serves 4 lanes, the binned
+// records and path 13.
+bool verify_on_vring(const enet_hip_context* ctx, int lg) {
+    return lg == 3 && ctx->ablation == 0 &&
+           (ctx->path == 0 || ctx->path == kVringPath || ctx->path == kVringInOrderPath);
+}
+
+int verify_vring_list(enet_hip_context* ctx, const ENetHipVerifyBatch* batches, size_t count, hipStream_t st) {
+    const KernelTables tb = tables_of(ctx);
+    VrVariant v;
+    v.in_order = ctx->path == kVringInOrderPath;
+    v.abl = ctx->vr_abl == 128 ? 128 : 0;
+    for (size_t b0 = 0; b0 < count; b0 += kVrMaxVBatches) {
+        VrVBatches bl{};
+        for (size_t b = b0; b < std::min(count, b0 + kVrMaxVBatches); ++b) {
+            const ENetHipVerifyBatch& e = batches[b];
+            bl.b[bl.count++] = VrVBatch{e.bytes, e.offsets, e.lengths, e.computed, static_cast<uint64_t>(e.count), 0u,
+                                        e.slotOffsets, e.connectIds, e.ok};
+        }
+        const int rc = vring_launch_vlist(ctx->num_cus * vring_wgs(ctx), v, st, bl, tb, ctx->d_basis2,
+                                          v.abl ? ctx->trace : nullptr);
+        if (rc) return rc;
+    }
+    return 0;
 }
 
 int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStream_t st) {
@@ -1263,7 +1290,11 @@ int enet_hip_context_create(int device, enet_hip_context** out) {
     const HostTables& ht = host_tables();
     int rc = 0;
     do {
-        if ((rc = herr(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)))) break;
+        // the stream a NULL `stream` argument selects: a BLOCKING stream, so work on it
+        // is ordered after work on the legacy null stream (hipStreamNonBlocking let a
+        // caller's fill of out[] on the null stream run concurrently with the kernel
+        // that writes it: the intermittent "unwritten" CRCs of tools/dbg/stress.py)
+        if ((rc = herr(hipStreamCreateWithFlags(&ctx->stream, hipStreamDefault)))) break;
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_image), ht.image.size() * 4)))) break;
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_xn), ht.xn.size() * 4)))) break;
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_init), ht.init.size() * 4)))) break;
@@ -1332,9 +1363,9 @@ int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgro
 
 #ifdef ENET_HIP_DIAG
 int enet_hip_diag_ablation(enet_hip_context* ctx, int mode) {
-    if (!ctx || mode < 0 || mode > 131071) return -static_cast<int>(hipErrorInvalidValue);
+    if (!ctx || mode < 0 || mode >= (1 << 19)) return -static_cast<int>(hipErrorInvalidValue);
     const int prio = (mode & 1024) ? 2 : (mode >> 3) & 1;    // 8: static / 1024: progress priority
-    ctx->vr_abl = (mode >> 11) & 63;                         // 2048 ... 65536: vring ablations
+    ctx->vr_abl = (mode >> 11) & 255;                        // 2048 ... 262144: vring ablations / end records
     mode &= 511;
     ctx->ablation = mode & ~8;
     ctx->ablation_prio = prio;
@@ -1482,7 +1513,12 @@ int enet_hip_verify_batch_device(enet_hip_context* ctx, const uint8_t* bytes, co
     pa.slot_off = slotOffsets;
     pa.connect = connectIds;
     pa.ok = ok;
-    return launch_packets(ctx, 1, pa, stream ? static_cast<hipStream_t>(stream) : ctx->stream);
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    if (verify_on_vring(ctx, static_cast<int>(pa.lg))) {
+        const ENetHipVerifyBatch b{bytes, offsets, lengths, slotOffsets, connectIds, count, ok, computed};
+        return verify_vring_list(ctx, &b, 1, st);
+    }
+    return launch_packets(ctx, 1, pa, st);
 }
 
 int enet_hip_verify_batch_list_device(enet_hip_context* ctx, const ENetHipVerifyBatch* batches, size_t batchCount,
@@ -1498,6 +1534,7 @@ int enet_hip_verify_batch_list_device(enet_hip_context* ctx, const ENetHipVerify
     ENH_CHECK(hipSetDevice(ctx->device));
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     const int lg = log2i(auto_lanes(ctx, 1));
+    if (verify_on_vring(ctx, lg)) return verify_vring_list(ctx, batches, batchCount, st);
     // the lean kernel's verify-list instance (geometry 0) on the paths where single
     // verify batches run the lean kernel (launch_packets, mode 1)
     if ((lg == 2 || lg == 3) && ctx->ablation == 0 && ctx->vr_abl == 0 &&

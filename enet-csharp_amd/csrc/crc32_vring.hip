@@ -120,14 +120,50 @@ __device__ __forceinline__ void vr_issue_meta(uint64_t addr, uint32_t base) {
                  :: "v"(addr), "s"(base) : "m0", "memory");
 }
 // the metadata of the lane's packet p (of kPk) once at most N younger loads are in
-// flight (BIN: and the record's caller index)
-template <int N, int BIN, uint32_t kPk>
-__device__ __forceinline__ void vr_wait_meta(uint32_t base, uint32_t p, uint32_t& L, uint64_t& off, uint32_t& idx) {
+// flight (BIN: and the record's caller index; VF: the slot offset and connectID)
+template <int N, int BIN, int VF, uint32_t kPk>
+__device__ __forceinline__ void vr_wait_meta(uint32_t base, uint32_t p, uint32_t& L, uint64_t& off, uint32_t& idx,
+                                             uint32_t& so, uint32_t& conn) {
     asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
     L = lds_load(base + 4u * p);
     off = static_cast<uint64_t>(lds_load(base + 4u * (kPk + p))) |
           (static_cast<uint64_t>(lds_load(base + 4u * (2u * kPk + p))) << 32);
     if constexpr (BIN) idx = lds_load(base + 4u * (3u * kPk + p));
+    if constexpr (VF) {
+        so = lds_load(base + 4u * (3u * kPk + p));
+        conn = lds_load(base + 4u * (4u * kPk + p));
+    }
+}
+
+// Receive verify (protocol.cs:1052-1068) in the lane folding the slot: the slot's
+// bytes [rel, rel + 4) of this block (block byte offsets, may lie partly outside)
+// are collected into `desired` (at their byte positions of the slot) and replaced
+// by connectID's.  A, B in lane order (swapped when hs), as vr_edge_mask.
+__device__ __forceinline__ void vr_slot_fix(u32x4& A, u32x4& B, uint32_t hs, int32_t rel, uint32_t conn,
+                                            uint32_t& desired) {
+    const bool sw = hs != 0;
+    const u32x4 h0 = sw ? B : A, h1 = sw ? A : B;
+    uint32_t v[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int d = rel - 4 * q;                       // the slot's start relative to dword q
+        if (d > -4 && d < 4) {
+            uint32_t M, C;
+            if (d >= 0) {
+                M = 0xFFFFFFFFu << (8 * d);
+                C = conn << (8 * d);
+                desired |= v[q] >> (8 * d);
+            } else {
+                M = 0xFFFFFFFFu >> (-8 * d);
+                C = conn >> (-8 * d);
+                desired |= (v[q] & M) << (-8 * d);
+            }
+            v[q] = (v[q] & ~M) | (C & M);
+        }
+    }
+    const u32x4 n0 = {v[0], v[1], v[2], v[3]}, n1 = {v[4], v[5], v[6], v[7]};
+    A = sw ? n1 : n0;
+    B = sw ? n0 : n1;
 }
 // every load retired (the wave's exit: no load may land after it has ended)
 __device__ __forceinline__ void vr_drain() {
@@ -310,7 +346,9 @@ struct VrIt {
 // may allocate v0-v47 only: amdgpu_num_vgpr(N) limits it to 2N VGPRs on gfx950
 // (the unified VGPR/AGPR file doubles the request), so the ring registers
 // v48-v63 are reserved -- never allocated, still counted in the kernel's VGPRs.
-// TR = 1: the diagnostics instance that writes the per-wave trace.
+// TR = 1: the diagnostics instance that writes the per-wave trace; TR = 2: only its
+// end record (slots taken, last slot, end time, HW_ID, groups), the product's code
+// path otherwise (diagnostics library, ablation 128).
 // ABL (diagnostics): bit 0 = no edge masking, bit 1 = no table lookups (the fold
 // XORs the prepared dwords) -- both wrong CRCs by design; bit 2 = each stage's
 // wait also retires the stage just issued (no load in flight during a fold); bit 3
@@ -319,11 +357,17 @@ struct VrIt {
 // BIN = 1: the batch's metadata are length-binned records (VrBatch::off points at
 // them, 4 dwords per packet), read in record order; packet r's CRC goes to
 // out[record r's index] (enet_hip_crc32_batch_device_binned).  One workgroup per CU.
-// ROT = 1: the tail-first stage order (below); 0 = stages in order (kernel path 17).
-template <int LG, int TR = 0, int NT = 0, int ABL = 0, int BIN = 0, int WK = 0, int ROT = 1>
+// ROT = 1: the tail-first stage order (below); 0 = stages in window order.
+// VF = 1: receive verify (protocol.cs:1052-1068) over a VrVBatches list, 8 lanes per
+// packet: the slot's lane substitutes connectID in registers (vr_slot_fix), and the
+// packet's lane 0 writes ok[] and computed[].
+template <int LG, int TR = 0, int NT = 0, int ABL = 0, int BIN = 0, int WK = 0, int ROT = 1, int VF = 0>
 __global__ void __launch_bounds__(64 * kVrW) __attribute__((amdgpu_waves_per_eu(8, 8), amdgpu_num_vgpr(24)))
-crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_t* trace) {
+crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, KernelTables tb, const uint32_t* basis,
+                   uint64_t* trace) {
     constexpr uint32_t P = 1u << LG, kPk = 64u >> LG;
+    // verify metadata: 5 fields x 8 packets in one 64-lane DMA
+    static_assert(!VF || (LG == 3 && !BIN), "receive verify: 8 lanes per packet, plain metadata");
     // Tail-first stage order.  A group of S > 1 stages runs its last stage first,
     // then stages 0 .. S-2.  Packed packets share a 128-byte line at every packet
     // boundary: packet j's last stage reads it, packet j+1's first stage too.  In
@@ -379,14 +423,21 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
     };
     uint32_t taken = 0;                                      // slots this wave has taken
     // the next slot: the first two static, later ones from the workgroup's counter
+    uint32_t last_slot = 0;                                  // (TR 2: the last slot taken)
     auto take = [&]() __attribute__((always_inline)) -> uint32_t {
         if (taken++ < 2u) return wave + kVrW * (taken - 1u);
+        // ds_add_rtn as inline asm: as a C++ atomic, hipcc put an s_waitcnt vmcnt(0)
+        // in front of it (an LDS atomic that may alias an LDS-DMA in flight), which
+        // drained the ring at every group switch.  The counter is no DMA's target.
         uint32_t sl = 0;
         if ((threadIdx.x & 63u) == 0u)
-            sl = __atomic_fetch_add(reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(
-                                        static_cast<uintptr_t>(BIN ? kVrCtrBin : kVrCtr)),
-                                    1u, __ATOMIC_RELAXED);
-        return __builtin_amdgcn_readfirstlane(sl);
+            asm volatile("v_mov_b32 %0, 1\n\t"
+                         "ds_add_rtn_u32 %0, %1, %0\n\t"
+                         "s_waitcnt lgkmcnt(0)"
+                         : "=&v"(sl) : "v"(BIN ? kVrCtrBin : kVrCtr) : "memory");
+        sl = __builtin_amdgcn_readfirstlane(sl);
+        if constexpr (TR == 2) last_slot = sl;
+        return sl;
     };
     auto advance = [&](VrIt& it) __attribute__((always_inline)) -> bool { return locate(it, slot_group(take())); };
     auto group_base = [&](const VrIt& it) __attribute__((always_inline)) -> uint64_t {   // its first packet
@@ -402,11 +453,15 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
     // (each mark is stored at once: held in registers, the marks cost SGPR spills)
     uint32_t ngroups = 0;
     auto mark = [&](int i) __attribute__((always_inline)) {
-        if (TR && (threadIdx.x & 63u) == 0u) trace[8u * wv + i] = __builtin_amdgcn_s_memrealtime();
+        if (TR == 1 && (threadIdx.x & 63u) == 0u) trace[8u * wv + i] = __builtin_amdgcn_s_memrealtime();
     };
     auto trace_end = [&]() __attribute__((always_inline)) {
         if (TR && (threadIdx.x & 63u) == 0u) {
             uint64_t* tr = trace + 8u * wv;
+            if (TR == 2) {
+                tr[0] = taken;
+                tr[1] = last_slot;
+            }
             tr[5] = __builtin_amdgcn_s_memrealtime();
             const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);      // HW_ID
             const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);    // XCC_ID
@@ -424,8 +479,9 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
     uint32_t mL = 0;                                         // metadata (read out at group switches)
     uint64_t moff = 0;
     uint32_t midx = 0;                                       // BIN: the record's caller index
+    uint32_t mso = 0, mconn = 0;                             // VF: slot offset, connectID
     auto load_meta = [&](const VrIt& it) __attribute__((always_inline)) {
-        const VrBatch& B = bl.b[it.b];
+        const auto& B = bl.b[it.b];
         // lane l loads field f = l / kPk of packet l % kPk (lanes past the fields: field
         // 0), the packet clamped to the batch's last (always a valid address; the
         // prologue of a wave with no group at all loads batch 0's last packet)
@@ -437,6 +493,12 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
         if constexpr (BIN) {
             f = f < 4u ? f : 0u;
             vr_issue_meta(reinterpret_cast<uint64_t>(B.off) + 16u * (base + q) + 4u * f, mbase);
+        } else if constexpr (VF) {
+            f = f < 5u ? f : 0u;
+            const uint64_t la = reinterpret_cast<uint64_t>(B.len + base) + 4u * q;
+            const uint64_t oa = reinterpret_cast<uint64_t>(B.off + base) + 8u * q + 4u * (f - 1u);
+            const uint64_t va = reinterpret_cast<uint64_t>(f == 3u ? B.slot_off + base : B.connect + base) + 4u * q;
+            vr_issue_meta(f == 0u ? la : f < 3u ? oa : va, mbase);
         } else {
             f = f < 3u ? f : 0u;
             const uint64_t la = reinterpret_cast<uint64_t>(B.len + base) + 4u * q;
@@ -445,7 +507,7 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
         }
     };
     load_meta(any ? pit : VrIt{0u, 0u});                     // (batch 0 exists: count >= 1)
-    vr_wait_meta<0, BIN, kPk>(mbase, lane_p(), mL, moff, midx);   // basis row and metadata have landed
+    vr_wait_meta<0, BIN, VF, kPk>(mbase, lane_p(), mL, moff, midx, mso, mconn);   // basis row and metadata landed
     mark(1);
 
     // ---- producer: window of the group it loads, one stage ahead of the consumer
@@ -457,9 +519,10 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
     auto plz = [&]() __attribute__((always_inline)) { return static_cast<uint32_t>(pwl) & (kAln - 1u); };
     uint32_t pst = 0, pstages = 0;
     uint32_t pidx = 0;                                       // BIN: the caller index of the lane's packet
+    uint32_t pps = ~0u, pconn = 0;                           // VF: the slot's window position (~0u: none), connectID
     bool pdone = !any;
     auto producer_enter = [&]() __attribute__((always_inline)) {   // group pit; metadata in mL / moff
-        const VrBatch& B = bl.b[pit.b];
+        const auto& B = bl.b[pit.b];
         if constexpr (BIN) pidx = midx;
         const uint64_t rem = B.n - group_base(pit);          // packets of the batch from the group's first
         const uint32_t L = lane_p() < rem ? mL : 0u;
@@ -468,6 +531,10 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
         const uint32_t z = L ? lz : 0u;                      // an empty packet: [0, 0)
         pwl = (a - lz) | z;
         pe = z + L;
+        if constexpr (VF) {                                  // a slot wholly inside the DGRAM, or none
+            pps = (L >= 4u && mso <= L - 4u) ? z + mso : ~0u;
+            pconn = mconn;
+        }
         const uint32_t nb = (pe + 31u) >> 5;
         pstages = max(1u, wave_max_u((nb + P - 1u) >> LG));
         pst = 0;
@@ -486,7 +553,7 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
                 // group qit's metadata was issued before the last produce's two stage
                 // loads (on this group's first stage, or at the prologue): retired
                 // once at most those two are in flight (stores do not count: older)
-                vr_wait_meta<2, BIN, kPk>(mbase, lane_p(), mL, moff, midx);
+                vr_wait_meta<2, BIN, VF, kPk>(mbase, lane_p(), mL, moff, midx, mso, mconn);
                 pit = qit;
                 qlive = advance(qit);
                 producer_enter();
@@ -562,6 +629,8 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
     // ---- consumer
     uint32_t reg = 0, clz = 0, ce = 0, cs = 0, cstages = 0, nedge = ~0u;
     uint32_t rt = 0;                                         // kRot: the last stage's fold
+    uint32_t cps = ~0u, cconn = 0, desired = 0;              // VF: slot position, connectID, the slot's bytes
+    uint8_t* cok = nullptr;                                  // VF: the keep mask of the group's packets
     uint32_t* cout = nullptr;                                // the CRCs of the group's packets (BIN: the batch's)
     uint32_t cidx = 0;                                       // BIN: the caller index of the lane's packet
     uint64_t crem = 0;                                       // packets of its batch from the group's first
@@ -575,6 +644,14 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
         t = step_of(t, cstages);
         h = h >= from ? h : ~0u;
         t = t >= from ? t : ~0u;
+        if constexpr (VF) {                                  // the slot's block(s)
+            const uint32_t s0 = cps >> 5, s1 = (cps + 3u) >> 5;
+            uint32_t a = (cps != ~0u && (s0 & (P - 1u)) == lane_k()) ? step_of(s0 >> LG, cstages) : ~0u;
+            uint32_t b = (cps != ~0u && s1 != s0 && (s1 & (P - 1u)) == lane_k()) ? step_of(s1 >> LG, cstages) : ~0u;
+            a = a >= from ? a : ~0u;
+            b = b >= from ? b : ~0u;
+            h = min(h, min(a, b));
+        }
         return wave_min_u(min(h, t));
     };
     // Entered right after the producer has entered the same group (the producer
@@ -583,13 +660,19 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
         clz = plz();
         ce = pe;
         const uint64_t base = group_base(pit);
-        cout = bl.b[pit.b].out + (BIN ? 0u : base);
+        cout = bl.b[pit.b].out ? bl.b[pit.b].out + (BIN ? 0u : base) : nullptr;
+        if constexpr (VF) {
+            cok = bl.b[pit.b].ok + base;
+            cps = pps;
+            cconn = pconn;
+            desired = 0;
+        }
         if constexpr (BIN) cidx = pidx;
         crem = bl.b[pit.b].n - base;
         const uint32_t nb = (ce + 31u) >> 5;                 // 0 for an empty packet ([0, 0))
         // the producer's count for this same group (no second wave reduction; the trace
         // instance keeps the reduction: without it, it spilled a VGPR)
-        if constexpr (TR) cstages = max(1u, wave_max_u((nb + P - 1u) >> LG));
+        if constexpr (TR == 1) cstages = max(1u, wave_max_u((nb + P - 1u) >> LG));
         else cstages = pstages;
         const uint32_t init = lds_load(init_addr(clz));
         reg = lane_k() == 0u ? (nb ? init : 0xFFFFFFFFu) : 0u;      // packet.cs:144 (empty packet: ~crc = 0)
@@ -601,7 +684,7 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
     bool done = false;
     auto iteration = [&](auto sc) __attribute__((always_inline)) {
         constexpr uint32_t S = decltype(sc)::value;
-        if constexpr (kVrLaneRecompute || BIN || kRot) lane = vr_lane();   // (BIN: its record register needs the room; kRot: rt)
+        if constexpr (kVrLaneRecompute || BIN || kRot || VF) lane = vr_lane();   // (the rt / record / slot registers need the room)
         produce(std::integral_constant<uint32_t, S ^ 1u>{}, std::integral_constant<int, static_cast<int>(S)>{});
         const uint32_t cst = stage_of(cs, cstages);          // the window stage this step folds
         const bool tail_first = kRot && cs == 0u && cstages > 1u;   // (wave-uniform)
@@ -613,6 +696,8 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
             const uint32_t q0 = 32u * (lane_k() + P * cst);              // windows < 2 GiB: differences fit int32
             if constexpr (!(ABL & 1))
                 vr_edge_mask(A, B, make_vr_sched(lane).hs, static_cast<int32_t>(clz - q0), static_cast<int32_t>(ce - q0));
+            if constexpr (VF)
+                if (cps != ~0u) vr_slot_fix(A, B, make_vr_sched(lane).hs, static_cast<int32_t>(cps - q0), cconn, desired);
             nedge = next_edge(cs + 1u);
             vr_shuffle(rin, lane, A, B, d);
         } else {
@@ -660,7 +745,16 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
             // by CINV[tz], which ran whenever any of the wave's packets had a ragged end
             if constexpr (!(ABL & 16))
                 if (lane_k() == 0u) reg = unstep_bytes(reg, tz);
-            if (lane_k() == 0u && lane_p() < crem) cout[BIN ? cidx : lane_p()] = finalize(reg);   // packet.cs:159
+            if constexpr (VF) {
+                desired = xor_lanes<0>(LG, desired);         // the slot's bytes, from at most two lanes
+                if (lane_k() == 0u && lane_p() < crem) {
+                    const uint32_t comp = cps != ~0u ? finalize(reg) : 0u;
+                    cok[lane_p()] = (cps != ~0u && comp == desired) ? 1 : 0;     // protocol.cs:1066-1068
+                    if (cout) cout[lane_p()] = comp;
+                }
+            } else if (lane_k() == 0u && lane_p() < crem) {
+                cout[BIN ? cidx : lane_p()] = finalize(reg);                     // packet.cs:159
+            }
             if (pdone) {
                 // no newer group entered: the wave is done.  The producer's last loads
                 // (zero lines past the end) are dead: retire them before the wave ends
@@ -686,9 +780,18 @@ crc32_vring_kernel(VrBatches bl, KernelTables tb, const uint32_t* basis, uint64_
 
 // ---------------------------------------------------------------- host side
 
-template <int LG, int TR = 0, int NT = 0, int ABL = 0, int BIN = 0, int WK = 0, int ROT = 1>
+template <int LG, int TR = 0, int NT = 0, int ABL = 0, int BIN = 0, int WK = 0, int ROT = 1, int VF = 0>
 const void* vring_fn() {
-    return reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT>);
+    return reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT, VF>);
+}
+// receive verify (8 lanes per packet): the product instance; diagnostics: in order, end records
+const void* vring_pick_v(bool trace, const VrVariant& v) {
+    if (!trace && !v.nt && !v.abl && !v.walk && !v.in_order) return vring_fn<3, 0, 0, 0, 0, 0, 1, 1>();
+#ifdef ENET_HIP_DIAG
+    if (!trace && !v.nt && !v.abl && !v.walk && v.in_order) return vring_fn<3, 0, 0, 0, 0, 0, 0, 1>();
+    if (trace && v.abl == 128 && !v.nt && !v.walk && !v.in_order) return vring_fn<3, 2, 0, 0, 0, 0, 1, 1>();
+#endif
+    return nullptr;
 }
 const void* vring_pick_bin(int lg) { return lg == 2 ? vring_fn<2, 0, 0, 0, 1>() : vring_fn<3, 0, 0, 0, 1>(); }
 
@@ -716,6 +819,7 @@ const void* vring_pick(int lg, bool trace, const VrVariant& v) {
                        : (nt ? vring_fn<3, 0, 1, 0, 0, 1>() : vring_fn<3, 0, 0, 0, 0, 1>());
     }
     if (trace) {
+        if (abl == 128 && !nt) return lg == 2 ? vring_fn<2, 2>() : vring_fn<3, 2>();   // end records only
         if (abl) return nullptr;
         return lg == 2 ? (nt ? vring_fn<2, 1, 1>() : vring_fn<2, 1>()) : (nt ? vring_fn<3, 1, 1>() : vring_fn<3, 1>());
     }
@@ -744,7 +848,15 @@ int vring_setup() {
         const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         return e == hipSuccess ? 0 : -static_cast<int>(e);
     };
-    static const int kAbl[] = {0, 1, 2, 3, 4, 6, 8, 19, 27, 32};
+    static const int kAbl[] = {0, 1, 2, 3, 4, 6, 8, 19, 27, 32, 128};
+    for (int t = 0; t < 2; ++t)
+        for (int w = 0; w < 2; ++w) {
+            VrVariant v;
+            v.in_order = w != 0;
+            v.abl = t ? 128 : 0;
+            const int rc = set(vring_pick_v(t != 0, v), kVrLds);
+            if (rc) return rc;
+        }
     for (int lg = 2; lg <= 3; ++lg) {
         int rc;
         if ((rc = set(vring_pick_bin(lg), kVrLdsBin))) return rc;
@@ -786,6 +898,28 @@ int vring_launch_list(int lg, int max_wgs, const VrVariant& v, hipStream_t st, c
         return -static_cast<int>(hipErrorInvalidValue);
     void* args[] = {&a, const_cast<KernelTables*>(&tb), const_cast<const uint32_t**>(&basis2), &trace};
     const hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(64 * kVrW), args, bin ? kVrLdsBin : kVrLds, st);
+    return e == hipSuccess ? 0 : -static_cast<int>(e);
+}
+
+int vring_launch_vlist(int max_wgs, const VrVariant& v, hipStream_t st, const VrVBatches& bl, const KernelTables& tb,
+                       const uint32_t* basis2, uint64_t* trace) {
+    if (bl.count > static_cast<uint32_t>(kVrMaxVBatches)) return -static_cast<int>(hipErrorInvalidValue);
+    const void* fn = vring_pick_v(trace != nullptr, v);
+    if (!fn) return -static_cast<int>(hipErrorInvalidValue);
+    VrVBatches a{};                                          // empty batches dropped
+    for (uint32_t b = 0; b < bl.count; ++b)
+        if (bl.b[b].n) a.b[a.count++] = bl.b[b];
+    if (a.count == 0) return 0;
+    for (uint32_t b = 0; b < a.count; ++b) {                 // the concatenated group space (8 packets a group)
+        a.b[b].g0 = a.groups;
+        a.groups += (a.b[b].n + 7u) / 8u;
+    }
+    const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(
+        1, std::min<uint64_t>((a.groups + kVrW - 1) / kVrW, static_cast<uint64_t>(max_wgs))));
+    if ((a.groups / (static_cast<uint64_t>(grid) * kVrW) + 2u) * kVrW > 0xFFFFFFF0ull)
+        return -static_cast<int>(hipErrorInvalidValue);
+    void* args[] = {&a, const_cast<KernelTables*>(&tb), const_cast<const uint32_t**>(&basis2), &trace};
+    const hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(64 * kVrW), args, kVrLds, st);
     return e == hipSuccess ? 0 : -static_cast<int>(e);
 }
 

@@ -35,6 +35,29 @@ struct VrBatches {
 };
 static_assert(sizeof(VrBatches) <= 3072, "kernel arguments");
 
+// One batch of a receive-verify list (c/protocol.cs:1052-1068 per DGRAM): the
+// checksum fields (out = computed[], may be null) plus each DGRAM's slot offset and
+// connectID and the keep mask ok[].
+struct VrVBatch {
+    const uint8_t* bytes;
+    const uint64_t* off;
+    const uint32_t* len;
+    uint32_t* out;
+    uint64_t n;
+    uint64_t g0;
+    const uint32_t* slot_off;
+    const uint32_t* connect;
+    uint8_t* ok;
+};
+constexpr int kVrMaxVBatches = 32;
+struct VrVBatches {
+    uint32_t count;
+    uint32_t pad;
+    uint64_t groups;
+    VrVBatch b[kVrMaxVBatches];
+};
+static_assert(sizeof(VrVBatches) <= 3072, "kernel arguments");
+
 // Kernel variants.  The product library builds the default alone (all fields at
 // their defaults); the diagnostics library (ENET_HIP_DIAG) also builds the sweep
 // variants: nt = nontemporal stage loads, abl = ablations (crc32_vring.hip; most
@@ -59,6 +82,13 @@ int vring_setup();
 // or -hipError_t (-hipErrorInvalidValue for a variant this library does not build).
 int vring_launch_list(int lg, int max_wgs, const VrVariant& v, hipStream_t st, const VrBatches& bl,
                       const KernelTables& tb, const uint32_t* basis2, uint64_t* trace, bool bin = false);
+
+// Receive verify over a list of batches (bl.count <= kVrMaxVBatches), 8 lanes per
+// packet (lg = 3): the slot is substituted by connectID in the registers of the lane
+// folding it, the CRC compared, ok[] and (if set) computed[] written.  Same
+// workgroups, LDS and variants as vring_launch_list (trace: end records only).
+int vring_launch_vlist(int max_wgs, const VrVariant& v, hipStream_t st, const VrVBatches& bl, const KernelTables& tb,
+                       const uint32_t* basis2, uint64_t* trace);
 
 // Launch the vring kernel over one batch: checksum mode, lanes per packet 2^lg
 // (lg = 2 or 3), at most max_wgs workgroups; pa.meta4 set = binned records.

@@ -97,8 +97,9 @@ ENET_HIP_API int enet_hip_is_diagnostics_build(void);
  * Packet i is bytes[offsets[i] .. offsets[i]+lengths[i]).  All pointers are
  * device pointers on ctx's device; out[i] receives what enet_crc32 would return
  * for that packet as a single ENetBuffer.  Inputs are read-only; `out` is
- * caller-allocated.  `stream` is a hipStream_t (NULL = ctx's stream).  Async:
- * returns after the launch. */
+ * caller-allocated.  `stream` is a hipStream_t (NULL = ctx's stream, a blocking
+ * stream: ordered after work on the legacy null stream, not after other non-blocking
+ * streams).  Async: returns after the launch. */
 ENET_HIP_API int enet_hip_crc32_batch_device(enet_hip_context* ctx, const uint8_t* bytes,
                                              const uint64_t* offsets, const uint32_t* lengths,
                                              size_t count, uint32_t* out, void* stream);

@@ -26,7 +26,7 @@ for diag, path in ((False, 0), (True, 19), (True, 21)):
             for name, (b, exp, d_p, d_o, d_l) in sets.items():
                 nbad, runs_bad = 0, 0
                 for r in range(reps):
-                    out = torch.full((b.n,), -1, dtype=torch.int32, device="cuda")
+                    out = torch.full((b.n,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")   # never-written sentinel
                     ctx.crc32_batch_device(d_p, d_o, d_l, b.n, out, torch.cuda.current_stream().cuda_stream)
                     torch.cuda.synchronize()
                     got = out.cpu().numpy().view(np.uint32)
@@ -37,7 +37,7 @@ for diag, path in ((False, 0), (True, 19), (True, 21)):
                         kpk = 64 // lanes
                         print(f"  BAD path {path} lanes {lanes} wgs {wgs} {name} rep {r}: {len(bad)} packets, "
                               f"idx {bad[:6].tolist()} groups {sorted(set((bad // kpk).tolist()))[:8]} "
-                              f"unset {(got[bad] == 0xFFFFFFFF).sum()}", flush=True)
+                              f"unwritten {(got[bad] == 0x5A5A5A5A).sum()} 0xFFFFFFFF {(got[bad] == 0xFFFFFFFF).sum()}", flush=True)
                 print(f"path {path} lanes {lanes} wgs {wgs} {name}: {runs_bad}/{reps} bad runs ({time.time()-t0:.0f}s)",
                       flush=True)
     ctx.close()

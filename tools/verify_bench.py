@@ -36,12 +36,14 @@ def main():
     ap.add_argument("--lanes", type=int, default=0)
     ap.add_argument("--rotate", type=int, default=5)
     ap.add_argument("--list", type=int, default=5)
+    ap.add_argument("--path", type=int, default=0, help="kernel path (13 = the lean kernel; 0 = vring at 8 lanes)")
     a = ap.parse_args()
     import torch
     import enethip
     from enethip import workloads
     import oracle as orc
     ctx = enethip.Context(0, a.lanes, 0)
+    ctx.set_kernel_path(a.path)
     st = torch.cuda.Stream()
     off = np.arange(N, dtype=np.uint64) * L
     lens = np.full(N, L, np.uint32)
@@ -111,7 +113,7 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / a.reps * 1e3
 
-    res = {"kind": "verify-bench", "list": a.list, "dgrams": N, "bytes_per_batch": N * L, "lanes": a.lanes or "default",
+    res = {"kind": "verify-bench", "path": a.path, "list": a.list, "dgrams": N, "bytes_per_batch": N * L, "lanes": a.lanes or "default",
            "bit_exact_vs_oracle": exact, "ok_count": int(exp_ok.sum())}
     fns = [("verify", verify, 1), ("checksum", checksum, 1)] + ([("verify_list", vlist, a.list)] if a.list else [])
     for name, fn, per in fns:
