@@ -71,7 +71,17 @@ struct KernelTables {
     const uint32_t* init;   // INIT[r], r < 32
     const uint8_t* zero;    // 256 zero bytes: DMA source of pieces wholly outside a packet
     const uint32_t* basis;  // kBasisDwords per image (lean kernel)
+    const uint32_t* tz;     // kTzTableDwords: the zero-byte multiplier tables (vring kernel)
 };
+
+// Zero-byte multipliers for a packet end's tz correction, reg x^(-8 tz): table k
+// (0: 16 zero bytes, 1: 8) byte b, entry v = (v << 8 b) x^(-8 (k ? 8 : 16)), at dword
+// 256 (4 k + b) + v.  reg x^(-128) = XOR of four lookups by reg's bytes.
+constexpr int kTzTables = 2;
+constexpr int kTzTableDwords = kTzTables * 4 * 256;        // 8 KiB
+__host__ __device__ constexpr uint32_t tz_addr(uint32_t k, uint32_t b, uint32_t v) {
+    return 4u * (256u * (4u * k + b) + v);
+}
 
 // ------------------------------------------------------------------ device helpers
 

@@ -905,11 +905,12 @@ constexpr int kImages = 4;                             // P = 1, 4, 8, 16
 constexpr int kImageP[kImages] = {1, 4, 8, 16};
 
 struct HostTables {
-    std::vector<uint32_t> image, xn, init, basis, basis2;
+    std::vector<uint32_t> image, xn, init, basis, basis2, tz;
     bool basis_ok = true;   // the bases rebuild every image dword the lean / vring kernels read
     HostTables()
         : image(static_cast<size_t>(kImages) * kImageDwords), xn(2 * kXnEntries), init(64),
-          basis(static_cast<size_t>(kImages) * kBasisDwords), basis2(static_cast<size_t>(kImages) * kVrBasisDwords) {
+          basis(static_cast<size_t>(kImages) * kBasisDwords), basis2(static_cast<size_t>(kImages) * kVrBasisDwords),
+          tz(kTzTableDwords) {
         init[0] = 0xFFFFFFFFu;
         for (int r = 1; r < 64; ++r) init[r] = unstep_zero(init[r - 1]);
         std::vector<uint32_t> cinv(kCinvEntries);
@@ -917,6 +918,10 @@ struct HostTables {
         for (int i = 0; i < 8; ++i) xinv8 = gf2_mulmod(xinv8, x_inverse());
         cinv[0] = kOneReflected;
         for (int i = 1; i < kCinvEntries; ++i) cinv[i] = gf2_mulmod(cinv[i - 1], xinv8);
+        for (uint32_t k = 0; k < static_cast<uint32_t>(kTzTables); ++k)       // x^(-128), x^(-64) by byte
+            for (uint32_t b = 0; b < 4; ++b)
+                for (uint32_t v = 0; v < 256; ++v)
+                    tz[tz_addr(k, b, v) / 4] = gf2_mulmod(v << (8 * b), cinv[k ? 8 : 16]);
         // image of P: dword 64j + 2t + (t>>4) = T_{t+32(P-1)}[j] (byte j followed by
         // t + 32(P-1) zero bytes); the free dwords hold INIT[] and CINV[]
         for (int im = 0; im < kImages; ++im) {
@@ -1012,7 +1017,8 @@ int log2i(int v) {
 }
 
 KernelTables tables_of(const enet_hip_context* ctx) {
-    return KernelTables{ctx->d_image, ctx->d_xn, ctx->d_xn + kXnEntries, ctx->d_init, ctx->d_zero, ctx->d_basis};
+    return KernelTables{ctx->d_image, ctx->d_xn, ctx->d_xn + kXnEntries, ctx->d_init, ctx->d_zero, ctx->d_basis,
+                        ctx->d_tz};
 }
 
 unsigned grid_for(const enet_hip_context* ctx, uint64_t tasks) {
@@ -1110,8 +1116,8 @@ constexpr int kVringPath = kLeanPath0 + kLeanGeoms;     // crc32_vring.hip (path
 constexpr int kVringAltPath = kVringPath + 1;           // the same with nontemporal stage loads
 constexpr int kVringWalkPath = kVringAltPath + 1;       // vring, workgroups walking contiguous group ranges
 constexpr int kVringWalkAltPath = kVringWalkPath + 1;   // the same with nontemporal stage loads
-constexpr int kVringInOrderPath = kVringWalkAltPath + 1;   // vring, stages in window order (not tail-first)
-constexpr int kMaxPath = kVringInOrderPath;
+constexpr int kVringTailFirstPath = kVringWalkAltPath + 1;   // vring, the tail-first stage order
+constexpr int kMaxPath = kVringTailFirstPath;
 
 // Paths this library builds: all in the diagnostics library; in the product one
 // the default (0), direct (1), stream geometry 0 (2), lean geometry 0 and vring.
@@ -1179,13 +1185,13 @@ int setup_stream() {
 // at two workgroups per CU against one).
 int vring_wgs(const enet_hip_context* ctx) { return ctx->wgs_per_cu == 1 ? 1 : 2; }
 bool vring_path(const enet_hip_context* ctx) {
-    return ctx->path == 0 || (ctx->path >= kVringPath && ctx->path <= kVringInOrderPath);
+    return ctx->path == 0 || (ctx->path >= kVringPath && ctx->path <= kVringTailFirstPath);
 }
 VrVariant vring_variant(const enet_hip_context* ctx, bool lists) {
     VrVariant v;
     v.nt = ctx->path == kVringAltPath || ctx->path == kVringWalkAltPath;
     v.walk = (ctx->path == kVringWalkPath || ctx->path == kVringWalkAltPath) && !ctx->trace;
-    v.in_order = ctx->path == kVringInOrderPath;
+    v.tail_first = ctx->path == kVringTailFirstPath;
     v.abl = (lists || ctx->vr_abl == 128) ? ctx->vr_abl : 0;   // (128: the end-record trace instance)
     return v;
 }
@@ -1195,13 +1201,13 @@ VrVariant vring_variant(const enet_hip_context* ctx, bool lists) {
 // records and path 13.
 bool verify_on_vring(const enet_hip_context* ctx, int lg) {
     return lg == 3 && ctx->ablation == 0 &&
-           (ctx->path == 0 || ctx->path == kVringPath || ctx->path == kVringInOrderPath);
+           (ctx->path == 0 || ctx->path == kVringPath || ctx->path == kVringTailFirstPath);
 }
 
 int verify_vring_list(enet_hip_context* ctx, const ENetHipVerifyBatch* batches, size_t count, hipStream_t st) {
     const KernelTables tb = tables_of(ctx);
     VrVariant v;
-    v.in_order = ctx->path == kVringInOrderPath;
+    v.tail_first = ctx->path == kVringTailFirstPath;
     v.abl = ctx->vr_abl == 128 ? 128 : 0;
     for (size_t b0 = 0; b0 < count; b0 += kVrMaxVBatches) {
         VrVBatches bl{};
@@ -1309,6 +1315,8 @@ int enet_hip_context_create(int device, enet_hip_context** out) {
         }
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_basis), ht.basis.size() * 4)))) break;
         if ((rc = herr(hipMemcpy(ctx->d_basis, ht.basis.data(), ht.basis.size() * 4, hipMemcpyHostToDevice)))) break;
+        if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_tz), ht.tz.size() * 4)))) break;
+        if ((rc = herr(hipMemcpy(ctx->d_tz, ht.tz.data(), ht.tz.size() * 4, hipMemcpyHostToDevice)))) break;
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_basis2), ht.basis2.size() * 4)))) break;
         if ((rc = herr(hipMemcpy(ctx->d_basis2, ht.basis2.data(), ht.basis2.size() * 4, hipMemcpyHostToDevice)))) break;
         if ((rc = vring_setup())) break;
@@ -1342,6 +1350,7 @@ int enet_hip_context_destroy(enet_hip_context* ctx) {
     (void)hipFree(ctx->d_zero);
     (void)hipFree(ctx->d_basis);
     (void)hipFree(ctx->d_basis2);
+    (void)hipFree(ctx->d_tz);
     pipeline_release(ctx);
     (void)hipFree(ctx->d_claim);
     (void)hipFree(ctx->d_frag_desc);

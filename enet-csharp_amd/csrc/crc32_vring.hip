@@ -51,7 +51,9 @@ constexpr uint32_t kVrStaging = kLdsTableBytes;                 // basis rows la
 constexpr uint32_t kVrMeta = kVrStaging + kVrBasisRows * 256;
 constexpr uint32_t kVrMetaWave = 256;
 constexpr uint32_t kVrCtr = kVrMeta + kVrW * kVrMetaWave;       // the workgroup's slot counter (16 B)
-constexpr int kVrLds = kVrCtr + 16;                              // 70.5 KiB: two workgroups per CU
+// the zero-byte multiplier tables (tz_addr, KernelTables::tz), DMA'd once per workgroup
+constexpr uint32_t kVrTz = kVrCtr + 16;
+constexpr int kVrLds = kVrTz + kTzTableDwords * 4;               // 78.5 KiB: two workgroups per CU
 static_assert(2 * kVrLds <= 160 * 1024, "two workgroups per CU");
 // length-binned records (BIN): the same area and layout
 constexpr uint32_t kVrMetaWaveBin = kVrMetaWave;
@@ -218,6 +220,50 @@ __device__ __forceinline__ VrSched make_vr_sched(uint32_t lane) {
     return s;
 }
 
+// reg x^(-8 z) for z = 16 (K = 0) or 8 (K = 1): four lookups in the zero-byte
+// multiplier tables at kVrTz (tz_addr), addresses by shift-and-add (asm: hipcc
+// would hoist the 4 table bases into VGPRs)
+template <int K>
+__device__ __forceinline__ uint32_t vr_tz_mul(uint32_t reg, uint32_t tzbase) {
+    uint32_t a0, a1, a2, a3;
+    const uint32_t b = tzbase + 4096u * K;
+    asm volatile("v_and_b32 %[a0], 0xff, %[r]\n\t"
+                 "v_bfe_u32 %[a1], %[r], 8, 8\n\t"
+                 "v_bfe_u32 %[a2], %[r], 16, 8\n\t"
+                 "v_lshrrev_b32 %[a3], 24, %[r]\n\t"
+                 "v_lshl_add_u32 %[a0], %[a0], 2, %[b0]\n\t"
+                 "v_lshl_add_u32 %[a1], %[a1], 2, %[b1]\n\t"
+                 "v_lshl_add_u32 %[a2], %[a2], 2, %[b2]\n\t"
+                 "v_lshl_add_u32 %[a3], %[a3], 2, %[b3]\n\t"
+                 "ds_read_b32 %[a0], %[a0]\n\t"
+                 "ds_read_b32 %[a1], %[a1]\n\t"
+                 "ds_read_b32 %[a2], %[a2]\n\t"
+                 "ds_read_b32 %[a3], %[a3]\n\t"
+                 "s_waitcnt lgkmcnt(0)\n\t"
+                 "v_bitop3_b32 %[r], %[a0], %[a1], %[a2] bitop3:0x96\n\t"
+                 "v_xor_b32 %[r], %[r], %[a3]"
+                 : [r] "+v"(reg), [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3)
+                 : [b0] "s"(b), [b1] "s"(b + 1024u), [b2] "s"(b + 2048u), [b3] "s"(b + 3072u)
+                 : "memory");
+    return reg;
+}
+
+// reg x^(-8 tz), tz < 32: the 16- and 8-byte parts by the tables, the rest by unsteps
+__device__ __forceinline__ uint32_t vr_unstep_tz(uint32_t reg, uint32_t tz, uint32_t tzbase) {
+    if (tz & 16u) reg = vr_tz_mul<0>(reg, tzbase);
+    if (tz & 8u) reg = vr_tz_mul<1>(reg, tzbase);
+    if (tz & 4u) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) reg = unstep_byte(reg);
+    }
+    if (tz & 2u) {
+        reg = unstep_byte(reg);
+        reg = unstep_byte(reg);
+    }
+    if (tz & 1u) reg = unstep_byte(reg);
+    return reg;
+}
+
 // mulmod (crc32_device.hpp) as a rolled loop: once per packet, so the few
 // cycles of loop overhead buy registers (the unrolled form set the kernel's peak)
 __device__ __forceinline__ uint32_t vr_mulmod(uint32_t a, uint32_t b) {
@@ -357,11 +403,12 @@ struct VrIt {
 // BIN = 1: the batch's metadata are length-binned records (VrBatch::off points at
 // them, 4 dwords per packet), read in record order; packet r's CRC goes to
 // out[record r's index] (enet_hip_crc32_batch_device_binned).  One workgroup per CU.
-// ROT = 1: the tail-first stage order (below); 0 = stages in window order.
+// ROT = 1: the tail-first stage order (below; diagnostics library); 0 = stages in
+// window order (the product).
 // VF = 1: receive verify (protocol.cs:1052-1068) over a VrVBatches list, 8 lanes per
 // packet: the slot's lane substitutes connectID in registers (vr_slot_fix), and the
 // packet's lane 0 writes ok[] and computed[].
-template <int LG, int TR = 0, int NT = 0, int ABL = 0, int BIN = 0, int WK = 0, int ROT = 1, int VF = 0>
+template <int LG, int TR = 0, int NT = 0, int ABL = 0, int BIN = 0, int WK = 0, int ROT = 0, int VF = 0>
 __global__ void __launch_bounds__(64 * kVrW) __attribute__((amdgpu_waves_per_eu(8, 8), amdgpu_num_vgpr(24)))
 crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, KernelTables tb, const uint32_t* basis,
                    uint64_t* trace) {
@@ -475,6 +522,8 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     if (wave < static_cast<uint32_t>(kVrBasisRows))
         dma4(basis + static_cast<size_t>(LG == 2 ? 1 : 2) * kVrBasisDwords + 64u * wave + lane,
              kVrStaging + 256u * wave);
+    // waves 0..7: one KiB each of the zero-byte multiplier tables
+    if (wave < static_cast<uint32_t>(kTzTableDwords / 256)) dma16(tb.tz + 256u * wave + 4u * lane, kVrTz + 1024u * wave);
     const uint32_t mbase = kVrMeta + (BIN ? kVrMetaWaveBin : kVrMetaWave) * wave;   // the wave's metadata area
     uint32_t mL = 0;                                         // metadata (read out at group switches)
     uint64_t moff = 0;
@@ -740,11 +789,12 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
             if constexpr (!(ABL & 16)) reg = o ? corr : reg;
             reg = xor_lanes<0>(LG, reg);
             const uint32_t tz = nb ? 32u * nb - ce : 0u;
-            // x^(-8 tz) as tz zero-byte unsteps, one LDS lookup each (the U column,
-            // unstep_bytes): about 6 VALU per byte against the 170 of a bit-serial multiply
-            // by CINV[tz], which ran whenever any of the wave's packets had a ragged end
+            // x^(-8 tz): 16 and 8 zero bytes by the multiplier tables (four lookups each,
+            // tz_mul), the rest (< 8) as zero-byte unsteps (the U column, unstep_byte, one
+            // lookup and about 6 VALU each).  All unsteps (round 2) cost 96 VALU for cfg2's
+            // tz = 16, run whenever any of the wave's packets had a ragged end.
             if constexpr (!(ABL & 16))
-                if (lane_k() == 0u) reg = unstep_bytes(reg, tz);
+                if (lane_k() == 0u) reg = vr_unstep_tz(reg, tz, kVrTz);
             if constexpr (VF) {
                 desired = xor_lanes<0>(LG, desired);         // the slot's bytes, from at most two lanes
                 if (lane_k() == 0u && lane_p() < crem) {
@@ -780,16 +830,16 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
 
 // ---------------------------------------------------------------- host side
 
-template <int LG, int TR = 0, int NT = 0, int ABL = 0, int BIN = 0, int WK = 0, int ROT = 1, int VF = 0>
+template <int LG, int TR = 0, int NT = 0, int ABL = 0, int BIN = 0, int WK = 0, int ROT = 0, int VF = 0>
 const void* vring_fn() {
     return reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT, VF>);
 }
-// receive verify (8 lanes per packet): the product instance; diagnostics: in order, end records
+// receive verify (8 lanes per packet): the product instance; diagnostics: tail first, end records
 const void* vring_pick_v(bool trace, const VrVariant& v) {
-    if (!trace && !v.nt && !v.abl && !v.walk && !v.in_order) return vring_fn<3, 0, 0, 0, 0, 0, 1, 1>();
+    if (!trace && !v.nt && !v.abl && !v.walk && !v.tail_first) return vring_fn<3, 0, 0, 0, 0, 0, 0, 1>();
 #ifdef ENET_HIP_DIAG
-    if (!trace && !v.nt && !v.abl && !v.walk && v.in_order) return vring_fn<3, 0, 0, 0, 0, 0, 0, 1>();
-    if (trace && v.abl == 128 && !v.nt && !v.walk && !v.in_order) return vring_fn<3, 2, 0, 0, 0, 0, 1, 1>();
+    if (!trace && !v.nt && !v.abl && !v.walk && v.tail_first) return vring_fn<3, 0, 0, 0, 0, 0, 1, 1>();
+    if (trace && v.abl == 128 && !v.nt && !v.walk && !v.tail_first) return vring_fn<3, 2, 0, 0, 0, 0, 0, 1>();
 #endif
     return nullptr;
 }
@@ -803,15 +853,15 @@ const void* vring_pick_bin(int lg) { return lg == 2 ? vring_fn<2, 0, 0, 0, 1>() 
 // record register was copied by hipcc between load and wait).
 const void* vring_pick(int lg, bool trace, const VrVariant& v) {
     if (lg != 2 && lg != 3) return nullptr;
-    const bool plain = !trace && !v.nt && !v.abl && !v.walk && !v.in_order;
+    const bool plain = !trace && !v.nt && !v.abl && !v.walk && !v.tail_first;
     if (plain) return lg == 2 ? vring_fn<2>() : vring_fn<3>();
 #ifdef ENET_HIP_DIAG
     const bool nt = v.nt;
     const int abl = v.abl;
-    if (v.in_order) {
+    if (v.tail_first) {
         if (trace || abl || v.walk) return nullptr;
-        return lg == 2 ? (nt ? vring_fn<2, 0, 1, 0, 0, 0, 0>() : vring_fn<2, 0, 0, 0, 0, 0, 0>())
-                       : (nt ? vring_fn<3, 0, 1, 0, 0, 0, 0>() : vring_fn<3, 0, 0, 0, 0, 0, 0>());
+        return lg == 2 ? (nt ? vring_fn<2, 0, 1, 0, 0, 0, 1>() : vring_fn<2, 0, 0, 0, 0, 0, 1>())
+                       : (nt ? vring_fn<3, 0, 1, 0, 0, 0, 1>() : vring_fn<3, 0, 0, 0, 0, 0, 1>());
     }
     if (v.walk) {
         if (trace || abl) return nullptr;
@@ -852,7 +902,7 @@ int vring_setup() {
     for (int t = 0; t < 2; ++t)
         for (int w = 0; w < 2; ++w) {
             VrVariant v;
-            v.in_order = w != 0;
+            v.tail_first = w != 0;
             v.abl = t ? 128 : 0;
             const int rc = set(vring_pick_v(t != 0, v), kVrLds);
             if (rc) return rc;
@@ -868,7 +918,7 @@ int vring_setup() {
                         v.nt = nt != 0;
                         v.abl = abl;
                         v.walk = (w & 1) != 0;
-                        v.in_order = (w & 2) != 0;
+                        v.tail_first = (w & 2) != 0;
                         if ((rc = set(vring_pick(lg, t != 0, v), kVrLds))) return rc;
                     }
     }

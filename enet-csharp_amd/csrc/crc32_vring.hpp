@@ -62,12 +62,12 @@ static_assert(sizeof(VrVBatches) <= 3072, "kernel arguments");
 // their defaults); the diagnostics library (ENET_HIP_DIAG) also builds the sweep
 // variants: nt = nontemporal stage loads, abl = ablations (crc32_vring.hip; most
 // give wrong CRCs by design), walk = each workgroup takes a contiguous range of the
-// launch's groups in order, in_order = stages in window order (not tail-first).
+// launch's groups in order, tail_first = the tail-first stage order (crc32_vring.hip).
 struct VrVariant {
     bool nt = false;
     int abl = 0;
     bool walk = false;
-    bool in_order = false;
+    bool tail_first = false;
 };
 
 // Set the dynamic-LDS attribute of every vring kernel instance built (once per context).

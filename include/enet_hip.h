@@ -86,8 +86,8 @@ ENET_HIP_API int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet
  * libenethip_diag.so only (-1 elsewhere): 2 + k = stream kernel geometry k
  * (k < 11), 13 + g = lean kernel geometry g (g < 4), 18 = vring with nontemporal
  * stage loads, 19 / 20 = vring with each workgroup walking a contiguous range of
- * groups (plain / nontemporal loads), 21 = vring with its stages in window order
- * (the schedule before the tail-first order). */
+ * groups (plain / nontemporal loads), 21 = vring with the tail-first stage order
+ * (each group's last stage first: less L2 refetch, more VALU; slower). */
 ENET_HIP_API int enet_hip_set_kernel_path(enet_hip_context* ctx, int path);
 
 /* 1 in libenethip_diag.so (built with -DENET_HIP_DIAG), 0 in libenethip.so. */

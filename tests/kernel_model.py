@@ -735,3 +735,24 @@ def unstep(reg: int, n: int, U=None) -> int:
     for _ in range(n):
         reg = ((reg << 8) & 0xFFFFFFFF) ^ U[reg >> 24]
     return reg
+
+
+# ---------------------------------------------------------------- tz multipliers
+def tz_tables() -> list[list[list[int]]]:
+    """crc32_vring.hip's zero-byte multiplier tables (HostTables::tz, tz_addr):
+    table k (0: 16 zero bytes, 1: 8), byte b, entry v = (v << 8b) x^(-8 (16 or 8))."""
+    return [[[mulmod(v << (8 * b), CINV[16 if k == 0 else 8]) for v in range(256)] for b in range(4)]
+            for k in range(2)]
+
+
+def vr_unstep_tz(reg: int, tz: int, tabs=None) -> int:
+    """vr_unstep_tz: reg x^(-8 tz), tz < 32 -- the 16- and 8-byte parts as four
+    table lookups each, the rest as zero-byte unsteps."""
+    tabs = tabs or tz_tables()
+    for k, z in ((0, 16), (1, 8)):
+        if tz & z:
+            reg = tabs[k][0][reg & 0xFF] ^ tabs[k][1][(reg >> 8) & 0xFF] ^ tabs[k][2][(reg >> 16) & 0xFF] ^ \
+                tabs[k][3][reg >> 24]
+    for _ in range(tz & 7):
+        reg = unstep_zero(reg)
+    return reg

@@ -552,7 +552,7 @@ def test_vring_many_groups(ctx, dctx, oracle_lib, path, wgs):
     tiny packets (one-stage groups, the producer switching group every stage, empty
     packets among them), long ones (many stages per group, the tail-first order's
     last stage far from the rest) and cfg2-shaped packed MTU packets, each against
-    the oracle.  18: nontemporal stage loads; 19, 20: walks; 21: stages in order."""
+    the oracle.  18: nontemporal stage loads; 19, 20: walks; 21: the tail-first stage order."""
     tiny = workloads.mixed(1_200_000, 0, 40, seed=177, len_seed=178)
     exp_t = oracle_lib.batch(tiny.payload, tiny.off, tiny.lens, threads=16)
     big = workloads.mixed(40_000, 2000, 9000, seed=179, len_seed=180)
@@ -611,7 +611,7 @@ def _run_list(ctx, cases):
 
 
 LIST_PATHS = (0, 13, 19, 20, 21)  # 0: the vring kernel (default), 13: the lean kernel's list instance,
-                                  # 19 / 20: vring with workgroups walking contiguous ranges, 21: in order
+                                  # 19 / 20: vring with workgroups walking contiguous ranges, 21: tail first
 
 
 @pytest.mark.parametrize("wgs", WGS)

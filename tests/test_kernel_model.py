@@ -315,3 +315,17 @@ def test_unstep_column_is_cinv():
         r, tz = rng.getrandbits(32), rng.randrange(32)
         assert km.unstep(r, tz, U) == km.mulmod(r, cinv[tz])
         assert km.unstep(km.zstep(r), 1, U) == r
+
+
+def test_tz_tables_equal_unsteps():
+    """The vring kernel's tz correction: four lookups in the x^(-128) / x^(-64)
+    multiplier tables plus < 8 unsteps equals tz zero-byte unsteps (= CINV[tz])."""
+    rng = random.Random(0x545A)
+    tabs = km.tz_tables()
+    for _ in range(300):
+        reg = rng.getrandbits(32)
+        tz = rng.randrange(32)
+        slow = reg
+        for _ in range(tz):
+            slow = km.unstep_zero(slow)
+        assert km.vr_unstep_tz(reg, tz, tabs) == slow == km.mulmod(reg, km.CINV[tz]), (hex(reg), tz)

@@ -10,4 +10,4 @@ grep -q " passed" $out/pytest.log || exit 1
 tools/gpu_step.sh 300 $out/verify_bench.log python -u tools/verify_bench.py || exit 1
 tools/gpu_step.sh 300 $out/verify_bench_list20.log python -u tools/verify_bench.py --list 20 || exit 1
 tools/gpu_step.sh 300 $out/verify_bench_lean.log python -u tools/verify_bench.py --path 13 || exit 1
-OUT=$out 
+OUT=$out bash tools/runs/r3f.sh || exit 1
