@@ -41,7 +41,8 @@ def parse(argv=None):
     ap.add_argument("--rotate", type=int, default=5, help="distinct resident batches cycled through")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per packet (0 = library default)")
     ap.add_argument("--wgs", type=int, default=0,
-                    help="workgroups per CU (enet_hip_set_tuning; 0 = the library default, 2 for the vring kernel)")
+                    help="workgroups per CU (enet_hip_set_tuning; 0 = the library default: "
+                         "2 for a multi-batch vring launch, 1 for a single batch)")
     ap.add_argument("--streams", type=int, default=6,
                     help="HIP streams the captured steps rotate over: batches are independent, so a "
                          "launch's prologue overlaps the previous launch's tail (1 = serial)")
@@ -485,7 +486,7 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
                 "entry": ("enet_hip_crc32_batch_device_binned" if args.binned else
                           "enet_hip_crc32_batch_list_device" if per_launch_steps > 1 else
                           "enet_hip_crc32_batch_device"),
-                "workgroups_per_cu": args.wgs or "default (2)",
+                "workgroups_per_cu": args.wgs or f"default ({2 if per_launch_steps > 1 else 1})",
                 "launch": args.launch,
                 "kernel_path": args.path,
             },

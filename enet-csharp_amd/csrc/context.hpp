@@ -35,6 +35,8 @@ struct enet_hip_context {
     uint8_t* h_pipe[2] = {nullptr, nullptr};    // per stream: pinned staging of the chunk's metadata
     size_t h_pipe_cap[2] = {0, 0};
     hipEvent_t pipe_ev[2] = {nullptr, nullptr}; // the staging of stream s has been copied
+    uint8_t* h_out = nullptr;                   // pinned landing zone of the D2H result copies
+    size_t h_out_cap = 0;
     uint8_t* d_ws = nullptr;                    // gather / binned workspace
     size_t d_ws_cap = 0;
     // fragment reassembly claim words (all ~0 between calls)

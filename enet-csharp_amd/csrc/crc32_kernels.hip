@@ -1181,9 +1181,13 @@ int setup_stream() {
 
 // vring workgroups per CU of one launch (enet_hip_set_tuning's workgroups_per_cu,
 // at most 2: the LDS and 64-VGPR budget of two 16-wave workgroups).  Default (0):
-// two, the configuration bench.py measures (profiles/r02e_*: the 5-batch lists
-// at two workgroups per CU against one).
-int vring_wgs(const enet_hip_context* ctx) { return ctx->wgs_per_cu == 1 ? 1 : 2; }
+// two for a launch of several batches, one for a single batch.  Measured on one box
+// (profiles/r03_wgs_ab/): 5-batch lists 5270-5360 GiB/s at two against 5153-5213 at
+// one; single-batch launches 5183 at one against 4301-4918 at two.
+int vring_wgs(const enet_hip_context* ctx, size_t batches) {
+    if (ctx->wgs_per_cu == 1 || ctx->wgs_per_cu == 2) return ctx->wgs_per_cu;
+    return batches > 1 ? 2 : 1;
+}
 bool vring_path(const enet_hip_context* ctx) {
     return ctx->path == 0 || (ctx->path >= kVringPath && ctx->path <= kVringTailFirstPath);
 }
@@ -1216,7 +1220,7 @@ int verify_vring_list(enet_hip_context* ctx, const ENetHipVerifyBatch* batches, 
             bl.b[bl.count++] = VrVBatch{e.bytes, e.offsets, e.lengths, e.computed, static_cast<uint64_t>(e.count), 0u,
                                         e.slotOffsets, e.connectIds, e.ok};
         }
-        const int rc = vring_launch_vlist(ctx->num_cus * vring_wgs(ctx), v, st, bl, tb, ctx->d_basis2,
+        const int rc = vring_launch_vlist(ctx->num_cus * vring_wgs(ctx, bl.count), v, st, bl, tb, ctx->d_basis2,
                                           v.abl ? ctx->trace : nullptr);
         if (rc) return rc;
     }
@@ -1234,7 +1238,7 @@ int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStr
     // profiles/r02d_cfg3_*; the vring records instance on path 17 / 18)
     if (mode == 0 && (pa.lg == 2 || pa.lg == 3) && ctx->ablation == 0 && vring_path(ctx) &&
         (!pa.meta4 || ctx->path != 0))
-        return vring_launch(pa.lg, ctx->num_cus * vring_wgs(ctx),
+        return vring_launch(pa.lg, ctx->num_cus * vring_wgs(ctx, 1),
                             pa.meta4 ? VrVariant{} : vring_variant(ctx, false), st, pa, tb, ctx->d_basis2);
     if (ctx->path != 1 && pa.lg >= 2 && pa.lg <= 4) {
         const bool lean_path = (ctx->path >= kLeanPath0 && ctx->path < kVringPath) || (ctx->path == 0 && ctx->ablation == 0);
@@ -1454,7 +1458,7 @@ int enet_hip_crc32_batch_list_device(enet_hip_context* ctx, const ENetHipBatch* 
             for (size_t b = b0; b < std::min(batchCount, b0 + kVrMaxBatches); ++b)
                 bl.b[bl.count++] = VrBatch{batches[b].bytes, batches[b].offsets, batches[b].lengths, batches[b].out,
                                            static_cast<uint64_t>(batches[b].count), 0u};
-            const int rc = vring_launch_list(lg, ctx->num_cus * vring_wgs(ctx), vring_variant(ctx, true), st, bl, tb,
+            const int rc = vring_launch_list(lg, ctx->num_cus * vring_wgs(ctx, bl.count), vring_variant(ctx, true), st, bl, tb,
                                              ctx->d_basis2, ctx->trace);
             if (rc) return rc;
         }

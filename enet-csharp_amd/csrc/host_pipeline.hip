@@ -54,6 +54,9 @@ void pipeline_release(enet_hip_context* ctx) {
     }
     (void)hipFree(ctx->d_ws);
     ctx->d_ws = nullptr;
+    (void)hipHostFree(ctx->h_out);
+    ctx->h_out = nullptr;
+    ctx->h_out_cap = 0;
 }
 
 namespace {
@@ -120,6 +123,11 @@ int enet_hip_crc32_batch_host(enet_hip_context* ctx, const uint8_t* bytes, size_
         if ((rc = ensure_device(&ctx->d_pipe[s], &ctx->d_pipe_cap[s], dbytes))) return rc;
         if ((rc = ensure_pinned(&ctx->h_pipe[s], &ctx->h_pipe_cap[s], hbytes))) return rc;
     }
+    // The CRCs land in pinned memory: a D2H into the caller's (pageable) array would be
+    // staged by the runtime, which holds the host thread until that chunk's kernel has
+    // run -- the next chunk's H2D would no longer overlap it.
+    if ((rc = ensure_pinned(&ctx->h_out, &ctx->h_out_cap, 4 * count))) return rc;
+    uint32_t* h_out = reinterpret_cast<uint32_t*>(ctx->h_out);
     for (size_t k = 0; k < plan.size(); ++k) {
         const Chunk& c = plan[k];
         const int s = static_cast<int>(k & 1u);
@@ -141,10 +149,11 @@ int enet_hip_crc32_batch_host(enet_hip_context* ctx, const uint8_t* bytes, size_
         ENH_CHECK(hipMemcpyAsync(d_len, h_len, 4 * n, hipMemcpyHostToDevice, st));
         ENH_CHECK(hipEventRecord(ctx->pipe_ev[s], st));
         if ((rc = enet_hip_crc32_batch_device(ctx, d_bytes, d_off, d_len, n, d_out, st))) return rc;
-        ENH_CHECK(hipMemcpyAsync(out + c.p0, d_out, 4 * n, hipMemcpyDeviceToHost, st));
+        ENH_CHECK(hipMemcpyAsync(h_out + c.p0, d_out, 4 * n, hipMemcpyDeviceToHost, st));
     }
     ENH_CHECK(hipStreamSynchronize(ctx->pipe[0]));
     ENH_CHECK(hipStreamSynchronize(ctx->pipe[1]));
+    memcpy(out, h_out, 4 * count);
     return 0;
 }
 
@@ -225,8 +234,10 @@ int enet_hip_crc32_gather_binned_host(enet_hip_context* ctx, const uint8_t* byte
     if ((rc = enet_hip_crc32_gather_binned_device(ctx, d, ns ? d_so : nullptr, ns ? d_sl : nullptr, ns, d_sf,
                                                   dgramCount, d_out, ctx->d_ws, ctx->d_ws_cap, s0)))
         return rc;
-    ENH_CHECK(hipMemcpyAsync(out, d_out, 4 * dgramCount, hipMemcpyDeviceToHost, s0));
+    if ((rc = ensure_pinned(&ctx->h_out, &ctx->h_out_cap, 4 * dgramCount))) return rc;
+    ENH_CHECK(hipMemcpyAsync(ctx->h_out, d_out, 4 * dgramCount, hipMemcpyDeviceToHost, s0));
     ENH_CHECK(hipStreamSynchronize(s0));
+    memcpy(out, ctx->h_out, 4 * dgramCount);
     return 0;
 }
 

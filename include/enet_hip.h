@@ -73,7 +73,8 @@ ENET_HIP_API const char* enet_hip_error_string(int code);
 /* Tuning knobs (0 = automatic).  lanes_per_packet: 1,2,4,...,64 lanes share one
  * packet (a power of two; default 8, and 4 for the length-binned entries);
  * workgroups_per_cu: resident workgroups per CU (the VGPR-ring kernel runs 1 or
- * 2, default 2; the direct / gather grids are sized for it). */
+ * 2; default 2 for a launch of several batches, 1 for a single batch; the direct /
+ * gather grids are sized for it). */
 ENET_HIP_API int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgroups_per_cu);
 
 /* Kernel path for the packet batch entry points (0 = default): checksum batches

@@ -92,7 +92,7 @@ def test_two_rank_gloo_harness():
     assert d["value"] == pytest.approx(2 * per_rank / (d["ms_per_step"] * 6e-3) / 2**30, rel=0.02)
     assert d["roofline"]["bound"] == "hbm" and d["roofline"]["peak"] == 8000.0
     assert d["cpu_baseline"]["cores"] == 2 and d["cpu_baseline"]["kind"] == "port"
-    assert d["config"]["workgroups_per_cu"] == "default (2)" and d["config"]["kernel_path"] == 0
+    assert d["config"]["workgroups_per_cu"] == ("default (2)" if d["config"]["steps_per_launch"] > 1 else "default (1)") and d["config"]["kernel_path"] == 0
 
 
 def test_cpu_baseline_uses_the_affinity_cores():
