@@ -357,12 +357,12 @@ def kernel_name(args, list_launch: bool = False) -> str:
     if path and path not in (17, 18, 21):
         return f"kernel path {path}"
     if args.binned:
-        return (f"crc32_vring_kernel<{lg}, 0, 0, 0, 1, 0, 1>" if path == 17
+        return (f"crc32_vring_kernel<{lg}, 0, 0, 0, 1, 0, 0, 0>" if path == 17
                 else f"crc32_lean_kernel<0, {lg}, 16, 2, 128>")
     if lg is None:
         return "crc32_stream_kernel / crc32_direct_kernel"
     nt, rot = (1 if path == 18 else 0), (1 if path == 21 else 0)
-    return f"crc32_vring_kernel<{lg}, 0, {nt}, 0, 0, 0, {rot}>"
+    return f"crc32_vring_kernel<{lg}, 0, {nt}, 0, 0, 0, {rot}, 0>"
 
 
 def load_traffic(cfg: str):

@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--lanes", type=int, default=0)
     ap.add_argument("--path", type=int, default=0, help="kernel path (enet_hip_set_kernel_path; 17 = vring records)")
+    ap.add_argument("--only", choices=["gather", "gather_binned"], help="time one entry only")
+    ap.add_argument("--probe", type=int, default=0, help="then run the read probe N times over the arena "
+                                                              "(FETCH_SIZE calibration)")
     a = ap.parse_args()
     import torch
     import enethip
@@ -56,6 +59,8 @@ def main():
     res = {"kind": "gather-bench", "dgrams": g.n, "segments": ns, "bytes": g.dgram_bytes,
            "lanes": a.lanes or "default"}
     for name, fn in (("gather", plain), ("gather_binned", binned)):
+        if a.only and name != a.only:
+            continue
         out.zero_()
         fn(0)
         torch.cuda.synchronize()
@@ -77,6 +82,12 @@ def main():
         res[name + "_GBps"] = round(g.dgram_bytes / us / 1e3, 1)
         res[name + "_GiBps"] = round(g.dgram_bytes / us * 1e6 / 2 ** 30, 1)
         res[name + "_bit_exact"] = ok
+    if a.probe:
+        sink = torch.zeros(4, dtype=torch.int32, device="cuda")
+        for _ in range(a.probe):
+            ctx.read_probe_device(d_p, (d_p.numel() // 16) * 16, sink, st.cuda_stream)
+        torch.cuda.synchronize()
+        res["probe_bytes"] = (d_p.numel() // 16) * 16
     print(json.dumps(res), flush=True)
     ctx.close()
 

@@ -27,11 +27,14 @@ def main():
     ap.add_argument("--probe", action="store_true", help="also run the read probe")
     ap.add_argument("--list", type=int, default=0, help="batches per launch (batch-list entry)")
     ap.add_argument("--wgs", type=int, default=0)
+    ap.add_argument("--binned", action="store_true", help="length-binned entry (one batch per launch)")
     a = ap.parse_args()
     batches = bench.make_batches(a.config, a.rotate, 0)
     diag = a.ablate != 0 or a.path not in bench.PRODUCT_PATHS   # sweep paths: libenethip_diag.so
     eng = bench.GpuEngine(0, batches, a.lanes, a.wgs, diag=diag)
-    if a.list:
+    if a.binned:
+        eng.set_binned(True)
+    elif a.list:
         eng.set_list(a.list)
     eng.ctx.set_kernel_path(a.path)
     if diag:
