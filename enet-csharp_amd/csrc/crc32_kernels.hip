@@ -40,6 +40,9 @@
 namespace enethip {
 
 constexpr int kThreads = 512;                     // direct / gather kernels: 8 waves
+// Gather segments of at most this many bytes are folded byte by byte by the join
+// (crc32_gather_join_kernel), not by the binned checksum pass
+constexpr uint32_t kGatherSmall = 64;
 
 template <int NT>
 __device__ __forceinline__ void fill_table(uint8_t* lds, const uint32_t* image) {
@@ -846,8 +849,17 @@ __global__ void __launch_bounds__(kThreads) crc32_gather_kernel(GatherArgs ga, K
 // reg(0xFFFFFFFF, B) ^ adv_|B|(0xFFFFFFFF), so one multiply per segment:
 // reg' = (reg ^ 0xFFFFFFFF) x^(8|B|) ^ reg(0xFFFFFFFF, B), from reg = 0xFFFFFFFF
 // (packet.cs:144-159 over the concatenated buffers, as enet_crc32 walks them).
+// Segments of at most `small` bytes (an ENet DGRAM's protocol header and command
+// headers: 4-8 and 4-48 B) had no checksum pass: the thread folds their bytes into
+// reg itself, byte by byte (packet.cs:150-155: the Sarwate step, T_0 = column 0 of
+// the P = 1 image, 1 KiB in LDS).
 __global__ void __launch_bounds__(kThreads) crc32_gather_join_kernel(GatherArgs ga, const uint32_t* seg_crc,
-                                                                     KernelTables tb) {
+                                                                     KernelTables tb, uint32_t small) {
+    __shared__ uint32_t t0[256];
+    if (small) {
+        for (uint32_t j = threadIdx.x; j < 256u; j += kThreads) t0[j] = tb.image[64u * j];
+        __syncthreads();
+    }
     const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
     for (uint64_t d = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; d < ga.n; d += stride) {
         // segFirst lives in device memory, so the host cannot check segFirst[n] ==
@@ -856,13 +868,16 @@ __global__ void __launch_bounds__(kThreads) crc32_gather_join_kernel(GatherArgs 
         const uint32_t s1 = static_cast<uint32_t>(min<uint64_t>(ga.seg_first[d + 1], ga.segs));
         const uint32_t s0 = min(ga.seg_first[d], s1);
         uint32_t reg = 0xFFFFFFFFu;
-        bool first = true;
         for (uint32_t q = s0; q < s1; ++q) {
             const uint32_t L = ga.seg_len[q];
             if (L == 0) continue;
-            const uint32_t r = ~bswap32(seg_crc[q]);
-            reg = (first ? 0u : mulmod(reg ^ 0xFFFFFFFFu, x8n_dev(L, tb))) ^ r;   // (first: reg ^ ~0 = 0)
-            first = false;
+            if (L <= small) {
+                const uint8_t* a = ga.bytes + ga.seg_off[q];
+                for (uint32_t i = 0; i < L; ++i) reg = t0[(reg ^ a[i]) & 0xFFu] ^ (reg >> 8);
+            } else {
+                const uint32_t r = ~bswap32(seg_crc[q]);
+                reg = (reg == 0xFFFFFFFFu ? 0u : mulmod(reg ^ 0xFFFFFFFFu, x8n_dev(L, tb))) ^ r;
+            }
         }
         ga.out[d] = finalize(reg);
     }
@@ -1616,7 +1631,8 @@ int enet_hip_crc32_gather_device(enet_hip_context* ctx, const uint8_t* bytes, co
 }
 
 size_t enet_hip_gather_binned_workspace_size(size_t segCount) {
-    return ((enet_hip_binned_workspace_size(segCount) + 15u) & ~static_cast<size_t>(15u)) + 4u * segCount;
+    // records | seg_crc[segCount] | the compacted records' count
+    return ((enet_hip_binned_workspace_size(segCount) + 15u) & ~static_cast<size_t>(15u)) + 4u * segCount + 16u;
 }
 
 int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* bytes, const uint64_t* segOffsets,
@@ -1633,14 +1649,33 @@ int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* by
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     const size_t bws = (enet_hip_binned_workspace_size(segCount) + 15u) & ~static_cast<size_t>(15u);
     uint32_t* seg_crc = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(workspace) + bws);
-    if (segCount) {                                        // every segment's CRC, mixed lengths: length-binned
+    uint32_t* count = seg_crc + segCount;                    // the compacted records' count
+    const int lanes = ctx->lanes_per_packet > 0 ? ctx->lanes_per_packet : 8;
+    // The default (vring paths, 4 or 8 lanes): segments of at most kGatherSmall bytes
+    // are folded by the join, the rest compacted into length-sorted records whose
+    // count stays on the device (VrBatches::n_dev) and checksummed by the vring's
+    // records instance.  Other paths: every segment through the binned entry.
+    const bool split = vring_path(ctx) && ctx->ablation == 0 && (lanes == 4 || lanes == 8);
+    if (segCount && split) {
+        const KernelTables tb = tables_of(ctx);
+        int rc;
+        if ((rc = length_bin_compact(segLengths, segOffsets, segCount, kGatherSmall, workspace, count, st))) return rc;
+        VrBatches bl{};
+        bl.count = 1;
+        bl.n_dev = count;
+        bl.b[0] = VrBatch{bytes, static_cast<const uint64_t*>(workspace), nullptr, seg_crc, segCount, 0u};
+        if ((rc = vring_launch_list(lanes == 4 ? 2 : 3, ctx->num_cus * vring_wgs(ctx, 1), VrVariant{}, st, bl, tb,
+                                    ctx->d_basis2, nullptr, true)))
+            return rc;
+    } else if (segCount) {                                   // every segment's CRC, mixed lengths: length-binned
         const int rc = enet_hip_crc32_batch_device_binned(ctx, bytes, segOffsets, segLengths, segCount, seg_crc,
                                                           workspace, bws, st);
         if (rc) return rc;
     }
     GatherArgs ga{bytes, segOffsets, segLengths, segFirst, dgramCount, out, segCount};
     const unsigned grid = grid_for(ctx, dgramCount);
-    hipLaunchKernelGGL(crc32_gather_join_kernel, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx));
+    hipLaunchKernelGGL(crc32_gather_join_kernel, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx),
+                       split ? kGatherSmall : 0u);
     return herr(hipGetLastError());
 }
 

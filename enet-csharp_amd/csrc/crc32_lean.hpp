@@ -79,5 +79,11 @@ int lean_launch_vlist(int lg, int num_cus, hipStream_t st, const ENetHipVerifyBa
 size_t length_bin_workspace(uint64_t n, bool verify);
 int length_bin(const uint32_t* len, const uint64_t* off, const uint32_t* slot_off, const uint32_t* connect, uint64_t n,
                uint32_t kpk, void* workspace, hipStream_t st);
+// The binned gather's records: the records {len, off_lo, off_hi, index} of the
+// segments longer than `small`, each tile's sorted longest first and appended at
+// a position taken from *count (zeroed here first, stream-ordered), so they fill
+// records[0, *count) -- a count only the device knows.  records: 16 n bytes.
+int length_bin_compact(const uint32_t* len, const uint64_t* off, uint64_t n, uint32_t small, void* records,
+                       uint32_t* count, hipStream_t st);
 
 }  // namespace enethip

@@ -198,6 +198,54 @@ __device__ __forceinline__ void vr_edge_mask(u32x4& A, u32x4& B, uint32_t hs, in
     B = sw ? n0 : n1;
 }
 
+// The same masking in place, on the landed slot registers themselves (the edge
+// path then folds them like any stage, vr_shuffle_slot): register R of the slot's
+// pair (A, B) holds block bytes [oR, oR + 16), oR = 0 or 16 by the lane's half swap
+// (hs16 = lane & 16: A holds [16, 32) when set).  Dword i of R keeps bytes j with
+// lo <= oR + 4i + j < hi.  Per dword and bound: s = clamp(4 (bound - oR) - 16 i, 0,
+// 16) and m = (~0 << s) << s (0 .. 32 bits without the 5-bit shift wrap), kept =
+// v & m (low bound) or v & ~m (high bound): four or five VALU.  Each bound is applied
+// only where some lane of the wave needs it (wave-uniform branches).
+#define VR_MASK_DWORD(REG, X, OFF, APPLY)                                                   \
+    "v_subrev_u32 %[t], " OFF ", " X "\n\t"                                                \
+    "v_med3_i32 %[t], %[t], 0, 16\n\t"                                                     \
+    "v_lshlrev_b32 %[m], %[t], -1\n\t"                                                     \
+    "v_lshlrev_b32 %[m], %[t], %[m]\n\t" APPLY(REG)
+#define VR_KEEP_LO(REG) "v_and_b32 " REG ", " REG ", %[m]\n\t"
+#define VR_DROP_HI(REG) "v_bfi_b32 " REG ", %[m], 0, " REG "\n\t"
+#define VR_MASK_REG(R0, R1, R2, R3, X, APPLY)                                                 \
+    "v_med3_i32 %[t], " X ", 0, 16\n\t"                                                        \
+    "v_lshlrev_b32 %[m], %[t], -1\n\t"                                                         \
+    "v_lshlrev_b32 %[m], %[t], %[m]\n\t" APPLY(R0)                                            \
+    VR_MASK_DWORD(R1, X, "16", APPLY) VR_MASK_DWORD(R2, X, "32", APPLY) VR_MASK_DWORD(R3, X, "48", APPLY)
+template <int SLOT>
+__device__ __forceinline__ void vr_edge_mask_slot(uint32_t hs16, int32_t lo, int32_t hi) {
+    const int32_t oa = static_cast<int32_t>(hs16), ob = 16 - oa;
+    uint32_t t, m;
+    if (__builtin_amdgcn_ballot_w64(lo > 0)) {
+        const int32_t xa = 4 * (lo - oa), xb = 4 * (lo - ob);
+        if constexpr (SLOT == 0)
+            asm volatile(VR_MASK_REG("v48", "v49", "v50", "v51", "%[xa]", VR_KEEP_LO)
+                         VR_MASK_REG("v52", "v53", "v54", "v55", "%[xb]", VR_KEEP_LO)
+                         : [t] "=&v"(t), [m] "=&v"(m) : [xa] "v"(xa), [xb] "v"(xb));
+        else
+            asm volatile(VR_MASK_REG("v56", "v57", "v58", "v59", "%[xa]", VR_KEEP_LO)
+                         VR_MASK_REG("v60", "v61", "v62", "v63", "%[xb]", VR_KEEP_LO)
+                         : [t] "=&v"(t), [m] "=&v"(m) : [xa] "v"(xa), [xb] "v"(xb));
+    }
+    if (__builtin_amdgcn_ballot_w64(hi < 32)) {
+        const int32_t ya = 4 * (hi - oa), yb = 4 * (hi - ob);
+        if constexpr (SLOT == 0)
+            asm volatile(VR_MASK_REG("v48", "v49", "v50", "v51", "%[ya]", VR_DROP_HI)
+                         VR_MASK_REG("v52", "v53", "v54", "v55", "%[yb]", VR_DROP_HI)
+                         : [t] "=&v"(t), [m] "=&v"(m) : [ya] "v"(ya), [yb] "v"(yb));
+        else
+            asm volatile(VR_MASK_REG("v56", "v57", "v58", "v59", "%[ya]", VR_DROP_HI)
+                         VR_MASK_REG("v60", "v61", "v62", "v63", "%[yb]", VR_DROP_HI)
+                         : [t] "=&v"(t), [m] "=&v"(m) : [ya] "v"(ya), [yb] "v"(yb));
+    }
+}
+
 // Lane constants of the fold (make_sched's, compressed).  The column byte of
 // table t is col_byte(t) = t << 3 | (t >> 4) << 2, GF(2)-linear in t, so the
 // column of step i = 4g + h for lane l, col_byte(31 ^ i ^ l5), is the
@@ -449,13 +497,23 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     auto lane_k = [&]() __attribute__((always_inline)) { return lane & (P - 1u); };   // block lane
     auto lane_p = [&]() __attribute__((always_inline)) { return lane >> LG; };         // packet of the group
     const uint64_t zero = reinterpret_cast<uint64_t>(tb.zero);
+    // batch b's packets and the launch's groups; BIN with a device-side count: the
+    // count the bin kernel wrote (the binned gather's compacted records)
+    uint64_t n0 = bl.b[0].n, ngroups_all = bl.groups;
+    if constexpr (BIN) {
+        if (bl.n_dev) {
+            n0 = min<uint64_t>(*bl.n_dev, n0);
+            ngroups_all = (n0 + kPk - 1u) / kPk;
+        }
+    }
+    auto batch_n = [&](uint32_t b) __attribute__((always_inline)) -> uint64_t { return BIN ? n0 : bl.b[b].n; };
 
     // ---- the wave's group sequence: slots of the workgroup (wave-uniform)
     // WK = 1 (walks): workgroup k owns the contiguous groups [k gw, (k + 1) gw) of the
     // concatenated space and takes them in order, so its waves walk one region of
     // the arena front to back (the access shape of tools/streamprobe.hip's chunk
     // and sub-stream probes) instead of a round of 16 groups every wt groups
-    const uint64_t gw = WK ? (bl.groups + gridDim.x - 1u) / gridDim.x : 0u;
+    const uint64_t gw = WK ? (ngroups_all + gridDim.x - 1u) / gridDim.x : 0u;
     auto slot_group = [&](uint32_t sl) __attribute__((always_inline)) -> uint64_t {
         if constexpr (WK) return sl < gw ? static_cast<uint64_t>(blockIdx.x) * gw + sl : ~0ull;
         return static_cast<uint64_t>(blockIdx.x) * kVrW + (sl & (kVrW - 1u)) + static_cast<uint64_t>(sl / kVrW) * wt;
@@ -463,7 +521,7 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     // `it` moved to global group gg (its batch found from it.b on: a wave's groups
     // ascend); false past the launch's last group
     auto locate = [&](VrIt& it, uint64_t gg) __attribute__((always_inline)) -> bool {
-        if (gg >= bl.groups) return false;
+        if (gg >= ngroups_all) return false;
         while (it.b + 1u < bl.count && gg >= bl.b[it.b + 1u].g0) ++it.b;
         it.g = gg;
         return true;
@@ -534,8 +592,9 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
         // lane l loads field f = l / kPk of packet l % kPk (lanes past the fields: field
         // 0), the packet clamped to the batch's last (always a valid address; the
         // prologue of a wave with no group at all loads batch 0's last packet)
-        const uint64_t base = min<uint64_t>(group_base(it), B.n - 1u);
-        const uint64_t left = B.n - 1u - base;               // (uniform: scalar select, no VALU)
+        const uint64_t bn = max<uint64_t>(batch_n(it.b), 1u);   // (a device count of 0: record 0, unused)
+        const uint64_t base = min<uint64_t>(group_base(it), bn - 1u);
+        const uint64_t left = bn - 1u - base;                // (uniform: scalar select, no VALU)
         const uint32_t l = vr_lane();                       // (recomputed: not a register held across the loop)
         uint32_t f = l / kPk;
         const uint32_t q = min(l & (kPk - 1u), left < 63u ? static_cast<uint32_t>(left) : 63u);
@@ -573,7 +632,7 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     auto producer_enter = [&]() __attribute__((always_inline)) {   // group pit; metadata in mL / moff
         const auto& B = bl.b[pit.b];
         if constexpr (BIN) pidx = midx;
-        const uint64_t rem = B.n - group_base(pit);          // packets of the batch from the group's first
+        const uint64_t rem = batch_n(pit.b) - group_base(pit);   // packets of the batch from the group's first
         const uint32_t L = lane_p() < rem ? mL : 0u;
         const uint64_t a = reinterpret_cast<uint64_t>(B.bytes) + moff;
         const uint32_t lz = static_cast<uint32_t>(a) & (kAln - 1u);
@@ -717,7 +776,7 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
             desired = 0;
         }
         if constexpr (BIN) cidx = pidx;
-        crem = bl.b[pit.b].n - base;
+        crem = batch_n(pit.b) - base;
         const uint32_t nb = (ce + 31u) >> 5;                 // 0 for an empty packet ([0, 0))
         // the producer's count for this same group (no second wave reduction; the trace
         // instance keeps the reduction: without it, it spilled a VGPR)
@@ -740,15 +799,21 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
         const uint32_t rin = tail_first ? 0u : reg;
         uint32_t d[8];
         if (cs == nedge) {                                   // head / tail pieces: keep [clz, ce) only
-            u32x4 A, B;
-            vr_read_stage<S>(A, B);
             const uint32_t q0 = 32u * (lane_k() + P * cst);              // windows < 2 GiB: differences fit int32
-            if constexpr (!(ABL & 1))
-                vr_edge_mask(A, B, make_vr_sched(lane).hs, static_cast<int32_t>(clz - q0), static_cast<int32_t>(ce - q0));
-            if constexpr (VF)
+            if constexpr (VF) {                              // (values: the slot fix-up works on copies)
+                u32x4 A, B;
+                vr_read_stage<S>(A, B);
+                if constexpr (!(ABL & 1))
+                    vr_edge_mask(A, B, make_vr_sched(lane).hs, static_cast<int32_t>(clz - q0), static_cast<int32_t>(ce - q0));
                 if (cps != ~0u) vr_slot_fix(A, B, make_vr_sched(lane).hs, static_cast<int32_t>(cps - q0), cconn, desired);
-            nedge = next_edge(cs + 1u);
-            vr_shuffle(rin, lane, A, B, d);
+                nedge = next_edge(cs + 1u);
+                vr_shuffle(rin, lane, A, B, d);
+            } else {                                         // masked in place, then folded as any stage
+                if constexpr (!(ABL & 1))
+                    vr_edge_mask_slot<S>(lane & 16u, static_cast<int32_t>(clz - q0), static_cast<int32_t>(ce - q0));
+                nedge = next_edge(cs + 1u);
+                vr_shuffle_slot<S>(rin, lane, d);
+            }
         } else {
             vr_shuffle_slot<S>(rin, lane, d);
         }
@@ -933,6 +998,8 @@ int vring_launch_list(int lg, int max_wgs, const VrVariant& v, hipStream_t st, c
     if (!fn) return -static_cast<int>(hipErrorInvalidValue);   // a variant this library does not build
     // empty batches dropped: the kernel may then read any batch's packet n - 1
     VrBatches a{};
+    if (bin && bl.n_dev && bl.count != 1) return -static_cast<int>(hipErrorInvalidValue);
+    a.n_dev = bin ? bl.n_dev : nullptr;
     for (uint32_t b = 0; b < bl.count; ++b)
         if (bl.b[b].n) a.b[a.count++] = bl.b[b];
     if (a.count == 0) return 0;

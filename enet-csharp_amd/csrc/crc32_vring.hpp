@@ -31,6 +31,9 @@ struct VrBatches {
     uint32_t count;
     uint32_t pad;
     uint64_t groups;    // all batches' groups (set by vring_launch_list)
+    // BIN only (one batch): batch 0's record count in device memory, at most b[0].n
+    // (the binned gather's compacted records: a count the host does not know), or null
+    const uint32_t* n_dev;
     VrBatch b[kVrMaxBatches];
 };
 static_assert(sizeof(VrBatches) <= 3072, "kernel arguments");

@@ -8,7 +8,8 @@ checked here on the gfx950 ISA hipcc emits with the Makefile's flags:
   * no instruction reads or overwrites a register while a load into it may be in
     flight, on any path of the control-flow graph (tools/isa_inflight_check.py);
   * no compiler instruction writes a ring register (v48-v63: the allocator limit
-    amdgpu_num_vgpr(24) is what keeps it out of them);
+    amdgpu_num_vgpr(24) is what keeps it out of them); only inline asm does (the
+    stage loads, and the edge path's masking of a landed slot);
   * at most 64 VGPRs: a launch runs one 16-wave workgroup per CU, and the next
     launch's workgroup (another stream) can share the CU as this one drains.
 Both builds are checked: the product library and the diagnostics one (-DENET_HIP_DIAG).
@@ -75,3 +76,15 @@ def test_ring_write_check_catches_a_compiler_write():
     assert chk.check(body, "k") == []
     bad = body[:-1] + ["v_mov_b32_e32 v52, 0", "s_endpgm"]
     assert any("writes ring" in e for e in chk.check(bad, "k"))
+
+
+def test_ring_write_check_asm_writes():
+    """An inline-asm write to a landed slot (the edge path's in-place masking) passes;
+    the same write while the slot's load may still be in flight is flagged."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import isa_inflight_check as chk
+    load = [";;#ASMSTART", "global_load_dwordx4 v[48:51], v[0:1], off", ";;#ASMEND"]
+    mask = [";;#ASMSTART", "v_and_b32 v48, v48, v2", ";;#ASMEND"]
+    assert chk.check(load + ["s_waitcnt vmcnt(0)"] + mask + ["s_endpgm"], "k") == []
+    errs = chk.check(load + mask + ["s_waitcnt vmcnt(0)", "s_endpgm"], "k")
+    assert any("may be in flight" in e for e in errs)

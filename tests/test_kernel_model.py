@@ -329,3 +329,40 @@ def test_tz_tables_equal_unsteps():
         for _ in range(tz):
             slow = km.unstep_zero(slow)
         assert km.vr_unstep_tz(reg, tz, tabs) == slow == km.mulmod(reg, km.CINV[tz]), (hex(reg), tz)
+
+
+def _edge_mask_slot(regs, hs16, lo, hi):
+    """crc32_vring.hip vr_edge_mask_slot on one lane: register R of (A, B) holds block
+    bytes [oR, oR + 16), oA = hs16, oB = 16 - hs16; per dword i and bound b,
+    s = clamp(4 (b - oR) - 16 i, 0, 16), m = (~0 << s) << s; v &= m (low bound),
+    v &= ~m (high bound)."""
+    out = []
+    for r, o in zip(regs, (hs16, 16 - hs16)):
+        vals = []
+        for i, v in enumerate(r):
+            s = min(max(4 * (lo - o) - 16 * i, 0), 16)
+            v &= ((0xFFFFFFFF << s) << s) & 0xFFFFFFFF
+            t = min(max(4 * (hi - o) - 16 * i, 0), 16)
+            v &= ~((0xFFFFFFFF << t) << t) & 0xFFFFFFFF
+            vals.append(v)
+        out.append(vals)
+    return out
+
+
+def test_vring_edge_mask_slot_keeps_exactly_the_window():
+    import numpy as np
+    """The in-place edge mask keeps exactly the block bytes in [lo, hi), for both
+    half-swap orders and bounds inside and outside the 32-byte block."""
+    rng = np.random.default_rng(5)
+    block = rng.integers(1, 256, 32, dtype=np.uint8)          # no zero bytes: a kept byte stays nonzero
+    for hs16 in (0, 16):
+        a = block[hs16:hs16 + 16].view("<u4").tolist()           # register A: bytes [hs16, hs16 + 16)
+        b = block[16 - hs16:32 - hs16].view("<u4").tolist()
+        for lo in range(-6, 40):
+            for hi in range(lo, 42):
+                ma, mb = _edge_mask_slot([a, b], hs16, lo, hi)
+                got = np.zeros(32, np.uint8)
+                got[hs16:hs16 + 16] = np.array(ma, "<u4").view(np.uint8)
+                got[16 - hs16:32 - hs16] = np.array(mb, "<u4").view(np.uint8)
+                keep = (np.arange(32) >= lo) & (np.arange(32) < hi)
+                assert (got == np.where(keep, block, 0)).all(), (hs16, lo, hi)
