@@ -57,6 +57,9 @@ def parse(argv=None):
     ap.add_argument("--path", type=int, default=0,
                     help="kernel path (enet_hip_set_kernel_path; 0 = the library default -- tuning sweeps only; "
                          "a path the product library does not build runs on libenethip_diag.so)")
+    ap.add_argument("--ablate", type=int, default=0,
+                    help="diagnostics library: enet_hip_diag_ablation value, set after the oracle gate "
+                         "(WRONG CRCs by design: a measurement of the kernel's parts, never a result)")
     ap.add_argument("--binned", action="store_true",
                     help="length-binned entry (enet_hip_crc32_batch_device_binned): for mixed lengths (cfg3)")
     ap.add_argument("--launch", default="graph", choices=["graph", "direct"],
@@ -357,7 +360,7 @@ def kernel_name(args, list_launch: bool = False) -> str:
     if path and path not in (17, 18, 21):
         return f"kernel path {path}"
     if args.binned:
-        return (f"crc32_vring_kernel<{lg}, 0, 0, 0, 1, 0, 0, 0>" if path == 17
+        return (f"crc32_vring_kernel<{lg}, 0, 0, 0, 1, 0, 0, 0>" if path in (0, 17)
                 else f"crc32_lean_kernel<0, {lg}, 16, 2, 128>")
     if lg is None:
         return "crc32_stream_kernel / crc32_direct_kernel"
@@ -381,7 +384,7 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
         args.gpus = ws
     dist = dist_init(ws)
     batches = make_batches(args.config, args.rotate, rank, ws)
-    diag = args.path not in PRODUCT_PATHS
+    diag = args.path not in PRODUCT_PATHS or args.ablate != 0
     eng = (engine_factory or GpuEngine)(local, batches, args.lanes, args.wgs, *((diag,) if diag else ()))
     if hasattr(eng, "set_streams"):
         eng.set_streams(args.streams)
@@ -403,6 +406,8 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
     if not (eng.outputs(0) == exp).all():
         raise SystemExit("bench.py: GPU CRCs differ from the oracle -- refusing to report a number")
 
+    if args.ablate:                       # (diagnostics: from here on the CRCs are wrong by design)
+        eng.ctx.diag_ablation(args.ablate)
     for first, count in (eng.launch_plan(args.warmup) if hasattr(eng, "launch_plan") else
                          [(i, 1) for i in range(args.warmup)]):
         eng.launch(first, count) if hasattr(eng, "launch") else eng.step(first)
@@ -413,7 +418,7 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
         eng.replay()
         eng.sync()
         lib = oracle.OracleLib()
-        for j in range(min(args.steps, len(batches))):
+        for j in range(0 if args.ablate else min(args.steps, len(batches))):
             ref = lib.batch(batches[j].payload, batches[j].off, batches[j].lens, threads=8)
             if not (eng.outputs(j) == ref).all():
                 raise SystemExit(f"bench.py: graph replay CRCs of batch {j} differ from the oracle")
@@ -489,6 +494,7 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
                 "workgroups_per_cu": args.wgs or f"default ({2 if per_launch_steps > 1 else 1})",
                 "launch": args.launch,
                 "kernel_path": args.path,
+                **({"ablation": args.ablate, "note": "ABLATION: wrong CRCs by design"} if args.ablate else {}),
             },
             "hbm_read_frac": round(value * GIB / 1e9 / (HBM_PEAK_GBPS * ws), 4),
             "roofline": {

@@ -1248,11 +1248,11 @@ int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStr
     const_cast<PacketArgs&>(pa).trace = ctx->trace;
     const_cast<PacketArgs&>(pa).prio = static_cast<uint32_t>(ctx->ablation_prio);
     // the stream kernel takes 4, 8 or 16 lanes per packet; anything else runs direct
-    // default (path 0) checksum batches at 4 or 8 lanes: the VGPR-ring kernel
-    // (length-binned records: the lean kernel by default, 60 vs 66 us on cfg3 at 4 lanes,
-    // profiles/r02d_cfg3_*; the vring records instance on path 17 / 18)
-    if (mode == 0 && (pa.lg == 2 || pa.lg == 3) && ctx->ablation == 0 && vring_path(ctx) &&
-        (!pa.meta4 || ctx->path != 0))
+    // default (path 0) checksum batches at 4 or 8 lanes: the VGPR-ring kernel, also for
+    // length-binned records (its records instance: cfg3 at 4 lanes 59.4 us against the
+    // lean kernel's 63.3 since the in-place edge masks, profiles/r03_cfg3_binned/;
+    // the lean kernel on paths 13-16)
+    if (mode == 0 && (pa.lg == 2 || pa.lg == 3) && ctx->ablation == 0 && vring_path(ctx))
         return vring_launch(pa.lg, ctx->num_cus * vring_wgs(ctx, 1),
                             pa.meta4 ? VrVariant{} : vring_variant(ctx, false), st, pa, tb, ctx->d_basis2);
     if (ctx->path != 1 && pa.lg >= 2 && pa.lg <= 4) {

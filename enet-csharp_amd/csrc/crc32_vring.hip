@@ -910,10 +910,10 @@ const void* vring_pick_v(bool trace, const VrVariant& v) {
 }
 const void* vring_pick_bin(int lg) { return lg == 2 ? vring_fn<2, 0, 0, 0, 1>() : vring_fn<3, 0, 0, 0, 1>(); }
 
-// The product instances: 64 VGPRs (WPE 8), one or two workgroups per CU, tail-first
-// stage order.  The diagnostics library (ENET_HIP_DIAG) adds the sweep variants: a
-// trace buffer (per-wave timestamps), nt stage loads, workgroup walks, the in-order
-// stage schedule and the ablations (wrong CRCs by design).  Null = not built here.
+// The product instances: 64 VGPRs (WPE 8), one or two workgroups per CU, stages in
+// window order.  The diagnostics library (ENET_HIP_DIAG) adds the sweep variants: a
+// trace buffer (per-wave timestamps), nt stage loads, workgroup walks, the tail-first
+// stage order and the ablations (wrong CRCs by design).  Null = not built here.
 // Measured and not kept: 3 and 4 ring slots and a binned-records variant (its
 // record register was copied by hipcc between load and wait).
 const void* vring_pick(int lg, bool trace, const VrVariant& v) {
@@ -924,6 +924,7 @@ const void* vring_pick(int lg, bool trace, const VrVariant& v) {
     const bool nt = v.nt;
     const int abl = v.abl;
     if (v.tail_first) {
+        if (abl == 2 && lg == 3 && !trace && !nt && !v.walk) return vring_fn<3, 0, 0, 2, 0, 0, 1>();   // no lookups
         if (trace || abl || v.walk) return nullptr;
         return lg == 2 ? (nt ? vring_fn<2, 0, 1, 0, 0, 0, 1>() : vring_fn<2, 0, 0, 0, 0, 0, 1>())
                        : (nt ? vring_fn<3, 0, 1, 0, 0, 0, 1>() : vring_fn<3, 0, 0, 0, 0, 0, 1>());
@@ -942,6 +943,7 @@ const void* vring_pick(int lg, bool trace, const VrVariant& v) {
     if (abl == 8 && lg == 3) return nt ? vring_fn<3, 0, 1, 8>() : vring_fn<3, 0, 0, 8>();
     if (abl == 27 && lg == 3) return nt ? vring_fn<3, 0, 1, 27>() : vring_fn<3, 0, 0, 27>();
     if (abl == 19 && !nt) return lg == 2 ? vring_fn<2, 0, 0, 19>() : vring_fn<3, 0, 0, 19>();
+    if (abl == 2 && lg == 3 && !nt) return vring_fn<3, 0, 0, 2>();
     if (abl == 32 && lg == 2) return nt ? vring_fn<2, 0, 3>() : vring_fn<2, 0, 2>();   // sc1 / sc0 sc1
     if (lg == 2 && !nt) {
         switch (abl) {
