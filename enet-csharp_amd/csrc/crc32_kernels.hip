@@ -850,14 +850,41 @@ __global__ void __launch_bounds__(kThreads) crc32_gather_kernel(GatherArgs ga, K
 // reg' = (reg ^ 0xFFFFFFFF) x^(8|B|) ^ reg(0xFFFFFFFF, B), from reg = 0xFFFFFFFF
 // (packet.cs:144-159 over the concatenated buffers, as enet_crc32 walks them).
 // Segments of at most `small` bytes (an ENet DGRAM's protocol header and command
-// headers: 4-8 and 4-48 B) had no checksum pass: the thread folds their bytes into
-// reg itself, byte by byte (packet.cs:150-155: the Sarwate step, T_0 = column 0 of
-// the P = 1 image, 1 KiB in LDS).
+// headers: 4-8 and 4-48 B) had no checksum pass: the thread folds them into reg
+// itself (packet.cs:150-155).  All of the segment's aligned dwords are loaded first
+// (<= 17 independent loads, never past the dword holding its last byte), then each
+// 4 bytes are one slicing-by-4 step on the dword v_alignbyte cuts at the segment's
+// offset, the last L mod 4 bytes Sarwate steps (T_3 .. T_0 = columns 6, 4, 2, 0 of
+// the P = 1 image, 4 KiB in LDS).
+__device__ __forceinline__ uint32_t fold_small(uint32_t reg, const uint8_t* a, uint32_t L, const uint32_t (*t4)[256]) {
+    constexpr int kMaxDwords = 17;                           // (3 + 64 + 3) / 4
+    const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a)) & 3u;
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(a) & ~static_cast<uintptr_t>(3));
+    const uint32_t nd = (sh + L + 3u) >> 2, nf = L >> 2;
+    uint32_t d[kMaxDwords + 1];
+#pragma unroll
+    for (int k = 0; k < kMaxDwords; ++k) d[k] = static_cast<uint32_t>(k) < nd ? w[k] : 0u;
+    d[kMaxDwords] = 0u;
+#pragma unroll
+    for (int i = 0; i < kMaxDwords - 1; ++i) {
+        if (static_cast<uint32_t>(i) < nf) {
+            const uint32_t x = reg ^ __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+            reg = t4[3][x & 0xFFu] ^ t4[2][(x >> 8) & 0xFFu] ^ t4[1][(x >> 16) & 0xFFu] ^ t4[0][x >> 24];
+        }
+    }
+    uint32_t tail = 0;
+#pragma unroll
+    for (int i = 0; i < kMaxDwords - 1; ++i)
+        if (static_cast<uint32_t>(i) == nf) tail = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+    for (uint32_t j = 0; j < (L & 3u); ++j) reg = t4[0][(reg ^ (tail >> (8u * j))) & 0xFFu] ^ (reg >> 8);
+    return reg;
+}
+
 __global__ void __launch_bounds__(kThreads) crc32_gather_join_kernel(GatherArgs ga, const uint32_t* seg_crc,
                                                                      KernelTables tb, uint32_t small) {
-    __shared__ uint32_t t0[256];
+    __shared__ uint32_t t4[4][256];
     if (small) {
-        for (uint32_t j = threadIdx.x; j < 256u; j += kThreads) t0[j] = tb.image[64u * j];
+        for (uint32_t i = threadIdx.x; i < 1024u; i += kThreads) t4[i >> 8][i & 255u] = tb.image[64u * (i & 255u) + 2u * (i >> 8)];
         __syncthreads();
     }
     const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
@@ -872,8 +899,7 @@ __global__ void __launch_bounds__(kThreads) crc32_gather_join_kernel(GatherArgs 
             const uint32_t L = ga.seg_len[q];
             if (L == 0) continue;
             if (L <= small) {
-                const uint8_t* a = ga.bytes + ga.seg_off[q];
-                for (uint32_t i = 0; i < L; ++i) reg = t0[(reg ^ a[i]) & 0xFFu] ^ (reg >> 8);
+                reg = fold_small(reg, ga.bytes + ga.seg_off[q], L, t4);
             } else {
                 const uint32_t r = ~bswap32(seg_crc[q]);
                 reg = (reg == 0xFFFFFFFFu ? 0u : mulmod(reg ^ 0xFFFFFFFFu, x8n_dev(L, tb))) ^ r;
@@ -1281,6 +1307,13 @@ int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStr
 
 int ensure(uint8_t** p, size_t* cap, size_t need) { return ensure_device(p, cap, need); }
 
+// The binned gather's workspace: records (1024 per tile of segments, length_bin_compact's
+// layout; the binned entry's records fit too) | seg_crc[segCount + 1] (the last: the
+// padding records' CRCs, never read) | tile counts
+size_t gather_tiles(size_t segCount) { return (segCount + 1023u) / 1024u; }
+size_t gather_records_bytes(size_t segCount) { return 16u * 1024u * gather_tiles(segCount); }
+size_t gather_crc_bytes(size_t segCount) { return (4u * (segCount + 1u) + 15u) & ~static_cast<size_t>(15u); }
+
 }  // namespace
 
 extern "C" {
@@ -1631,8 +1664,7 @@ int enet_hip_crc32_gather_device(enet_hip_context* ctx, const uint8_t* bytes, co
 }
 
 size_t enet_hip_gather_binned_workspace_size(size_t segCount) {
-    // records | seg_crc[segCount] | the compacted records' count
-    return ((enet_hip_binned_workspace_size(segCount) + 15u) & ~static_cast<size_t>(15u)) + 4u * segCount + 16u;
+    return gather_records_bytes(segCount) + gather_crc_bytes(segCount) + 4u * gather_tiles(segCount) + 16u;
 }
 
 int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* bytes, const uint64_t* segOffsets,
@@ -1647,23 +1679,26 @@ int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* by
         return -static_cast<int>(hipErrorInvalidValue);
     ENH_CHECK(hipSetDevice(ctx->device));
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-    const size_t bws = (enet_hip_binned_workspace_size(segCount) + 15u) & ~static_cast<size_t>(15u);
+    const size_t bws = gather_records_bytes(segCount);
     uint32_t* seg_crc = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(workspace) + bws);
-    uint32_t* count = seg_crc + segCount;                    // the compacted records' count
+    uint32_t* counts = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(workspace) + bws + gather_crc_bytes(segCount));
     const int lanes = ctx->lanes_per_packet > 0 ? ctx->lanes_per_packet : 8;
     // The default (vring paths, 4 or 8 lanes): segments of at most kGatherSmall bytes
-    // are folded by the join, the rest compacted into length-sorted records whose
-    // count stays on the device (VrBatches::n_dev) and checksummed by the vring's
+    // are folded by the join, the rest sorted per tile into records (padded, tile
+    // counts on the device: VrBatches::tile_counts) and checksummed by the vring's
     // records instance.  Other paths: every segment through the binned entry.
     const bool split = vring_path(ctx) && ctx->ablation == 0 && (lanes == 4 || lanes == 8);
     if (segCount && split) {
         const KernelTables tb = tables_of(ctx);
+        const uint32_t kpk = lanes == 4 ? 16u : 8u;
         int rc;
-        if ((rc = length_bin_compact(segLengths, segOffsets, segCount, kGatherSmall, workspace, count, st))) return rc;
+        if ((rc = length_bin_compact(segLengths, segOffsets, segCount, kpk, kGatherSmall, workspace, counts, st)))
+            return rc;
         VrBatches bl{};
         bl.count = 1;
-        bl.n_dev = count;
-        bl.b[0] = VrBatch{bytes, static_cast<const uint64_t*>(workspace), nullptr, seg_crc, segCount, 0u};
+        bl.tiles = static_cast<uint32_t>(gather_tiles(segCount));
+        bl.tile_counts = counts;
+        bl.b[0] = VrBatch{bytes, static_cast<const uint64_t*>(workspace), nullptr, seg_crc, 1024ull * bl.tiles, 0u};
         if ((rc = vring_launch_list(lanes == 4 ? 2 : 3, ctx->num_cus * vring_wgs(ctx, 1), VrVariant{}, st, bl, tb,
                                     ctx->d_basis2, nullptr, true)))
             return rc;

@@ -744,16 +744,16 @@ __device__ __forceinline__ uint32_t bin_of(uint32_t len) { return kBins - 1u - m
 // VERIFY: 32-byte records {len, off_lo, off_hi, slot_off, connect, index, 0, 0}
 // (the lean kernel's MODE 1 metadata fields), else 16-byte {len, off_lo, off_hi, index}.
 // COMPACT (the binned gather): records of length <= small are left out (the join
-// folds those segments itself), and each tile's sorted records are appended at a
-// position taken from *count (a global atomic per tile; *count = 0 before the
-// launch): the records are [0, *count), tile after tile, each longest first.
+// folds those segments itself); each tile, the ragged last one included, writes
+// its kept records sorted and then empty records {0, 0, 0, pad_index} up to 1024,
+// all rank-interleaved (group q T + t, T = every tile), and count[t] = its kept
+// records.  No global atomics: the vring's records instance reads the counts.
 template <bool VERIFY, bool COMPACT = false>
 __global__ void __launch_bounds__(kBinThreads) bin_tile_kernel(const uint32_t* len, const uint64_t* off, uint64_t n,
                                                                uint32_t kpk, const uint32_t* slot_off,
                                                                const uint32_t* connect, uint4* rec, uint32_t small,
                                                                uint32_t* count) {
     __shared__ uint32_t h[kBins], sc[kBins];
-    __shared__ uint32_t first;                               // COMPACT: the tile's first record
     const uint32_t tid = threadIdx.x;
     h[tid] = 0;
     __syncthreads();
@@ -781,17 +781,20 @@ __global__ void __launch_bounds__(kBinThreads) bin_tile_kernel(const uint32_t* l
         __syncthreads();
     }
     h[tid] = sc[tid] - mine;                                 // first slot of bin tid in the tile
-    if constexpr (COMPACT)
-        if (tid == kBins - 1u) first = atomicAdd(count, sc[tid]);   // (sc[last] = the tile's kept records)
+    const uint32_t kept_n = sc[kBins - 1u];                  // (COMPACT: the tile's kept records)
     __syncthreads();
-    const uint64_t full = n / kBinTile;                      // T
-    const bool interleave = blockIdx.x < full;
+    const uint64_t full = COMPACT ? gridDim.x : n / kBinTile;    // T
+    const bool interleave = COMPACT || blockIdx.x < full;
+    if constexpr (COMPACT) {
+        if (tid == 0) count[blockIdx.x] = kept_n;
+        for (uint32_t srt = kept_n + tid; srt < kBinTile; srt += kBinThreads)        // the padding
+            rec[((srt / kpk) * full + blockIdx.x) * kpk + srt % kpk] = make_uint4(0u, 0u, 0u, static_cast<uint32_t>(n));
+    }
 #pragma unroll
     for (uint32_t r = 0; r < kBinItems; ++r) {
         const uint64_t i = base + r * kBinThreads + tid;
         const uint32_t srt = h[bin_of(L[r])] + slot[r];      // rank inside the tile
-        const uint64_t dst = COMPACT ? static_cast<uint64_t>(first) + srt
-                             : interleave ? ((srt / kpk) * full + blockIdx.x) * kpk + srt % kpk : base + srt;
+        const uint64_t dst = interleave ? ((srt / kpk) * full + blockIdx.x) * kpk + srt % kpk : base + srt;
         if (kept(r)) {
             if constexpr (VERIFY) {
                 rec[2 * dst] = make_uint4(L[r], static_cast<uint32_t>(o[r]), static_cast<uint32_t>(o[r] >> 32), slot_off[i]);
@@ -821,16 +824,15 @@ int length_bin(const uint32_t* len, const uint64_t* off, const uint32_t* slot_of
     return e == hipSuccess ? 0 : -static_cast<int>(e);
 }
 
-int length_bin_compact(const uint32_t* len, const uint64_t* off, uint64_t n, uint32_t small, void* records,
-                       uint32_t* count, hipStream_t st) {
+int length_bin_compact(const uint32_t* len, const uint64_t* off, uint64_t n, uint32_t kpk, uint32_t small,
+                       void* records, uint32_t* counts, hipStream_t st) {
     if (n == 0) return 0;
-    if (n > 0xFFFFFFFFull || !records || !count) return -static_cast<int>(hipErrorInvalidValue);
+    if (n > 0xFFFFFFFFull || !records || !counts || kpk == 0 || kBinTile % kpk)
+        return -static_cast<int>(hipErrorInvalidValue);
     const unsigned tiles = static_cast<unsigned>((n + kBinTile - 1) / kBinTile);
-    hipError_t e = hipMemsetAsync(count, 0, sizeof(uint32_t), st);
-    if (e != hipSuccess) return -static_cast<int>(e);
-    hipLaunchKernelGGL((bin_tile_kernel<false, true>), dim3(tiles), dim3(kBinThreads), 0, st, len, off, n, 8u, nullptr,
-                       nullptr, static_cast<uint4*>(records), small, count);
-    e = hipGetLastError();
+    hipLaunchKernelGGL((bin_tile_kernel<false, true>), dim3(tiles), dim3(kBinThreads), 0, st, len, off, n, kpk, nullptr,
+                       nullptr, static_cast<uint4*>(records), small, counts);
+    const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : -static_cast<int>(e);
 }
 

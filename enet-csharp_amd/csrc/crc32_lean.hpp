@@ -79,11 +79,13 @@ int lean_launch_vlist(int lg, int num_cus, hipStream_t st, const ENetHipVerifyBa
 size_t length_bin_workspace(uint64_t n, bool verify);
 int length_bin(const uint32_t* len, const uint64_t* off, const uint32_t* slot_off, const uint32_t* connect, uint64_t n,
                uint32_t kpk, void* workspace, hipStream_t st);
-// The binned gather's records: the records {len, off_lo, off_hi, index} of the
-// segments longer than `small`, each tile's sorted longest first and appended at
-// a position taken from *count (zeroed here first, stream-ordered), so they fill
-// records[0, *count) -- a count only the device knows.  records: 16 n bytes.
-int length_bin_compact(const uint32_t* len, const uint64_t* off, uint64_t n, uint32_t small, void* records,
-                       uint32_t* count, hipStream_t st);
+// The binned gather's records: per 1024-segment tile (T = ceil(n / 1024), the
+// ragged last one included), the records {len, off_lo, off_hi, index} of the
+// segments longer than `small`, sorted longest first, then empty records {0, 0, 0,
+// n} up to 1024, rank-interleaved as length_bin's full tiles (group q T + t =
+// tile t's records [q kpk, (q + 1) kpk)); counts[t] = tile t's kept records.
+// records: 16 x 1024 T bytes; counts: 4 T bytes.  No global atomics.
+int length_bin_compact(const uint32_t* len, const uint64_t* off, uint64_t n, uint32_t kpk, uint32_t small,
+                       void* records, uint32_t* counts, hipStream_t st);
 
 }  // namespace enethip

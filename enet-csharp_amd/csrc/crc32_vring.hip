@@ -497,13 +497,18 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     auto lane_k = [&]() __attribute__((always_inline)) { return lane & (P - 1u); };   // block lane
     auto lane_p = [&]() __attribute__((always_inline)) { return lane >> LG; };         // packet of the group
     const uint64_t zero = reinterpret_cast<uint64_t>(tb.zero);
-    // batch b's packets and the launch's groups; BIN with a device-side count: the
-    // count the bin kernel wrote (the binned gather's compacted records)
+    // batch b's packets and the launch's groups; BIN with tile counts (the binned
+    // gather): the ranks up to the fullest tile's, R = ceil(max_t count_t / kPk), i.e.
+    // R x tiles groups, every record of them valid (kept or empty padding).  Each wave
+    // reduces the counts itself (a few KiB, from L2): no barrier, no global atomic.
     uint64_t n0 = bl.b[0].n, ngroups_all = bl.groups;
     if constexpr (BIN) {
-        if (bl.n_dev) {
-            n0 = min<uint64_t>(*bl.n_dev, n0);
-            ngroups_all = (n0 + kPk - 1u) / kPk;
+        if (bl.tile_counts) {
+            uint32_t m = 0;
+            for (uint32_t t = threadIdx.x & 63u; t < bl.tiles; t += 64u) m = max(m, bl.tile_counts[t]);
+            const uint32_t r = (wave_max_u(m) + kPk - 1u) / kPk;
+            ngroups_all = static_cast<uint64_t>(r) * bl.tiles;
+            n0 = ngroups_all * kPk;
         }
     }
     auto batch_n = [&](uint32_t b) __attribute__((always_inline)) -> uint64_t { return BIN ? n0 : bl.b[b].n; };
@@ -592,7 +597,7 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
         // lane l loads field f = l / kPk of packet l % kPk (lanes past the fields: field
         // 0), the packet clamped to the batch's last (always a valid address; the
         // prologue of a wave with no group at all loads batch 0's last packet)
-        const uint64_t bn = max<uint64_t>(batch_n(it.b), 1u);   // (a device count of 0: record 0, unused)
+        const uint64_t bn = max<uint64_t>(batch_n(it.b), 1u);   // (no kept record at all: record 0, unused)
         const uint64_t base = min<uint64_t>(group_base(it), bn - 1u);
         const uint64_t left = bn - 1u - base;                // (uniform: scalar select, no VALU)
         const uint32_t l = vr_lane();                       // (recomputed: not a register held across the loop)
@@ -1000,8 +1005,10 @@ int vring_launch_list(int lg, int max_wgs, const VrVariant& v, hipStream_t st, c
     if (!fn) return -static_cast<int>(hipErrorInvalidValue);   // a variant this library does not build
     // empty batches dropped: the kernel may then read any batch's packet n - 1
     VrBatches a{};
-    if (bin && bl.n_dev && bl.count != 1) return -static_cast<int>(hipErrorInvalidValue);
-    a.n_dev = bin ? bl.n_dev : nullptr;
+    if (bin && bl.tile_counts && (bl.count != 1 || bl.b[0].n != 1024ull * bl.tiles))
+        return -static_cast<int>(hipErrorInvalidValue);
+    a.tile_counts = bin ? bl.tile_counts : nullptr;
+    a.tiles = bin ? bl.tiles : 0u;
     for (uint32_t b = 0; b < bl.count; ++b)
         if (bl.b[b].n) a.b[a.count++] = bl.b[b];
     if (a.count == 0) return 0;

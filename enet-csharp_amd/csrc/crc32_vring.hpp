@@ -29,11 +29,15 @@ struct VrBatch {
 constexpr int kVrMaxBatches = 48;
 struct VrBatches {
     uint32_t count;
-    uint32_t pad;
+    // BIN with tile_counts: the number of 1024-record tiles (see tile_counts)
+    uint32_t tiles;
     uint64_t groups;    // all batches' groups (set by vring_launch_list)
-    // BIN only (one batch): batch 0's record count in device memory, at most b[0].n
-    // (the binned gather's compacted records: a count the host does not know), or null
-    const uint32_t* n_dev;
+    // BIN only (one batch), or null: the binned gather's records, length_bin_tiles's
+    // layout -- tile t's kept records sorted and padded with empty records to 1024,
+    // rank-interleaved (group q T + t holds tile t's records [q kpk, (q + 1) kpk)) --
+    // and tile_counts[t] = tile t's kept records.  The kernel runs the groups of the
+    // ranks q < ceil(max_t tile_counts[t] / kpk): a count the host does not know.
+    const uint32_t* tile_counts;
     VrBatch b[kVrMaxBatches];
 };
 static_assert(sizeof(VrBatches) <= 3072, "kernel arguments");
