@@ -368,13 +368,16 @@ def kernel_name(args, list_launch: bool = False) -> str:
     return f"crc32_vring_kernel<{lg}, 0, {nt}, 0, 0, 0, {rot}, 0>"
 
 
-def load_traffic(cfg: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/), or None."""
+def load_traffic(cfg: str, binned: bool = False):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/), or None
+    when there is none for this entry (a file marked "binned" is the length-binned
+    entry's; unmarked ones are the plain / batch-list entry's)."""
     p = os.path.join(ROOT, "profiles", f"traffic_{cfg}.json")
     try:
-        return json.load(open(p))
+        doc = json.load(open(p))
     except (OSError, ValueError):
         return None
+    return doc if bool(doc.get("binned", False)) == bool(binned) else None
 
 
 def main(argv=None, engine_factory=None, cpu_factory=None):
@@ -462,7 +465,7 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
         cpu = (cpu_factory or cpu_baseline)(batches[0], args.cpu_seconds, args.cpu_threads)
 
     if rank == 0:
-        traffic = load_traffic(args.config)
+        traffic = load_traffic(args.config, args.binned)
         line = {
             "metric": METRIC,
             "value": round(value, 2),

@@ -42,7 +42,7 @@ namespace enethip {
 constexpr int kThreads = 512;                     // direct / gather kernels: 8 waves
 // Gather segments of at most this many bytes are folded byte by byte by the join
 // (crc32_gather_join_kernel), not by the binned checksum pass
-constexpr uint32_t kGatherSmall = 64;
+constexpr uint32_t kGatherSmall = 48;
 
 template <int NT>
 __device__ __forceinline__ void fill_table(uint8_t* lds, const uint32_t* image) {
@@ -849,39 +849,46 @@ __global__ void __launch_bounds__(kThreads) crc32_gather_kernel(GatherArgs ga, K
 // reg(0xFFFFFFFF, B) ^ adv_|B|(0xFFFFFFFF), so one multiply per segment:
 // reg' = (reg ^ 0xFFFFFFFF) x^(8|B|) ^ reg(0xFFFFFFFF, B), from reg = 0xFFFFFFFF
 // (packet.cs:144-159 over the concatenated buffers, as enet_crc32 walks them).
-// Segments of at most `small` bytes (an ENet DGRAM's protocol header and command
-// headers: 4-8 and 4-48 B) had no checksum pass: the thread folds them into reg
-// itself (packet.cs:150-155).  All of the segment's aligned dwords are loaded first
-// (<= 17 independent loads, never past the dword holding its last byte), then each
-// 4 bytes are one slicing-by-4 step on the dword v_alignbyte cuts at the segment's
-// offset, the last L mod 4 bytes Sarwate steps (T_3 .. T_0 = columns 6, 4, 2, 0 of
-// the P = 1 image, 4 KiB in LDS).
-__device__ __forceinline__ uint32_t fold_small(uint32_t reg, const uint8_t* a, uint32_t L, const uint32_t (*t4)[256]) {
-    constexpr int kMaxDwords = 17;                           // (3 + 64 + 3) / 4
+// Segments of at most `small` (<= kGatherSmall) bytes -- an ENet DGRAM's protocol
+// header and command headers: 4-8 and 4-48 B -- had no checksum pass: the thread
+// folds them into reg itself (packet.cs:150-155).  Latency first: a thread takes its
+// DGRAM's segments four at a time and issues every load of the four -- lengths and
+// offsets, then the short segments' aligned dwords (never past the dword holding a
+// segment's last byte), the long ones' CRCs and x^(8 len) -- before folding any.  A
+// short segment's 4-byte steps are slicing-by-4 on the dword v_alignbyte cuts at its
+// offset, its last L mod 4 bytes Sarwate steps (T_3 .. T_0 = columns 6, 4, 2, 0 of
+// the P = 1 image, 4 KiB in LDS).  Restated in tests/kernel_model.py (fold_small).
+constexpr int kSmallDwords = (3 + static_cast<int>(kGatherSmall) + 3) / 4;
+
+__device__ __forceinline__ void load_small(const uint8_t* a, uint32_t L, uint32_t (&d)[kSmallDwords + 1]) {
     const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a)) & 3u;
     const uint32_t* w = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(a) & ~static_cast<uintptr_t>(3));
-    const uint32_t nd = (sh + L + 3u) >> 2, nf = L >> 2;
-    uint32_t d[kMaxDwords + 1];
+    const uint32_t nd = (sh + L + 3u) >> 2;
 #pragma unroll
-    for (int k = 0; k < kMaxDwords; ++k) d[k] = static_cast<uint32_t>(k) < nd ? w[k] : 0u;
-    d[kMaxDwords] = 0u;
-#pragma unroll
-    for (int i = 0; i < kMaxDwords - 1; ++i) {
-        if (static_cast<uint32_t>(i) < nf) {
-            const uint32_t x = reg ^ __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
-            reg = t4[3][x & 0xFFu] ^ t4[2][(x >> 8) & 0xFFu] ^ t4[1][(x >> 16) & 0xFFu] ^ t4[0][x >> 24];
-        }
-    }
+    for (int k = 0; k < kSmallDwords; ++k) d[k] = static_cast<uint32_t>(k) < nd ? w[k] : 0u;
+    d[kSmallDwords] = 0u;
+}
+
+__device__ __forceinline__ uint32_t fold_small(uint32_t reg, uint32_t sh, uint32_t L,
+                                               const uint32_t (&d)[kSmallDwords + 1], const uint32_t (*t4)[256]) {
+    const uint32_t nf = L >> 2;
     uint32_t tail = 0;
 #pragma unroll
-    for (int i = 0; i < kMaxDwords - 1; ++i)
-        if (static_cast<uint32_t>(i) == nf) tail = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+    for (int i = 0; i < kSmallDwords - 1; ++i) {
+        const uint32_t v = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+        if (static_cast<uint32_t>(i) < nf) {
+            const uint32_t x = reg ^ v;
+            reg = t4[3][x & 0xFFu] ^ t4[2][(x >> 8) & 0xFFu] ^ t4[1][(x >> 16) & 0xFFu] ^ t4[0][x >> 24];
+        }
+        tail = static_cast<uint32_t>(i) == nf ? v : tail;
+    }
     for (uint32_t j = 0; j < (L & 3u); ++j) reg = t4[0][(reg ^ (tail >> (8u * j))) & 0xFFu] ^ (reg >> 8);
     return reg;
 }
 
 __global__ void __launch_bounds__(kThreads) crc32_gather_join_kernel(GatherArgs ga, const uint32_t* seg_crc,
                                                                      KernelTables tb, uint32_t small) {
+    constexpr int kQ = 4;                                    // segments in flight per thread
     __shared__ uint32_t t4[4][256];
     if (small) {
         for (uint32_t i = threadIdx.x; i < 1024u; i += kThreads) t4[i >> 8][i & 255u] = tb.image[64u * (i & 255u) + 2u * (i >> 8)];
@@ -895,14 +902,35 @@ __global__ void __launch_bounds__(kThreads) crc32_gather_join_kernel(GatherArgs 
         const uint32_t s1 = static_cast<uint32_t>(min<uint64_t>(ga.seg_first[d + 1], ga.segs));
         const uint32_t s0 = min(ga.seg_first[d], s1);
         uint32_t reg = 0xFFFFFFFFu;
-        for (uint32_t q = s0; q < s1; ++q) {
-            const uint32_t L = ga.seg_len[q];
-            if (L == 0) continue;
-            if (L <= small) {
-                reg = fold_small(reg, ga.bytes + ga.seg_off[q], L, t4);
-            } else {
-                const uint32_t r = ~bswap32(seg_crc[q]);
-                reg = (reg == 0xFFFFFFFFu ? 0u : mulmod(reg ^ 0xFFFFFFFFu, x8n_dev(L, tb))) ^ r;
+        for (uint32_t q0 = s0; q0 < s1; q0 += kQ) {
+            uint32_t L[kQ];
+            const uint8_t* A[kQ];
+#pragma unroll
+            for (int i = 0; i < kQ; ++i) {
+                const bool in = q0 + i < s1;
+                L[i] = in ? ga.seg_len[q0 + i] : 0u;
+                A[i] = ga.bytes + (in ? ga.seg_off[q0 + i] : 0u);
+            }
+            uint32_t D[kQ][kSmallDwords + 1], C[kQ], X[kQ];
+#pragma unroll
+            for (int i = 0; i < kQ; ++i) {
+                const bool sm = L[i] != 0u && L[i] <= small;
+                if (sm) load_small(A[i], L[i], D[i]);
+                else
+#pragma unroll
+                    for (int k = 0; k <= kSmallDwords; ++k) D[i][k] = 0u;
+                C[i] = L[i] > small ? seg_crc[q0 + i] : 0u;
+                X[i] = L[i] > small ? tb.xn_lo[L[i] & 0xFFFFu] : 0u;
+            }
+#pragma unroll
+            for (int i = 0; i < kQ; ++i) {
+                if (L[i] == 0u) continue;
+                if (L[i] <= small) {
+                    reg = fold_small(reg, static_cast<uint32_t>(reinterpret_cast<uintptr_t>(A[i])) & 3u, L[i], D[i], t4);
+                } else {
+                    const uint32_t x = (L[i] >> 16) ? mulmod(X[i], tb.xn_hi[L[i] >> 16]) : X[i];
+                    reg = (reg == 0xFFFFFFFFu ? 0u : mulmod(reg ^ 0xFFFFFFFFu, x)) ^ ~bswap32(C[i]);
+                }
             }
         }
         ga.out[d] = finalize(reg);

@@ -718,6 +718,28 @@ def gather_join(seg_crcs, seg_lens) -> int:
     return finalize(reg)
 
 
+def fold_small(reg: int, arena: bytes, a: int, L: int) -> int:
+    """crc32_kernels.hip fold_small (the join's short segments, <= 64 B): the aligned
+    dwords covering [a, a + L) loaded first, each 4 bytes one slicing-by-4 step on the
+    dword v_alignbyte cuts at a mod 4 (T_3 for the first byte .. T_0 for the last),
+    the last L mod 4 bytes Sarwate steps."""
+    sh, base = a & 3, a & ~3
+    nd = (sh + L + 3) >> 2
+    d = [int.from_bytes(arena[base + 4 * k:base + 4 * k + 4], "little") if k < nd else 0 for k in range(18)]
+
+    def alignbyte(hi, lo, s):
+        return ((hi << 32 | lo) >> (8 * s)) & 0xFFFFFFFF
+
+    nf = L >> 2
+    for i in range(nf):
+        x = reg ^ alignbyte(d[i + 1], d[i], sh)
+        reg = TS[3][x & 0xFF] ^ TS[2][(x >> 8) & 0xFF] ^ TS[1][(x >> 16) & 0xFF] ^ TS[0][x >> 24]
+    tail = alignbyte(d[nf + 1], d[nf], sh)
+    for j in range(L & 3):
+        reg = TS[0][(reg ^ (tail >> (8 * j))) & 0xFF] ^ (reg >> 8)
+    return reg
+
+
 # ---------------------------------------------------------------- unstep column
 def unstep_table() -> list[int]:
     """Free column 28 of every image (kUnstepCol): U[t0(b) >> 24] = (t0(b) << 8) | b, so one

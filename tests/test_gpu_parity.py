@@ -504,7 +504,7 @@ def test_gather_binned(ctx, golden, oracle_lib):
     the golden multi-buffer vectors, cfg5's 3-segment DGRAMs, random gather lists of 0-65
     segments (empty segments and empty DGRAMs among them, arbitrary byte alignment,
     segments shared between DGRAMs), a list of only empty DGRAMs, lists of only short
-    segments (folded by the join) and of lengths around the join's 64-byte split, each
+    segments (folded by the join) and of lengths around the join's 48-byte split, each
     against the oracle's gather, at the default, 4 and 8 lanes and 1 / 2 workgroups per CU."""
     vecs, blob = golden
     seg_off, seg_len, first, exp = [], [], [0], []
@@ -531,9 +531,9 @@ def test_gather_binned(ctx, golden, oracle_lib):
     cases.append((payload, offs, lens, sf, oracle_lib.gather(payload, offs, lens, sf)))
     empty_first = np.zeros(7, np.uint32)
     cases.append((payload[:64], np.zeros(0, np.uint64), np.zeros(0, np.uint32), empty_first, np.zeros(6, np.uint32)))
-    # only segments the join folds itself (<= 64 B: the checksum pass gets no record at
-    # all), and lengths around that split (63 / 64 / 65 B)
-    for lo, hi in ((1, 65), (63, 66)):
+    # only segments the join folds itself (<= 48 B: the checksum pass gets no record at
+    # all), and lengths around that split (47 / 48 / 49 B)
+    for lo, hi in ((1, 49), (47, 50)):
         sl = rng.integers(lo, hi, size=4000).astype(np.uint32)
         so = rng.integers(0, len(payload) - 100, size=4000).astype(np.uint64)
         f = np.arange(0, 4001, 4, dtype=np.uint32)

@@ -366,3 +366,17 @@ def test_vring_edge_mask_slot_keeps_exactly_the_window():
                 got[16 - hs16:32 - hs16] = np.array(mb, "<u4").view(np.uint8)
                 keep = (np.arange(32) >= lo) & (np.arange(32) < hi)
                 assert (got == np.where(keep, block, 0)).all(), (hs16, lo, hi)
+
+
+def test_gather_join_fold_small_matches_oracle(oracle_lib):
+    """The join's short-segment fold (fold_small: preloaded aligned dwords, v_alignbyte,
+    slicing-by-4, Sarwate tail), chained over 1-4 short segments at every offset mod 4,
+    equals the oracle's CRC of their concatenation."""
+    rng = random.Random(7)
+    arena = bytes(rng.getrandbits(8) for _ in range(4096))
+    for _ in range(400):
+        segs = [(rng.randrange(0, 4000), rng.randint(1, 64)) for _ in range(rng.randint(1, 4))]
+        reg = 0xFFFFFFFF
+        for a, L in segs:
+            reg = km.fold_small(reg, arena, a, L)
+        assert km.finalize(reg) == oracle_lib.crc32(b"".join(arena[a:a + L] for a, L in segs))

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--kernels", default="vring_kernel|lean_kernel|bin_tile_kernel|gather_join|gather_small")
     ap.add_argument("--probe-bytes", type=float, default=0.0, help="bytes one read-probe dispatch reads")
     ap.add_argument("--what", default="")
+    ap.add_argument("--binned", action="store_true", help="mark the file as the length-binned entry's "
+                                                           "(bench.py --binned reads it)")
     ap.add_argument("--out")
     a = ap.parse_args()
     rx = re.compile(a.kernels)
@@ -49,6 +51,8 @@ def main():
         "per_kernel_mean_bytes": {k: round(sum(v) / len(v) * 2048) for k, v in per_kernel.items()},
         "per_kernel_dispatches": {k: len(v) for k, v in per_kernel.items()},
         "hbm_bytes_per_call": round(hbm),
+        "hbm_bytes_per_batch": round(hbm),                 # (one batch per call)
+        "binned": a.binned,
         "traffic_over_algorithmic": round(hbm / a.bytes, 4),
         "probe_calibration": (round(sum(probe) / len(probe) * 2048 / a.probe_bytes, 4)
                               if probe and a.probe_bytes else None),
