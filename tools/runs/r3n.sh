@@ -1,0 +1,13 @@
+set -o pipefail
+# round 3 (m): short segments and multipliers in the bin kernel; join = loads + multiplies
+out=gpurun_out/r3n
+mkdir -p $out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+tools/gpu_step.sh 1000 $out/pytest.log python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread || exit 1
+grep -q " passed" $out/pytest.log || exit 1
+grep -q "FAILED" $out/pytest.log && exit 1
+for r in 1 2 3; do
+  tools/gpu_step.sh 300 $out/gather_$r.log python -u tools/gather_bench.py --only gather_binned || exit 1
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/gather_trace -o run --output-format csv \
+  -- python3 tools/gather_bench.py --only gather_binned --reps 20 > $out/gather_trace.log 2>&1 || exit 1
