@@ -175,6 +175,55 @@ namespace enet
                                                             nuint byteCount, ulong* offsets, uint* lengths,
                                                             nuint count, uint* output);
 
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_crc32_gather_binned_host(IntPtr ctx, byte* bytes, nuint byteCount,
+            ulong* segOffsets, uint* segLengths, nuint segCount, uint* segFirst, nuint dgramCount, uint* output);
+
+        // ---- UDP socket batching harness (Linux recvmmsg / sendmmsg; include/enet_hip.h) ----
+        // fd: a bound IPv4 UDP socket (Socket.Handle); addresses and ports in host order.
+        // Return 0, -1 (bad argument) or -(ENET_HIP_ERRNO_BASE + errno).
+        public const int ENET_HIP_ERRNO_BASE = 100000;
+        public const uint ENET_HIP_DGRAM_TRUNCATED = 0xFFFFFFFFu;
+        public const byte ENET_HIP_DGRAM_CHECKSUM = 0, ENET_HIP_DROP_SHORT = 1, ENET_HIP_DROP_PEER = 2,
+                          ENET_HIP_DROP_COMPRESSED = 3, ENET_HIP_DROP_TRUNCATED = 4;
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_udp_receive(int fd, byte* arena, nuint stride, nuint maxDgrams, uint* lengths,
+            uint* srcAddr, ushort* srcPort, int timeoutMs, nuint* received);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_parse_headers(byte* arena, nuint stride, uint* lengths, nuint count,
+            uint* peerConnectIds, nuint peerCount, uint* slotOffsets, uint* connectIds, byte* verdict);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_udp_send(int fd, byte* bytes, ulong* segOffsets, uint* segLengths,
+            uint* segFirst, nuint dgramCount, uint dstAddr, ushort dstPort, nuint* sent);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_stamp_callback(byte* bytes, ulong* segOffsets, uint* segLengths,
+            uint* segFirst, uint* slotOffsets, nuint dgramCount);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_verify_callback(byte* arena, nuint stride, uint* lengths, uint* slotOffsets,
+            uint* connectIds, byte* verdict, nuint count, byte* ok);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_udp_receive_verify(IntPtr ctx, int fd, byte* arena, nuint stride,
+            nuint maxDgrams, uint* peerConnectIds, nuint peerCount, int timeoutMs, uint* lengths, byte* ok,
+            nuint* received);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_udp_stamp_send(IntPtr ctx, int fd, byte* bytes, nuint byteCount,
+            ulong* segOffsets, uint* segLengths, nuint segCount, uint* segFirst, uint* slotOffsets, nuint dgramCount,
+            uint dstAddr, ushort dstPort, nuint* sent);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_read_probe_device(IntPtr ctx, byte* bytes, nuint byteCount, uint* sink,
+            void* stream);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_is_diagnostics_build();
+
         // ---- memory helpers ----
         [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
         public static extern int enet_hip_device_alloc(IntPtr ctx, nuint bytes, void** output);
