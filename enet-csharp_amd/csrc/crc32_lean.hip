@@ -739,7 +739,13 @@ int lean_launch(int mode, int lg, int geom, int abl, int num_cus, hipStream_t st
 
 constexpr uint32_t kBins = 256, kBinThreads = 256, kBinItems = 4, kBinTile = kBinThreads * kBinItems;
 
-__device__ __forceinline__ uint32_t bin_of(uint32_t len) { return kBins - 1u - min(len >> 5, kBins - 1u); }
+// the bin of a record: its vring window length, lz + L (the window starts at the
+// 64-byte boundary at or before the packet), in 32-byte bins, longest first.  Keyed
+// by the window rather than L, a group's packets need about the same stage count
+// whatever their alignment.
+__device__ __forceinline__ uint32_t bin_of(uint32_t len, uint64_t off) {
+    return kBins - 1u - min((len + (static_cast<uint32_t>(off) & 63u)) >> 5, kBins - 1u);
+}
 
 // VERIFY: 32-byte records {len, off_lo, off_hi, slot_off, connect, index, 0, 0}
 // (the lean kernel's MODE 1 metadata fields), else 16-byte {len, off_lo, off_hi, index}.
@@ -800,7 +806,7 @@ __global__ void __launch_bounds__(kBinThreads) bin_tile_kernel(const uint32_t* l
     auto kept = [&](uint32_t r) { return base + r * kBinThreads + tid < n && (!COMPACT || L[r] > small); };
 #pragma unroll
     for (uint32_t r = 0; r < kBinItems; ++r)
-        slot[r] = kept(r) ? atomicAdd(&h[bin_of(L[r])], 1u) : 0u;
+        slot[r] = kept(r) ? atomicAdd(&h[bin_of(L[r], o[r])], 1u) : 0u;
     __syncthreads();
     const uint32_t mine = h[tid];
     sc[tid] = mine;
@@ -824,7 +830,7 @@ __global__ void __launch_bounds__(kBinThreads) bin_tile_kernel(const uint32_t* l
 #pragma unroll
     for (uint32_t r = 0; r < kBinItems; ++r) {
         const uint64_t i = base + r * kBinThreads + tid;
-        const uint32_t srt = h[bin_of(L[r])] + slot[r];      // rank inside the tile
+        const uint32_t srt = h[bin_of(L[r], o[r])] + slot[r];   // rank inside the tile
         const uint64_t dst = interleave ? ((srt / kpk) * full + blockIdx.x) * kpk + srt % kpk : base + srt;
         if (kept(r)) {
             if constexpr (VERIFY) {

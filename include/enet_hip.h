@@ -126,9 +126,9 @@ ENET_HIP_API int enet_hip_crc32_batch_list_device(enet_hip_context* ctx, const E
 
 /* Same results as enet_hip_crc32_batch_device (enet_crc32, c/packet.cs:142-160,
  * per packet), for batches of mixed lengths (SURVEY cfg3): inside each tile of
- * 1024 packets the packet records are first ordered by length (32-byte bins,
- * longest first) on the GPU, so the packets the kernel runs together have about
- * the same length; out[] stays in caller order.  `workspace` is caller-owned
+ * 1024 packets the packet records are first ordered by window length (offset mod
+ * 64 + length, 32-byte bins, longest first) on the GPU, so the packets the kernel
+ * runs together need about the same number of stages; out[] stays in caller order.  `workspace` is caller-owned
  * device memory of at least enet_hip_binned_workspace_size(count) bytes (16 per
  * packet: the ordered {len, off_lo, off_hi, index} records), 16-byte aligned, not
  * shared with a call in flight on another stream; count < 2^32.  No state is

@@ -501,12 +501,13 @@ def lean_group(arena: bytes, offs: list[int], lens: list[int], P: int, check_ban
 BIN_TILE = 1024
 
 
-def bin_of(length: int) -> int:
-    """32-byte bins, longest first (bin 0 holds lengths >= 8160)."""
-    return 255 - min(length >> 5, 255)
+def bin_of(length: int, off: int = 0) -> int:
+    """32-byte bins of the vring window length lz + L (lz = off mod 64), longest first
+    (bin 0 holds windows >= 8160 B)."""
+    return 255 - min((length + (off & 63)) >> 5, 255)
 
 
-def binned_order(lens, kpk: int):
+def binned_order(lens, kpk: int, offs=None):
     """Caller index held by each record position: every 1024-packet tile sorted by
     bin (ties in index order here; on the GPU the order inside a bin is free), sorted
     group q of full tile t placed as global group q * T + t, a ragged last tile in place."""
@@ -515,7 +516,7 @@ def binned_order(lens, kpk: int):
     order = [0] * n
     for t in range((n + BIN_TILE - 1) // BIN_TILE):
         ids = range(t * BIN_TILE, min(n, (t + 1) * BIN_TILE))
-        srt = sorted(ids, key=lambda i: (bin_of(int(lens[i])), i))
+        srt = sorted(ids, key=lambda i: (bin_of(int(lens[i]), 0 if offs is None else int(offs[i])), i))
         for s, i in enumerate(srt):
             dst = ((s // kpk) * full + t) * kpk + s % kpk if t < full else t * BIN_TILE + s
             order[dst] = i

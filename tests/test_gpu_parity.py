@@ -181,7 +181,8 @@ def test_binned_golden_and_edges(ctx, golden, oracle_lib, lanes, path):
 def test_binned_records_are_a_length_ordered_permutation(ctx, oracle_lib):
     """The workspace's records (documented layout: n x {len, off_lo, off_hi, index}
     first) are a permutation of the batch: each 1024-packet tile ordered by non-increasing
-    32-byte length bin, full tiles interleaved group by group; 600 K packets, ragged last tile."""
+    32-byte bin of the window length (offset mod 64 + length), full tiles interleaved
+    group by group; 600 K packets, ragged last tile."""
     rng = np.random.default_rng(11)
     n = 600_000
     lens = rng.integers(0, 1500, size=n).astype(np.uint32)
@@ -209,7 +210,7 @@ def test_binned_records_are_a_length_ordered_permutation(ctx, oracle_lib):
     grp = pos[full] // kpk
     assert (t_of[full] == grp % T).all()
     assert (t_of[~full] == T).all()
-    bins = np.minimum(rec[:, 0] >> 5, 255).astype(np.int64)
+    bins = np.minimum((rec[:, 0] + (rec[:, 1] & 63)) >> 5, 255).astype(np.int64)   # window lz + L
     order = np.lexsort((pos, t_of))                           # each tile's records in position order
     same = np.diff(t_of[order]) == 0
     assert (np.diff(bins[order])[same] <= 0).all()            # longest bin first inside a tile

@@ -11,3 +11,6 @@ for r in 1 2 3; do
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/gather_trace -o run --output-format csv \
   -- python3 tools/gather_bench.py --only gather_binned --reps 20 > $out/gather_trace.log 2>&1 || exit 1
+B="python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --sustain-ms 0"
+tools/gpu_step.sh 300 $out/cfg3b_1.json $B --config cfg3 --binned || exit 1
+tools/gpu_step.sh 300 $out/cfg3b_2.json $B --config cfg3 --binned || exit 1
