@@ -216,43 +216,6 @@ __device__ __forceinline__ uint32_t x8n_dev(uint32_t n, const KernelTables& tb) 
     return x;
 }
 
-// The binned gather's short segments (enet_hip_crc32_gather_binned_device): segments
-// of at most kGatherSmall bytes -- an ENet DGRAM's protocol header and command
-// headers, 4-8 and 4-48 B -- get no records-kernel group; the bin kernel folds them
-// itself (packet.cs:150-155).  load_small issues the segment's aligned dwords (never
-// past the dword holding its last byte); fold_small then takes each 4 bytes as one
-// slicing-by-4 step on the dword v_alignbyte cuts at the segment's offset and the
-// last L mod 4 bytes as Sarwate steps (t4 = T_0 .. T_3 in LDS: columns 0, 2, 4, 6 of
-// the P = 1 image).  Restated in tests/kernel_model.py (fold_small).
-constexpr uint32_t kGatherSmall = 48;
-constexpr int kSmallDwords = (3 + static_cast<int>(kGatherSmall) + 3) / 4;
-
-__device__ __forceinline__ void load_small(const uint8_t* a, uint32_t L, uint32_t (&d)[kSmallDwords + 1]) {
-    const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a)) & 3u;
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(a) & ~static_cast<uintptr_t>(3));
-    const uint32_t nd = (sh + L + 3u) >> 2;
-#pragma unroll
-    for (int k = 0; k < kSmallDwords; ++k) d[k] = static_cast<uint32_t>(k) < nd ? w[k] : 0u;
-    d[kSmallDwords] = 0u;
-}
-
-__device__ __forceinline__ uint32_t fold_small(uint32_t reg, uint32_t sh, uint32_t L,
-                                               const uint32_t (&d)[kSmallDwords + 1], const uint32_t (*t4)[256]) {
-    const uint32_t nf = L >> 2;
-    uint32_t tail = 0;
-#pragma unroll
-    for (int i = 0; i < kSmallDwords - 1; ++i) {
-        const uint32_t v = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
-        if (static_cast<uint32_t>(i) < nf) {
-            const uint32_t x = reg ^ v;
-            reg = t4[3][x & 0xFFu] ^ t4[2][(x >> 8) & 0xFFu] ^ t4[1][(x >> 16) & 0xFFu] ^ t4[0][x >> 24];
-        }
-        tail = static_cast<uint32_t>(i) == nf ? v : tail;
-    }
-    for (uint32_t j = 0; j < (L & 3u); ++j) reg = t4[0][(reg ^ (tail >> (8u * j))) & 0xFFu] ^ (reg >> 8);
-    return reg;
-}
-
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) v = max(v, static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), m)));

@@ -40,6 +40,9 @@
 namespace enethip {
 
 constexpr int kThreads = 512;                     // direct / gather kernels: 8 waves
+// Gather segments of at most this many bytes are folded byte by byte by the join
+// (crc32_gather_join_kernel), not by the binned checksum pass
+constexpr uint32_t kGatherSmall = 48;
 
 template <int NT>
 __device__ __forceinline__ void fill_table(uint8_t* lds, const uint32_t* image) {
@@ -846,13 +849,51 @@ __global__ void __launch_bounds__(kThreads) crc32_gather_kernel(GatherArgs ga, K
 // reg(0xFFFFFFFF, B) ^ adv_|B|(0xFFFFFFFF), so one multiply per segment:
 // reg' = (reg ^ 0xFFFFFFFF) x^(8|B|) ^ reg(0xFFFFFFFF, B), from reg = 0xFFFFFFFF
 // (packet.cs:144-159 over the concatenated buffers, as enet_crc32 walks them).
-// With the split (xm non-null), the bin kernel has already written every short
-// segment's CRC into seg_crc and every segment's x^(8 len) into xm, so the thread's
-// chain is segFirst -> {len, CRC, x^(8 len)} of four segments at a time -> the
-// multiplies.
+// Segments of at most `small` (<= kGatherSmall) bytes -- an ENet DGRAM's protocol
+// header and command headers: 4-8 and 4-48 B -- had no checksum pass: the thread
+// folds them into reg itself (packet.cs:150-155).  Latency first: a thread takes its
+// DGRAM's segments four at a time and issues every load of the four -- lengths and
+// offsets, then the short segments' aligned dwords (never past the dword holding a
+// segment's last byte), the long ones' CRCs and x^(8 len) -- before folding any.  A
+// short segment's 4-byte steps are slicing-by-4 on the dword v_alignbyte cuts at its
+// offset, its last L mod 4 bytes Sarwate steps (T_3 .. T_0 = columns 6, 4, 2, 0 of
+// the P = 1 image, 4 KiB in LDS).  Restated in tests/kernel_model.py (fold_small).
+constexpr int kSmallDwords = (3 + static_cast<int>(kGatherSmall) + 3) / 4;
+
+__device__ __forceinline__ void load_small(const uint8_t* a, uint32_t L, uint32_t (&d)[kSmallDwords + 1]) {
+    const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a)) & 3u;
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(a) & ~static_cast<uintptr_t>(3));
+    const uint32_t nd = (sh + L + 3u) >> 2;
+#pragma unroll
+    for (int k = 0; k < kSmallDwords; ++k) d[k] = static_cast<uint32_t>(k) < nd ? w[k] : 0u;
+    d[kSmallDwords] = 0u;
+}
+
+__device__ __forceinline__ uint32_t fold_small(uint32_t reg, uint32_t sh, uint32_t L,
+                                               const uint32_t (&d)[kSmallDwords + 1], const uint32_t (*t4)[256]) {
+    const uint32_t nf = L >> 2;
+    uint32_t tail = 0;
+#pragma unroll
+    for (int i = 0; i < kSmallDwords - 1; ++i) {
+        const uint32_t v = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+        if (static_cast<uint32_t>(i) < nf) {
+            const uint32_t x = reg ^ v;
+            reg = t4[3][x & 0xFFu] ^ t4[2][(x >> 8) & 0xFFu] ^ t4[1][(x >> 16) & 0xFFu] ^ t4[0][x >> 24];
+        }
+        tail = static_cast<uint32_t>(i) == nf ? v : tail;
+    }
+    for (uint32_t j = 0; j < (L & 3u); ++j) reg = t4[0][(reg ^ (tail >> (8u * j))) & 0xFFu] ^ (reg >> 8);
+    return reg;
+}
+
 __global__ void __launch_bounds__(kThreads) crc32_gather_join_kernel(GatherArgs ga, const uint32_t* seg_crc,
-                                                                     const uint32_t* xm, KernelTables tb) {
+                                                                     KernelTables tb, uint32_t small) {
     constexpr int kQ = 4;                                    // segments in flight per thread
+    __shared__ uint32_t t4[4][256];
+    if (small) {
+        for (uint32_t i = threadIdx.x; i < 1024u; i += kThreads) t4[i >> 8][i & 255u] = tb.image[64u * (i & 255u) + 2u * (i >> 8)];
+        __syncthreads();
+    }
     const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
     for (uint64_t d = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; d < ga.n; d += stride) {
         // segFirst lives in device memory, so the host cannot check segFirst[n] ==
@@ -862,20 +903,34 @@ __global__ void __launch_bounds__(kThreads) crc32_gather_join_kernel(GatherArgs 
         const uint32_t s0 = min(ga.seg_first[d], s1);
         uint32_t reg = 0xFFFFFFFFu;
         for (uint32_t q0 = s0; q0 < s1; q0 += kQ) {
-            uint32_t L[kQ], C[kQ], X[kQ];
+            uint32_t L[kQ];
+            const uint8_t* A[kQ];
 #pragma unroll
             for (int i = 0; i < kQ; ++i) {
                 const bool in = q0 + i < s1;
                 L[i] = in ? ga.seg_len[q0 + i] : 0u;
-                C[i] = in ? seg_crc[q0 + i] : 0u;
-                X[i] = in && xm ? xm[q0 + i] : 0u;
+                A[i] = ga.bytes + (in ? ga.seg_off[q0 + i] : 0u);
+            }
+            uint32_t D[kQ][kSmallDwords + 1], C[kQ], X[kQ];
+#pragma unroll
+            for (int i = 0; i < kQ; ++i) {
+                const bool sm = L[i] != 0u && L[i] <= small;
+                if (sm) load_small(A[i], L[i], D[i]);
+                else
+#pragma unroll
+                    for (int k = 0; k <= kSmallDwords; ++k) D[i][k] = 0u;
+                C[i] = L[i] > small ? seg_crc[q0 + i] : 0u;
+                X[i] = L[i] > small ? tb.xn_lo[L[i] & 0xFFFFu] : 0u;
             }
 #pragma unroll
             for (int i = 0; i < kQ; ++i) {
                 if (L[i] == 0u) continue;
-                // (reg = ~0: the multiply would give 0; skipped)
-                const uint32_t x = xm ? X[i] : x8n_dev(L[i], tb);
-                reg = (reg == 0xFFFFFFFFu ? 0u : mulmod(reg ^ 0xFFFFFFFFu, x)) ^ ~bswap32(C[i]);
+                if (L[i] <= small) {
+                    reg = fold_small(reg, static_cast<uint32_t>(reinterpret_cast<uintptr_t>(A[i])) & 3u, L[i], D[i], t4);
+                } else {
+                    const uint32_t x = (L[i] >> 16) ? mulmod(X[i], tb.xn_hi[L[i] >> 16]) : X[i];
+                    reg = (reg == 0xFFFFFFFFu ? 0u : mulmod(reg ^ 0xFFFFFFFFu, x)) ^ ~bswap32(C[i]);
+                }
             }
         }
         ga.out[d] = finalize(reg);
@@ -1282,7 +1337,7 @@ int ensure(uint8_t** p, size_t* cap, size_t need) { return ensure_device(p, cap,
 
 // The binned gather's workspace: records (1024 per tile of segments, length_bin_compact's
 // layout; the binned entry's records fit too) | seg_crc[segCount + 1] (the last: the
-// padding records' CRCs, never read) | xm[segCount + 1] (x^(8 len)) | tile counts
+// padding records' CRCs, never read) | tile counts
 size_t gather_tiles(size_t segCount) { return (segCount + 1023u) / 1024u; }
 size_t gather_records_bytes(size_t segCount) { return 16u * 1024u * gather_tiles(segCount); }
 size_t gather_crc_bytes(size_t segCount) { return (4u * (segCount + 1u) + 15u) & ~static_cast<size_t>(15u); }
@@ -1637,7 +1692,7 @@ int enet_hip_crc32_gather_device(enet_hip_context* ctx, const uint8_t* bytes, co
 }
 
 size_t enet_hip_gather_binned_workspace_size(size_t segCount) {
-    return gather_records_bytes(segCount) + 2u * gather_crc_bytes(segCount) + 4u * gather_tiles(segCount) + 16u;
+    return gather_records_bytes(segCount) + gather_crc_bytes(segCount) + 4u * gather_tiles(segCount) + 16u;
 }
 
 int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* bytes, const uint64_t* segOffsets,
@@ -1654,8 +1709,7 @@ int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* by
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     const size_t bws = gather_records_bytes(segCount);
     uint32_t* seg_crc = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(workspace) + bws);
-    uint32_t* xm = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(workspace) + bws + gather_crc_bytes(segCount));
-    uint32_t* counts = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(workspace) + bws + 2u * gather_crc_bytes(segCount));
+    uint32_t* counts = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(workspace) + bws + gather_crc_bytes(segCount));
     const int lanes = ctx->lanes_per_packet > 0 ? ctx->lanes_per_packet : 8;
     // The default (vring paths, 4 or 8 lanes): segments of at most kGatherSmall bytes
     // are folded by the join, the rest sorted per tile into records (padded, tile
@@ -1666,8 +1720,7 @@ int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* by
         const KernelTables tb = tables_of(ctx);
         const uint32_t kpk = lanes == 4 ? 16u : 8u;
         int rc;
-        if ((rc = length_bin_compact(bytes, segLengths, segOffsets, segCount, kpk, workspace, seg_crc, xm, counts, tb,
-                                     st)))
+        if ((rc = length_bin_compact(segLengths, segOffsets, segCount, kpk, kGatherSmall, workspace, counts, st)))
             return rc;
         VrBatches bl{};
         bl.count = 1;
@@ -1684,8 +1737,8 @@ int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* by
     }
     GatherArgs ga{bytes, segOffsets, segLengths, segFirst, dgramCount, out, segCount};
     const unsigned grid = grid_for(ctx, dgramCount);
-    hipLaunchKernelGGL(crc32_gather_join_kernel, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc,
-                       (segCount && split) ? xm : nullptr, tables_of(ctx));
+    hipLaunchKernelGGL(crc32_gather_join_kernel, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx),
+                       split ? kGatherSmall : 0u);
     return herr(hipGetLastError());
 }
 

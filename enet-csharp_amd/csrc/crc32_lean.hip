@@ -749,28 +749,17 @@ __device__ __forceinline__ uint32_t bin_of(uint32_t len, uint64_t off) {
 
 // VERIFY: 32-byte records {len, off_lo, off_hi, slot_off, connect, index, 0, 0}
 // (the lean kernel's MODE 1 metadata fields), else 16-byte {len, off_lo, off_hi, index}.
-// COMPACT (the binned gather): records of length <= kGatherSmall are left out --
-// this kernel folds those segments itself into seg_crc (finalize(reg(~0, segment)),
-// load_small / fold_small) -- and every segment's x^(8 len) goes to xm (the join's
-// multipliers).  Each tile, the ragged last one included, writes its kept records
-// sorted and then empty records {0, 0, 0, n} up to 1024, all rank-interleaved (group
-// q T + t, T = every tile), and count[t] = its kept records.  No global atomics: the
-// vring's records instance reads the counts.
-struct GatherBin {
-    const uint8_t* bytes;
-    uint32_t* seg_crc;
-    uint32_t* xm;
-    uint32_t* count;
-};
+// COMPACT (the binned gather): records of length <= small are left out (the join
+// folds those segments itself); each tile, the ragged last one included, writes
+// its kept records sorted and then empty records {0, 0, 0, pad_index} up to 1024,
+// all rank-interleaved (group q T + t, T = every tile), and count[t] = its kept
+// records.  No global atomics: the vring's records instance reads the counts.
 template <bool VERIFY, bool COMPACT = false>
 __global__ void __launch_bounds__(kBinThreads) bin_tile_kernel(const uint32_t* len, const uint64_t* off, uint64_t n,
                                                                uint32_t kpk, const uint32_t* slot_off,
-                                                               const uint32_t* connect, uint4* rec, GatherBin gb,
-                                                               KernelTables tb) {
+                                                               const uint32_t* connect, uint4* rec, uint32_t small,
+                                                               uint32_t* count) {
     __shared__ uint32_t h[kBins], sc[kBins];
-    __shared__ uint32_t t4[COMPACT ? 4 : 1][256];
-    if constexpr (COMPACT)
-        for (uint32_t i = threadIdx.x; i < 1024u; i += kBinThreads) t4[i >> 8][i & 255u] = tb.image[64u * (i & 255u) + 2u * (i >> 8)];
     const uint32_t tid = threadIdx.x;
     h[tid] = 0;
     __syncthreads();
@@ -782,26 +771,6 @@ __global__ void __launch_bounds__(kBinThreads) bin_tile_kernel(const uint32_t* l
         const uint64_t i = base + r * kBinThreads + tid;
         L[r] = i < n ? len[i] : 0u;
         o[r] = i < n ? off[i] : 0u;
-    }
-    constexpr uint32_t small = COMPACT ? kGatherSmall : 0u;
-    if constexpr (COMPACT) {                                 // the short segments' CRCs, every multiplier
-        uint32_t D[kBinItems][kSmallDwords + 1], X[kBinItems];
-#pragma unroll
-        for (uint32_t r = 0; r < kBinItems; ++r) {
-            const uint64_t i = base + r * kBinThreads + tid;
-            const bool sm = i < n && L[r] != 0u && L[r] <= small;
-            if (sm) load_small(gb.bytes + o[r], L[r], D[r]);
-            X[r] = i < n ? tb.xn_lo[L[r] & 0xFFFFu] : 0u;
-        }
-        __syncthreads();                                     // (t4 filled)
-#pragma unroll
-        for (uint32_t r = 0; r < kBinItems; ++r) {
-            const uint64_t i = base + r * kBinThreads + tid;
-            if (i >= n) continue;
-            gb.xm[i] = (L[r] >> 16) ? mulmod(X[r], tb.xn_hi[L[r] >> 16]) : X[r];
-            if (L[r] != 0u && L[r] <= small)
-                gb.seg_crc[i] = finalize(fold_small(0xFFFFFFFFu, static_cast<uint32_t>(o[r]) & 3u, L[r], D[r], t4));
-        }
     }
     auto kept = [&](uint32_t r) { return base + r * kBinThreads + tid < n && (!COMPACT || L[r] > small); };
 #pragma unroll
@@ -823,7 +792,7 @@ __global__ void __launch_bounds__(kBinThreads) bin_tile_kernel(const uint32_t* l
     const uint64_t full = COMPACT ? gridDim.x : n / kBinTile;    // T
     const bool interleave = COMPACT || blockIdx.x < full;
     if constexpr (COMPACT) {
-        if (tid == 0) gb.count[blockIdx.x] = kept_n;
+        if (tid == 0) count[blockIdx.x] = kept_n;
         for (uint32_t srt = kept_n + tid; srt < kBinTile; srt += kBinThreads)        // the padding
             rec[((srt / kpk) * full + blockIdx.x) * kpk + srt % kpk] = make_uint4(0u, 0u, 0u, static_cast<uint32_t>(n));
     }
@@ -853,23 +822,22 @@ int length_bin(const uint32_t* len, const uint64_t* off, const uint32_t* slot_of
     const unsigned tiles = static_cast<unsigned>((n + kBinTile - 1) / kBinTile);
     if (slot_off && connect)
         hipLaunchKernelGGL(bin_tile_kernel<true>, dim3(tiles), dim3(kBinThreads), 0, st, len, off, n, kpk, slot_off,
-                           connect, static_cast<uint4*>(workspace), GatherBin{}, KernelTables{});
+                           connect, static_cast<uint4*>(workspace), 0u, nullptr);
     else
         hipLaunchKernelGGL(bin_tile_kernel<false>, dim3(tiles), dim3(kBinThreads), 0, st, len, off, n, kpk, nullptr,
-                           nullptr, static_cast<uint4*>(workspace), GatherBin{}, KernelTables{});
+                           nullptr, static_cast<uint4*>(workspace), 0u, nullptr);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : -static_cast<int>(e);
 }
 
-int length_bin_compact(const uint8_t* bytes, const uint32_t* len, const uint64_t* off, uint64_t n, uint32_t kpk,
-                       void* records, uint32_t* seg_crc, uint32_t* xm, uint32_t* counts, const KernelTables& tb,
-                       hipStream_t st) {
+int length_bin_compact(const uint32_t* len, const uint64_t* off, uint64_t n, uint32_t kpk, uint32_t small,
+                       void* records, uint32_t* counts, hipStream_t st) {
     if (n == 0) return 0;
-    if (n > 0xFFFFFFFFull || !records || !counts || !seg_crc || !xm || kpk == 0 || kBinTile % kpk)
+    if (n > 0xFFFFFFFFull || !records || !counts || kpk == 0 || kBinTile % kpk)
         return -static_cast<int>(hipErrorInvalidValue);
     const unsigned tiles = static_cast<unsigned>((n + kBinTile - 1) / kBinTile);
     hipLaunchKernelGGL((bin_tile_kernel<false, true>), dim3(tiles), dim3(kBinThreads), 0, st, len, off, n, kpk, nullptr,
-                       nullptr, static_cast<uint4*>(records), GatherBin{bytes, seg_crc, xm, counts}, tb);
+                       nullptr, static_cast<uint4*>(records), small, counts);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : -static_cast<int>(e);
 }

@@ -81,13 +81,11 @@ int length_bin(const uint32_t* len, const uint64_t* off, const uint32_t* slot_of
                uint32_t kpk, void* workspace, hipStream_t st);
 // The binned gather's records: per 1024-segment tile (T = ceil(n / 1024), the
 // ragged last one included), the records {len, off_lo, off_hi, index} of the
-// segments longer than kGatherSmall, sorted longest first, then empty records {0,
-// 0, 0, n} up to 1024, rank-interleaved as length_bin's full tiles (group q T + t =
-// tile t's records [q kpk, (q + 1) kpk)); counts[t] = tile t's kept records.  The
-// short segments' CRCs go to seg_crc[i], every segment's x^(8 len) to xm[i].
+// segments longer than `small`, sorted longest first, then empty records {0, 0, 0,
+// n} up to 1024, rank-interleaved as length_bin's full tiles (group q T + t =
+// tile t's records [q kpk, (q + 1) kpk)); counts[t] = tile t's kept records.
 // records: 16 x 1024 T bytes; counts: 4 T bytes.  No global atomics.
-int length_bin_compact(const uint8_t* bytes, const uint32_t* len, const uint64_t* off, uint64_t n, uint32_t kpk,
-                       void* records, uint32_t* seg_crc, uint32_t* xm, uint32_t* counts, const KernelTables& tb,
-                       hipStream_t st);
+int length_bin_compact(const uint32_t* len, const uint64_t* off, uint64_t n, uint32_t kpk, uint32_t small,
+                       void* records, uint32_t* counts, hipStream_t st);
 
 }  // namespace enethip
