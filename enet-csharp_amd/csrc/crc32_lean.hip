@@ -759,7 +759,7 @@ __global__ void __launch_bounds__(kBinThreads) bin_tile_kernel(const uint32_t* l
                                                                uint32_t kpk, const uint32_t* slot_off,
                                                                const uint32_t* connect, uint4* rec, uint32_t small,
                                                                uint32_t* count) {
-    __shared__ uint32_t h[kBins], sc[kBins];
+    __shared__ uint32_t h[kBins], wsum[kBinThreads / 64];
     const uint32_t tid = threadIdx.x;
     h[tid] = 0;
     __syncthreads();
@@ -777,17 +777,26 @@ __global__ void __launch_bounds__(kBinThreads) bin_tile_kernel(const uint32_t* l
     for (uint32_t r = 0; r < kBinItems; ++r)
         slot[r] = kept(r) ? atomicAdd(&h[bin_of(L[r], o[r])], 1u) : 0u;
     __syncthreads();
-    const uint32_t mine = h[tid];
-    sc[tid] = mine;
-    __syncthreads();
-    for (uint32_t s = 1; s < kBins; s <<= 1) {               // inclusive scan over the bins
-        const uint32_t v = tid >= s ? sc[tid - s] : 0u;
-        __syncthreads();
-        sc[tid] += v;
-        __syncthreads();
+    // exclusive scan over the bins (thread tid = bin tid): an inclusive scan inside
+    // each wave (ds_bpermute shifts, no barrier), then the waves' totals -- two
+    // barriers instead of the sixteen of a block-wide Hillis-Steele scan
+    static_assert(kBins == kBinThreads, "one bin per thread");
+    const uint32_t mine = h[tid], ln = tid & 63u;
+    uint32_t incl = mine;
+#pragma unroll
+    for (uint32_t s = 1; s < 64u; s <<= 1) {
+        const uint32_t u = static_cast<uint32_t>(__shfl_up(static_cast<int>(incl), s));
+        incl += ln >= s ? u : 0u;
     }
-    h[tid] = sc[tid] - mine;                                 // first slot of bin tid in the tile
-    const uint32_t kept_n = sc[kBins - 1u];                  // (COMPACT: the tile's kept records)
+    if (ln == 63u) wsum[tid >> 6] = incl;
+    __syncthreads();
+    uint32_t pre = 0, kept_n = 0;                            // (COMPACT: kept_n = the tile's kept records)
+#pragma unroll
+    for (uint32_t w = 0; w < kBinThreads / 64u; ++w) {
+        pre += w < (tid >> 6) ? wsum[w] : 0u;
+        kept_n += wsum[w];
+    }
+    h[tid] = pre + incl - mine;                              // first slot of bin tid in the tile
     __syncthreads();
     const uint64_t full = COMPACT ? gridDim.x : n / kBinTile;    // T
     const bool interleave = COMPACT || blockIdx.x < full;

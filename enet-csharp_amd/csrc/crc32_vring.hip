@@ -59,6 +59,8 @@ static_assert(2 * kVrLds <= 160 * 1024, "two workgroups per CU");
 constexpr uint32_t kVrMetaWaveBin = kVrMetaWave;
 constexpr uint32_t kVrCtrBin = kVrCtr;
 constexpr int kVrLdsBin = kVrLds;                                // two workgroups per CU as well
+// BIN's index stash (two slots of kPk dwords per wave) fits the basis staging area
+static_assert(kVrW * 2 * 16 * 4 <= kVrBasisRows * 256, "index stash over the basis staging area");
 
 // Global loads as inline asm, waited for by explicit counted vmcnt.  The
 // compiler's own wait insertion loses count across the loop's group-switch
@@ -631,12 +633,25 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     constexpr uint32_t kAln = (ABL & 8) ? 128u : 64u;         // window start alignment
     auto plz = [&]() __attribute__((always_inline)) { return static_cast<uint32_t>(pwl) & (kAln - 1u); };
     uint32_t pst = 0, pstages = 0;
-    uint32_t pidx = 0;                                       // BIN: the caller index of the lane's packet
+    uint32_t pidx = 0;                                       // BIN: the first group's caller index (prologue)
+    // BIN: the caller indices of the producer's group go to an LDS stash, two slots per
+    // wave by group parity, over the basis staging area (free once barrier B is
+    // passed; the first group's, taken before it, is stored after it).  The consumer
+    // reads its group's slot when it writes the CRCs: no index register held across
+    // the ring loop, so the records instance keeps the lane constants live too.
+    uint32_t pgn = 0, cgn = 0;                               // groups entered by producer / consumer
+    auto stash_addr = [&](uint32_t gn) __attribute__((always_inline)) -> uint32_t {
+        return kVrStaging + 4u * kPk * (2u * wave + (gn & 1u)) + 4u * lane_p();
+    };
     uint32_t pps = ~0u, pconn = 0;                           // VF: the slot's window position (~0u: none), connectID
     bool pdone = !any;
-    auto producer_enter = [&]() __attribute__((always_inline)) {   // group pit; metadata in mL / moff
+    auto producer_enter = [&](auto loop_c) __attribute__((always_inline)) {   // group pit; metadata in mL / moff
         const auto& B = bl.b[pit.b];
-        if constexpr (BIN) pidx = midx;
+        if constexpr (BIN) {
+            if constexpr (decltype(loop_c)::value) lds_store(stash_addr(pgn), midx);
+            else pidx = midx;
+            ++pgn;
+        }
         const uint64_t rem = batch_n(pit.b) - group_base(pit);   // packets of the batch from the group's first
         const uint32_t L = lane_p() < rem ? mL : 0u;
         const uint64_t a = reinterpret_cast<uint64_t>(B.bytes) + moff;
@@ -669,7 +684,7 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
                 vr_wait_meta<2, BIN, VF, kPk>(mbase, lane_p(), mL, moff, midx, mso, mconn);
                 pit = qit;
                 qlive = advance(qit);
-                producer_enter();
+                producer_enter(std::true_type{});
             } else {
                 pdone = true;
                 pwl &= ~static_cast<uint64_t>(kAln - 1u);     // [0, 0): every piece reads the zero line
@@ -697,7 +712,7 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
         ++pst;
     };
     if (any) {
-        producer_enter();
+        producer_enter(std::false_type{});
         produce(std::integral_constant<uint32_t, 0>{}, std::integral_constant<int, -1>{});
     }
 
@@ -734,6 +749,9 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();                            // (B) the image is complete
     mark(3);
+    if constexpr (BIN) {                                     // the first group's indices (slot 0)
+        if (any) lds_store(stash_addr(0u), pidx);
+    }
     if (!any) {
         trace_end();                                         // (the prologue's loads are retired)
         return;
@@ -745,7 +763,6 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     uint32_t cps = ~0u, cconn = 0, desired = 0;              // VF: slot position, connectID, the slot's bytes
     uint8_t* cok = nullptr;                                  // VF: the keep mask of the group's packets
     uint32_t* cout = nullptr;                                // the CRCs of the group's packets (BIN: the batch's)
-    uint32_t cidx = 0;                                       // BIN: the caller index of the lane's packet
     uint64_t crem = 0;                                       // packets of its batch from the group's first
     // first stage >= from holding a partly covered head or tail piece (~0u = none)
     auto next_edge = [&](uint32_t from) __attribute__((always_inline)) -> uint32_t {
@@ -780,7 +797,7 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
             cconn = pconn;
             desired = 0;
         }
-        if constexpr (BIN) cidx = pidx;
+        if constexpr (BIN) ++cgn;
         crem = batch_n(pit.b) - base;
         const uint32_t nb = (ce + 31u) >> 5;                 // 0 for an empty packet ([0, 0))
         // the producer's count for this same group (no second wave reduction; the trace
@@ -797,7 +814,7 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     bool done = false;
     auto iteration = [&](auto sc) __attribute__((always_inline)) {
         constexpr uint32_t S = decltype(sc)::value;
-        if constexpr (kVrLaneRecompute || BIN || kRot || VF) lane = vr_lane();   // (the rt / record / slot registers need the room)
+        if constexpr (kVrLaneRecompute || kRot || VF) lane = vr_lane();   // (the rt / slot registers need the room)
         produce(std::integral_constant<uint32_t, S ^ 1u>{}, std::integral_constant<int, static_cast<int>(S)>{});
         const uint32_t cst = stage_of(cs, cstages);          // the window stage this step folds
         const bool tail_first = kRot && cs == 0u && cstages > 1u;   // (wave-uniform)
@@ -873,7 +890,8 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
                     if (cout) cout[lane_p()] = comp;
                 }
             } else if (lane_k() == 0u && lane_p() < crem) {
-                cout[BIN ? cidx : lane_p()] = finalize(reg);                     // packet.cs:159
+                const uint32_t ci = BIN ? lds_load(stash_addr(cgn - 1u)) : lane_p();   // (BIN: the record's index)
+                cout[ci] = finalize(reg);                                         // packet.cs:159
             }
             if (pdone) {
                 // no newer group entered: the wave is done.  The producer's last loads

@@ -206,11 +206,11 @@ ENET_HIP_API int enet_hip_crc32_gather_device(enet_hip_context* ctx, const uint8
                                               void* stream);
 
 /* Same results as enet_hip_crc32_gather_device, with the segment count known on
- * the host (segCount = segFirst[dgramCount]).  Two passes on `stream`: every
- * segment's CRC as one length-binned checksum batch (enet_hip_crc32_batch_device_binned:
- * the 8-B headers, 24-B commands and MTU payloads of a send batch run in groups of
- * about one length), then one thread per DGRAM joins its segments' CRCs with one
- * GF(2) multiply by x^(8 len) each.  `workspace`: caller-owned device memory of at
+ * the host (segCount = segFirst[dgramCount]).  Three passes on `stream`: segments
+ * over 48 B (MTU payloads) sorted per tile of 1024 by length bin, their CRCs from
+ * the vring kernel's records instance, then one thread per DGRAM folds the short
+ * ones (headers, commands) itself and joins the long ones' CRCs with one GF(2)
+ * multiply by x^(8 len) each.  `workspace`: caller-owned device memory of at
  * least enet_hip_gather_binned_workspace_size(segCount) bytes, 16-byte aligned, not
  * shared with a call in flight; segCount < 2^32.  Async; graph-capturable. */
 ENET_HIP_API size_t enet_hip_gather_binned_workspace_size(size_t segCount);

@@ -135,7 +135,7 @@ def run_binned(ctx, payload, off, lens, lanes=0, path=0):
         ctx.set_kernel_path(0)
 
 
-BINNED_PATHS = (0, 17)        # 0: the lean kernel's records instance (default), 17: the vring kernel's
+BINNED_PATHS = (0, 17)        # 0: the default (the vring kernel's records instance), 17: the vring path itself
 
 
 def test_binned_cfg3_full(ctx, oracle_lib):
@@ -547,6 +547,56 @@ def test_gather_binned(ctx, golden, oracle_lib):
                 assert (got == e).all(), (lanes, i, np.nonzero(got != e)[0][:5])
     finally:
         ctx.set_tuning(0, 0)
+
+
+def test_gather_binned_back_to_back_and_graph(ctx, oracle_lib):
+    """The binned gather's three passes (bin, records checksum, join) over workspaces that
+    calls reuse: 12 calls back to back on one non-default stream without a sync, three
+    batches with their own output / workspace pairs in turn (one of them with more empty
+    DGRAMs than segments), then the same calls captured in a CUDA graph and replayed
+    twice.  Every output against the oracle."""
+    g1, g2 = workloads.cfg5(messages=64), workloads.cfg5(messages=48, message_bytes=20000)
+    rng = np.random.default_rng(5)
+    sf3 = np.zeros(41, np.uint32)                             # 40 DGRAMs, 6 segments: dgramCount > segCount + 2
+    sf3[35:] = np.arange(1, 7, dtype=np.uint32)
+    so3 = rng.integers(0, 4000, size=6).astype(np.uint64)
+    sl3 = np.array([1360, 24, 0, 8, 300, 49], np.uint32)
+    p3 = rng.integers(0, 256, size=8192, dtype=np.uint8)
+    batches = []
+    for p, so, sl, sf in ((g1.payload, g1.seg_off, g1.seg_len, g1.seg_first),
+                          (g2.payload, g2.seg_off, g2.seg_len, g2.seg_first), (p3, so3, sl3, sf3)):
+        n, ns = len(sf) - 1, int(sf[-1])
+        wsb = ctx.gather_binned_workspace_size(ns)
+        batches.append(dict(p=dev(p), so=dev(so), sl=dev(sl), sf=dev(sf), n=n, ns=ns, wsb=wsb,
+                            ws=torch.zeros(wsb, dtype=torch.uint8, device="cuda"),
+                            out=torch.full((n,), -1, dtype=torch.int32, device="cuda"),
+                            exp=oracle_lib.gather(p, so, sl, sf)))
+    st = torch.cuda.Stream()
+
+    def call(b):
+        ctx.gather_binned_device(b["p"], b["so"], b["sl"], b["ns"], b["sf"], b["n"], b["out"], b["ws"], b["wsb"],
+                                 stream=st.cuda_stream)
+
+    def check():
+        for b in batches:
+            got = b["out"].cpu().numpy().view(np.uint32)
+            assert (got == b["exp"]).all(), np.nonzero(got != b["exp"])[0][:5]
+            b["out"].fill_(-1)
+        torch.cuda.synchronize()
+
+    torch.cuda.synchronize()
+    for i in range(12):
+        call(batches[i % 3])
+    st.synchronize()
+    check()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=st):
+        for i in range(6):
+            call(batches[i % 3])
+    for _ in range(2):
+        graph.replay()
+        torch.cuda.synchronize()
+        check()
 
 
 def test_bad_tuning_raises(ctx):
