@@ -628,10 +628,29 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     // ---- producer: window of the group it loads, one stage ahead of the consumer
     // the window start (64-byte aligned) with the packet's first byte in it, plz,
     // in the low 6 bits: one 64-bit register for both; pe = the packet's end
+    // EA (the records instance): a packet whose end is 16-byte aligned gets a window
+    // that ENDS on its last byte -- nb = ceil(L / 32) blocks, lz = 32 nb - L < 32
+    // leading zero bytes -- so no trailing zero bytes (tz = 0: no x^(-8 tz)
+    // correction); its start is 16-byte aligned too, so every piece stays an aligned
+    // 16-B load, and its partly covered head piece is the granule holding its first
+    // byte.  Other packets keep the 64-byte-aligned start.  lz goes to pwl's top 6
+    // bits.  Measured: windows ending on ANY packet end (byte-granular 16-B loads)
+    // made cfg3 binned 61.6 against 55.9 us (tools/alignprobe.hip: that load shape
+    // streams 4.3 against 4.9 TB/s); cfg5's 16-byte-aligned segments gain (vring
+    // records 53.5 against 56 us) -- profiles/r03_ea_windows/.
+    constexpr bool kEA = BIN != 0;
+    constexpr uint64_t kEAMask = (1ull << 58) - 1u;
     uint64_t pwl = 0;
     uint32_t pe = 0;
     constexpr uint32_t kAln = (ABL & 8) ? 128u : 64u;         // window start alignment
-    auto plz = [&]() __attribute__((always_inline)) { return static_cast<uint32_t>(pwl) & (kAln - 1u); };
+    auto plz = [&]() __attribute__((always_inline)) {
+        if constexpr (kEA) return static_cast<uint32_t>(pwl >> 58);
+        return static_cast<uint32_t>(pwl) & (kAln - 1u);
+    };
+    auto pws = [&]() __attribute__((always_inline)) -> uint64_t {     // the window start
+        if constexpr (kEA) return pwl & kEAMask;
+        return pwl & ~static_cast<uint64_t>(kAln - 1u);
+    };
     uint32_t pst = 0, pstages = 0;
     uint32_t pidx = 0;                                       // BIN: the first group's caller index (prologue)
     // BIN: the caller indices of the producer's group go to an LDS stash, two slots per
@@ -657,8 +676,16 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
         const uint64_t a = reinterpret_cast<uint64_t>(B.bytes) + moff;
         const uint32_t lz = static_cast<uint32_t>(a) & (kAln - 1u);
         const uint32_t z = L ? lz : 0u;                      // an empty packet: [0, 0)
-        pwl = (a - lz) | z;
-        pe = z + L;
+        if constexpr (kEA) {
+            const uint32_t eb = (L + 31u) & ~31u;            // 32 nb
+            const bool ea = ((static_cast<uint32_t>(a) + L) & 15u) == 0u;
+            const uint32_t w = ea ? eb - L : z;
+            pwl = (a - w) | (static_cast<uint64_t>(w) << 58);
+            pe = ea ? eb : z + L;
+        } else {
+            pwl = (a - lz) | z;
+            pe = z + L;
+        }
         if constexpr (VF) {                                  // a slot wholly inside the DGRAM, or none
             pps = (L >= 4u && mso <= L - 4u) ? z + mso : ~0u;
             pconn = mconn;
@@ -687,7 +714,7 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
                 producer_enter(std::true_type{});
             } else {
                 pdone = true;
-                pwl &= ~static_cast<uint64_t>(kAln - 1u);     // [0, 0): every piece reads the zero line
+                pwl = pws();                                 // [0, 0): every piece reads the zero line
                 pe = 0;
             }
         }
@@ -697,7 +724,7 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
         const uint32_t a0 = (ABL & 8) ? 32u * P * pst + 16u * lane_k() : q0 + hs16;
         const uint32_t a1 = (ABL & 8) ? a0 + 16u * P : q0 + 16u - hs16;
         const uint32_t lz = plz();
-        const uint64_t ws = pwl & ~static_cast<uint64_t>(kAln - 1u);
+        const uint64_t ws = pws();
         const uint64_t s0 = (a0 < pe && a0 + 16u > lz) ? ws + a0 : zero;
         const uint64_t s1 = (a1 < pe && a1 + 16u > lz) ? ws + a1 : zero;
         const bool meta = (pst == 0u) & qlive & !pdone;     // (one branch, no short-circuit flow blocks)

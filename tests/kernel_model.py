@@ -569,8 +569,15 @@ def vring_image(P: int) -> list[int]:
     return _VR_CACHE[P]
 
 
-def vring_window(addr: int, L: int):
-    """(ws, lz, e, nb): window start (64-byte aligned), packet bytes [lz, e) of it."""
+def vring_window(addr: int, L: int, end_aligned: bool = False):
+    """(ws, lz, e, nb): window start (64-byte aligned), packet bytes [lz, e) of it.
+    end_aligned (the records instance's EA windows, for packets whose end is 16-byte
+    aligned): the window of nb = ceil(L / 32) blocks ends on the packet's last byte, so
+    e = 32 nb (no trailing zero bytes: tz = 0) and lz = 32 nb - L < 32.  (The model
+    takes any end alignment.)"""
+    if end_aligned:
+        nb = (L + 31) // 32
+        return addr + L - 32 * nb, 32 * nb - L, 32 * nb, nb
     lz = addr & 63
     e = lz + L
     nb = (e + 31) // 32 if L else 0
@@ -595,14 +602,14 @@ def vring_adv(img, reg: int) -> int:
 
 
 def vring_packet(arena: bytes, addr: int, L: int, P: int, lane_base: int = 0, rotate: bool = False,
-                 group_stages: int = 0) -> int:
+                 group_stages: int = 0, end_aligned: bool = False) -> int:
     """What crc32_vring_kernel's P lanes (lanes lane_base .. lane_base+P-1) compute
     for the packet arena[addr:addr+L]; returns the wire CRC.  rotate: the
     tail-first stage order (the group's last stage first, folded from a zero
     register into rt; rt ^ adv(reg) joins it at the end); group_stages: the
-    group's stage count (>= this packet's own)."""
+    group's stage count (>= this packet's own); end_aligned: vring_window's EA windows."""
     img = vring_image(P)
-    ws, lz, e, nb = vring_window(addr, L)
+    ws, lz, e, nb = vring_window(addr, L, end_aligned)
     stages = max((nb + P - 1) // P, group_stages)
     order = vring_stage_order(stages, rotate)
     total = 0

@@ -250,6 +250,27 @@ def test_vring_model_matches_oracle(P):
 
 
 @pytest.mark.parametrize("P", [4, 8])
+def test_vring_end_aligned_model_matches_oracle(P):
+    """The records instance's end-aligned windows (the last block ends on the packet's
+    last byte: no trailing zero bytes to undo, no tail edge; lz = 32 nb - L leading zero
+    bytes, the partly covered head piece masked): equal to packet.cs:142-160 for every
+    start and end alignment, lengths across block and stage boundaries, empty packets,
+    and packets shorter than their group."""
+    rng = random.Random(0x4541 + P)
+    arena = bytes(rng.getrandbits(8) for _ in range(16384))
+    ol = oracle.OracleLib()
+    cases = [(a, L, 0) for a in range(0, 64, 3) for L in (0, 1, 15, 16, 17, 31, 32, 33, 63, 64, 65, 255, 257)]
+    cases += [(rng.randrange(0, 2048), rng.randrange(0, 3000), rng.randrange(0, 14)) for _ in range(60)]
+    for a, L, gs in cases:
+        ws, lz, e, nb = km.vring_window(128 + a, L, True)
+        assert e == 32 * nb and 0 <= lz < 32 and ws + lz == 128 + a
+        lane_base = P * rng.randrange(0, 64 // P)
+        got = km.vring_packet(arena, 128 + a, L, P, lane_base, group_stages=gs, end_aligned=True)
+        exp = ol.crc32(arena[128 + a:128 + a + L])
+        assert got == exp, (a, L, P, gs, hex(got), hex(exp))
+
+
+@pytest.mark.parametrize("P", [4, 8])
 def test_vring_tail_first_model_matches_oracle(P):
     """The vring kernel's tail-first stage order (the group's last stage folded
     first, from a zero register into rt; the others in order; then rt ^ adv(reg),

@@ -1,0 +1,124 @@
+// alignprobe.hip -- measurement only: does gfx950 stream global_load_dwordx4 at
+// addresses off a 16-byte boundary as fast as aligned ones?  (An end-aligned CRC
+// window -- its last block ending on the packet's last byte, so no trailing zero
+// bytes to undo -- reads every 16-B piece at the packet's end alignment.)
+// Grid-stride over a resident buffer, 16 B per lane, 4 loads in flight per lane,
+// the base shifted by `shift` bytes; every kernel XOR-reduces what it reads into a
+// never-taken sink store.  Also the packet shape of the vring kernel (4 lanes per
+// packet, lane k reading pieces 32 k and 32 k + 16 of each 128-B stage) with the
+// windows 64-B aligned (as the kernel) or ending on packed packets' ends.
+//   hipcc --offload-arch=gfx950 -O3 -o alignprobe tools/alignprobe.hip && ./alignprobe
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <vector>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ u32x4 ld16(const uint8_t* a) { return *reinterpret_cast<const u32x4*>(a); }
+
+__global__ void __launch_bounds__(256) ap_stride(const uint8_t* p, uint64_t nvec, uint32_t shift, uint32_t* sink) {
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256u;
+    uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
+    const uint8_t* b = p + shift;
+    for (; i + 3 * stride < nvec; i += 4 * stride) {
+        const u32x4 v0 = ld16(b + 16 * i), v1 = ld16(b + 16 * (i + stride)), v2 = ld16(b + 16 * (i + 2 * stride)),
+                    v3 = ld16(b + 16 * (i + 3 * stride));
+        acc ^= v0 ^ v1 ^ v2 ^ v3;
+    }
+    const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+    if (x == 0x9E3779B9u) sink[0] = x;
+}
+
+// packets: starts s[j], window of nb blocks from w[j] (any alignment); 16 packets per
+// wave (4 lanes each), a wave's group = 16 consecutive packets, stage t: lane k reads
+// the two 16-B pieces of block k + 4 t
+__global__ void __launch_bounds__(256) ap_packets(const uint8_t* p, const uint64_t* w, const uint32_t* nb,
+                                                  uint64_t n, uint32_t* sink) {
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    const uint32_t lane = threadIdx.x & 63u, k = lane & 3u, pk = lane >> 2;
+    const uint64_t waves = static_cast<uint64_t>(gridDim.x) * 4u;
+    for (uint64_t g = static_cast<uint64_t>(blockIdx.x) * 4u + (threadIdx.x >> 6); g * 16u < n; g += waves) {
+        const uint64_t j = g * 16u + pk;
+        const bool live = j < n;
+        const uint64_t ws = live ? w[j] : 0u;
+        const uint32_t m = live ? nb[j] : 0u;
+        uint32_t ms = m;                                  // the group's stage count: the max block count
+        for (int o = 4; o < 64; o <<= 1) ms = max(ms, static_cast<uint32_t>(__shfl_xor(static_cast<int>(ms), o)));
+        const uint32_t st = (ms + 3u) >> 2;
+        for (uint32_t t = 0; t < st; ++t) {
+            const uint32_t blk = k + 4u * t;
+            if (blk < m) acc ^= ld16(p + ws + 32u * blk) ^ ld16(p + ws + 32u * blk + 16u);
+        }
+    }
+    const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+    if (x == 0x9E3779B9u) sink[0] = x;
+}
+
+int main() {
+    const uint64_t bytes = 768ull << 20;
+    uint8_t* d;
+    uint32_t* sink;
+    hipMalloc(&d, bytes + 4096);
+    hipMemset(d, 1, bytes + 4096);
+    hipMalloc(&sink, 64);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    auto timeit = [&](auto fn, double B, const char* what) {
+        for (int r = 0; r < 3; ++r) fn();
+        hipDeviceSynchronize();
+        hipEventRecord(e0);
+        const int reps = 20;
+        for (int r = 0; r < reps; ++r) fn();
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms = 0;
+        hipEventElapsedTime(&ms, e0, e1);
+        printf("%-58s %7.3f TB/s (%.1f us per launch)\n", what, B * reps / (ms * 1e-3) / 1e12, ms * 1e3 / reps);
+    };
+    const uint64_t nvec = bytes / 16;
+    for (uint32_t sh : {0u, 1u, 4u, 8u, 13u}) {
+        char name[96];
+        snprintf(name, sizeof name, "linear grid-stride, 16 B/lane, base + %u B", sh);
+        timeit([&] { hipLaunchKernelGGL(ap_stride, dim3(256 * 8), dim3(256), 0, 0, d, nvec, sh, sink); },
+               static_cast<double>(nvec) * 16, name);
+    }
+    // cfg3-like packed packets: lengths U[64, 1400], 1 M of them (~ 766 MB)
+    const uint64_t n = 1000000;
+    std::vector<uint32_t> len(n);
+    uint64_t s = 0x4C454E53ull;
+    uint64_t tot = 0;
+    for (uint64_t j = 0; j < n; ++j) {
+        s = s * 6364136223846793005ull + 1442695040888963407ull;
+        len[j] = 64u + static_cast<uint32_t>((s >> 33) % 1337u);
+        tot += len[j];
+    }
+    if (tot + 256 > bytes) return 1;
+    std::vector<uint64_t> wa(n), we(n);
+    std::vector<uint32_t> na(n), ne(n);
+    uint64_t off = 64;
+    for (uint64_t j = 0; j < n; ++j) {
+        const uint64_t lz = off & 63u;                      // 64-B aligned window start (the vring kernel)
+        wa[j] = off - lz;
+        na[j] = static_cast<uint32_t>((lz + len[j] + 31u) / 32u);
+        const uint32_t nbe = (len[j] + 31u) / 32u;          // end-aligned window: ends at the packet's end
+        we[j] = off + len[j] - 32ull * nbe;
+        ne[j] = nbe;
+        off += len[j];
+    }
+    uint64_t *dw;
+    uint32_t *dn;
+    hipMalloc(&dw, 8 * n);
+    hipMalloc(&dn, 4 * n);
+    for (int v = 0; v < 2; ++v) {
+        hipMemcpy(dw, v ? we.data() : wa.data(), 8 * n, hipMemcpyHostToDevice);
+        hipMemcpy(dn, v ? ne.data() : na.data(), 4 * n, hipMemcpyHostToDevice);
+        timeit([&] { hipLaunchKernelGGL(ap_packets, dim3(256 * 4), dim3(256), 0, 0, d, dw, dn, n, sink); },
+               static_cast<double>(tot),
+               v ? "packets (4 lanes, 16/wave), windows ending on packet ends" : "packets (4 lanes, 16/wave), 64-B aligned windows");
+    }
+    return 0;
+}

@@ -1,6 +1,6 @@
 set -o pipefail
-# round 3 (r): serial join again (split join dropped), wave-scan bin kernel, BIN index stash; full -m gpu
-out=gpurun_out/r3r
+# round 3 (s): records instance with end-aligned windows (EA), BIN index stash, wave-scan bin kernel; full -m gpu
+out=gpurun_out/r3s
 mkdir -p $out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 tools/gpu_step.sh 1000 $out/pytest.log python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread || exit 1
