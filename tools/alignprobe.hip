@@ -35,21 +35,23 @@ __global__ void __launch_bounds__(256) ap_stride(const uint8_t* p, uint64_t nvec
 // packets: starts s[j], window of nb blocks from w[j] (any alignment); 16 packets per
 // wave (4 lanes each), a wave's group = 16 consecutive packets, stage t: lane k reads
 // the two 16-B pieces of block k + 4 t
+template <int P>
 __global__ void __launch_bounds__(256) ap_packets(const uint8_t* p, const uint64_t* w, const uint32_t* nb,
                                                   uint64_t n, uint32_t* sink) {
+    constexpr uint32_t kPk = 64 / P;
     u32x4 acc = {0u, 0u, 0u, 0u};
-    const uint32_t lane = threadIdx.x & 63u, k = lane & 3u, pk = lane >> 2;
+    const uint32_t lane = threadIdx.x & 63u, k = lane % P, pk = lane / P;
     const uint64_t waves = static_cast<uint64_t>(gridDim.x) * 4u;
-    for (uint64_t g = static_cast<uint64_t>(blockIdx.x) * 4u + (threadIdx.x >> 6); g * 16u < n; g += waves) {
-        const uint64_t j = g * 16u + pk;
+    for (uint64_t g = static_cast<uint64_t>(blockIdx.x) * 4u + (threadIdx.x >> 6); g * kPk < n; g += waves) {
+        const uint64_t j = g * kPk + pk;
         const bool live = j < n;
         const uint64_t ws = live ? w[j] : 0u;
         const uint32_t m = live ? nb[j] : 0u;
         uint32_t ms = m;                                  // the group's stage count: the max block count
-        for (int o = 4; o < 64; o <<= 1) ms = max(ms, static_cast<uint32_t>(__shfl_xor(static_cast<int>(ms), o)));
-        const uint32_t st = (ms + 3u) >> 2;
+        for (int o = P; o < 64; o <<= 1) ms = max(ms, static_cast<uint32_t>(__shfl_xor(static_cast<int>(ms), o)));
+        const uint32_t st = (ms + P - 1u) / P;
         for (uint32_t t = 0; t < st; ++t) {
-            const uint32_t blk = k + 4u * t;
+            const uint32_t blk = k + P * t;
             if (blk < m) acc ^= ld16(p + ws + 32u * blk) ^ ld16(p + ws + 32u * blk + 16u);
         }
     }
@@ -116,9 +118,38 @@ int main() {
     for (int v = 0; v < 2; ++v) {
         hipMemcpy(dw, v ? we.data() : wa.data(), 8 * n, hipMemcpyHostToDevice);
         hipMemcpy(dn, v ? ne.data() : na.data(), 4 * n, hipMemcpyHostToDevice);
-        timeit([&] { hipLaunchKernelGGL(ap_packets, dim3(256 * 4), dim3(256), 0, 0, d, dw, dn, n, sink); },
+        timeit([&] { hipLaunchKernelGGL(ap_packets<4>, dim3(256 * 4), dim3(256), 0, 0, d, dw, dn, n, sink); },
                static_cast<double>(tot),
                v ? "packets (4 lanes, 16/wave), windows ending on packet ends" : "packets (4 lanes, 16/wave), 64-B aligned windows");
+    }
+    // lanes per packet, 64-B aligned windows (packets in memory order: neighbours share lines)
+    hipMemcpy(dw, wa.data(), 8 * n, hipMemcpyHostToDevice);
+    hipMemcpy(dn, na.data(), 4 * n, hipMemcpyHostToDevice);
+    timeit([&] { hipLaunchKernelGGL(ap_packets<1>, dim3(256 * 4), dim3(256), 0, 0, d, dw, dn, n, sink); },
+           static_cast<double>(tot), "packets (1 lane, 64/wave), 64-B aligned windows");
+    timeit([&] { hipLaunchKernelGGL(ap_packets<2>, dim3(256 * 4), dim3(256), 0, 0, d, dw, dn, n, sink); },
+           static_cast<double>(tot), "packets (2 lanes, 32/wave), 64-B aligned windows");
+    timeit([&] { hipLaunchKernelGGL(ap_packets<8>, dim3(256 * 4), dim3(256), 0, 0, d, dw, dn, n, sink); },
+           static_cast<double>(tot), "packets (8 lanes, 8/wave), 64-B aligned windows");
+    // the same in a shuffled packet order (binned records: neighbours in other groups)
+    {
+        std::vector<uint64_t> ws2(wa);
+        std::vector<uint32_t> ns2(na);
+        uint64_t r = 12345;
+        for (uint64_t j = n - 1; j > 0; --j) {
+            r = r * 6364136223846793005ull + 1442695040888963407ull;
+            const uint64_t q = (r >> 33) % (j + 1);
+            std::swap(ws2[j], ws2[q]);
+            std::swap(ns2[j], ns2[q]);
+        }
+        hipMemcpy(dw, ws2.data(), 8 * n, hipMemcpyHostToDevice);
+        hipMemcpy(dn, ns2.data(), 4 * n, hipMemcpyHostToDevice);
+        timeit([&] { hipLaunchKernelGGL(ap_packets<2>, dim3(256 * 4), dim3(256), 0, 0, d, dw, dn, n, sink); },
+               static_cast<double>(tot), "shuffled packets, 2 lanes");
+        timeit([&] { hipLaunchKernelGGL(ap_packets<4>, dim3(256 * 4), dim3(256), 0, 0, d, dw, dn, n, sink); },
+               static_cast<double>(tot), "shuffled packets, 4 lanes");
+        timeit([&] { hipLaunchKernelGGL(ap_packets<8>, dim3(256 * 4), dim3(256), 0, 0, d, dw, dn, n, sink); },
+               static_cast<double>(tot), "shuffled packets, 8 lanes");
     }
     return 0;
 }
