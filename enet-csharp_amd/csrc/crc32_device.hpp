@@ -245,6 +245,15 @@ __device__ __forceinline__ uint32_t wave_max_u(uint32_t v) {
     const uint32_t c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
     return __builtin_amdgcn_readfirstlane(max(max(a, b), max(c, d)));   // an SGPR: uniform
 }
+__device__ __forceinline__ uint32_t wave_or_u(uint32_t v) {
+    v |= dpp<kDppQuadXor1>(v);
+    v |= dpp<kDppQuadXor2>(v);
+    v |= dpp<kDppRowHalfMirror>(v);
+    v |= dpp<kDppRowMirror>(v);
+    const uint32_t a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
+    const uint32_t c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+    return __builtin_amdgcn_readfirstlane(a | b | c | d);   // an SGPR: uniform
+}
 __device__ __forceinline__ uint32_t wave_min_u(uint32_t v) {
     v = min(v, dpp<kDppQuadXor1>(v));
     v = min(v, dpp<kDppQuadXor2>(v));

@@ -791,7 +791,8 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     uint8_t* cok = nullptr;                                  // VF: the keep mask of the group's packets
     uint32_t* cout = nullptr;                                // the CRCs of the group's packets (BIN: the batch's)
     uint64_t crem = 0;                                       // packets of its batch from the group's first
-    // first stage >= from holding a partly covered head or tail piece (~0u = none)
+    // first stage >= from holding a partly covered head or tail piece (~0u = none):
+    // the per-lane search, one wave reduction per call
     auto next_edge = [&](uint32_t from) __attribute__((always_inline)) -> uint32_t {
         const bool live = ce != clz;
         const uint32_t wh = clz >> 5, wl = (ce - 1u) >> 5;
@@ -810,6 +811,32 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
             h = min(h, min(a, b));
         }
         return wave_min_u(min(h, t));
+    };
+    // ... and the same from the group's edge-stage mask: bit s = stage s holds such a
+    // piece in some lane, bit 31 = some stage >= 31 does.  One wave reduction per
+    // group (consumer_enter) instead of one per edge stage; groups of more than 31
+    // stages fall back to the search from stage 31 on.
+    uint32_t emask = 0;
+    auto next_edge_m = [&](uint32_t from) __attribute__((always_inline)) -> uint32_t {
+        if (from >= 31u) return (emask >> 31) ? next_edge(from) : ~0u;
+        const uint32_t m = emask & (~0u << from);
+        if (!m) return ~0u;
+        const uint32_t st = static_cast<uint32_t>(__builtin_ctz(m));
+        return st < 31u ? st : next_edge(31u);
+    };
+    // this lane's edge stages as mask bits (stages >= 31 on bit 31)
+    auto next_edge_lane_bits = [&]() __attribute__((always_inline)) -> uint32_t {
+        const bool live = ce != clz;
+        const uint32_t wh = clz >> 5, wl = (ce - 1u) >> 5;
+        auto bit = [](uint32_t st) __attribute__((always_inline)) { return st == ~0u ? 0u : 1u << min(st, 31u); };
+        uint32_t e = bit((live && (clz & 15u) && (wh & (P - 1u)) == lane_k()) ? step_of(wh >> LG, cstages) : ~0u) |
+                     bit((live && (ce & 15u) && (wl & (P - 1u)) == lane_k()) ? step_of(wl >> LG, cstages) : ~0u);
+        if constexpr (VF) {                                  // the slot's block(s)
+            const uint32_t s0 = cps >> 5, s1 = (cps + 3u) >> 5;
+            e |= bit((cps != ~0u && (s0 & (P - 1u)) == lane_k()) ? step_of(s0 >> LG, cstages) : ~0u);
+            e |= bit((cps != ~0u && s1 != s0 && (s1 & (P - 1u)) == lane_k()) ? step_of(s1 >> LG, cstages) : ~0u);
+        }
+        return e;
     };
     // Entered right after the producer has entered the same group (the producer
     // runs exactly one stage ahead), so pit / plz / pe are that group's.
@@ -833,7 +860,11 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
         else cstages = pstages;
         const uint32_t init = lds_load(init_addr(clz));
         reg = lane_k() == 0u ? (nb ? init : 0xFFFFFFFFu) : 0u;      // packet.cs:144 (empty packet: ~crc = 0)
-        nedge = next_edge(0);
+        {
+            const uint32_t e = next_edge_lane_bits();
+            emask = wave_or_u(e);
+        }
+        nedge = next_edge_m(0);
         cs = 0;
         if (TR) ++ngroups;
     };
@@ -855,12 +886,12 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
                 if constexpr (!(ABL & 1))
                     vr_edge_mask(A, B, make_vr_sched(lane).hs, static_cast<int32_t>(clz - q0), static_cast<int32_t>(ce - q0));
                 if (cps != ~0u) vr_slot_fix(A, B, make_vr_sched(lane).hs, static_cast<int32_t>(cps - q0), cconn, desired);
-                nedge = next_edge(cs + 1u);
+                nedge = next_edge_m(cs + 1u);
                 vr_shuffle(rin, lane, A, B, d);
             } else {                                         // masked in place, then folded as any stage
                 if constexpr (!(ABL & 1))
                     vr_edge_mask_slot<S>(lane & 16u, static_cast<int32_t>(clz - q0), static_cast<int32_t>(ce - q0));
-                nedge = next_edge(cs + 1u);
+                nedge = next_edge_m(cs + 1u);
                 vr_shuffle_slot<S>(rin, lane, d);
             }
         } else {
