@@ -71,7 +71,7 @@ struct KernelTables {
     const uint32_t* init;   // INIT[r], r < 32
     const uint8_t* zero;    // 256 zero bytes: DMA source of pieces wholly outside a packet
     const uint32_t* basis;  // kBasisDwords per image (lean kernel)
-    const uint32_t* tz;     // kTzTableDwords: the zero-byte multiplier tables (vring kernel)
+    const uint32_t* tz;     // kTzTableDwords + kTzSmallDwords: the zero-byte multiplier tables (vring kernel)
 };
 
 // Zero-byte multipliers for a packet end's tz correction, reg x^(-8 tz): table k
@@ -81,6 +81,14 @@ constexpr int kTzTables = 2;
 constexpr int kTzTableDwords = kTzTables * 4 * 256;        // 8 KiB
 __host__ __device__ constexpr uint32_t tz_addr(uint32_t k, uint32_t b, uint32_t v) {
     return 4u * (256u * (4u * k + b) + v);
+}
+// ... and for c = 1..7 zero bytes (the vring records instance: tz mod 8 by four lookups
+// instead of up to seven unsteps), after them: entry v of byte b = (v << 8 b) x^(-8 c)
+// at dword 256 (4 (c - 1) + b) + v of this block
+constexpr int kTzSmallTables = 7;
+constexpr int kTzSmallDwords = kTzSmallTables * 4 * 256;  // 28 KiB
+__host__ __device__ constexpr uint32_t tz_small_addr(uint32_t c, uint32_t b, uint32_t v) {
+    return 4u * (256u * (4u * (c - 1u) + b) + v);
 }
 
 // ------------------------------------------------------------------ device helpers

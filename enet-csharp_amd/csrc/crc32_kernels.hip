@@ -979,7 +979,7 @@ struct HostTables {
     HostTables()
         : image(static_cast<size_t>(kImages) * kImageDwords), xn(2 * kXnEntries), init(64),
           basis(static_cast<size_t>(kImages) * kBasisDwords), basis2(static_cast<size_t>(kImages) * kVrBasisDwords),
-          tz(kTzTableDwords) {
+          tz(kTzTableDwords + kTzSmallDwords) {
         init[0] = 0xFFFFFFFFu;
         for (int r = 1; r < 64; ++r) init[r] = unstep_zero(init[r - 1]);
         std::vector<uint32_t> cinv(kCinvEntries);
@@ -991,6 +991,10 @@ struct HostTables {
             for (uint32_t b = 0; b < 4; ++b)
                 for (uint32_t v = 0; v < 256; ++v)
                     tz[tz_addr(k, b, v) / 4] = gf2_mulmod(v << (8 * b), cinv[k ? 8 : 16]);
+        for (uint32_t c = 1; c <= static_cast<uint32_t>(kTzSmallTables); ++c)     // x^(-8 c), c < 8
+            for (uint32_t b = 0; b < 4; ++b)
+                for (uint32_t v = 0; v < 256; ++v)
+                    tz[kTzTableDwords + tz_small_addr(c, b, v) / 4] = gf2_mulmod(v << (8 * b), cinv[c]);
         // image of P: dword 64j + 2t + (t>>4) = T_{t+32(P-1)}[j] (byte j followed by
         // t + 32(P-1) zero bytes); the free dwords hold INIT[] and CINV[]
         for (int im = 0; im < kImages; ++im) {

@@ -55,10 +55,13 @@ constexpr uint32_t kVrCtr = kVrMeta + kVrW * kVrMetaWave;       // the workgroup
 constexpr uint32_t kVrTz = kVrCtr + 16;
 constexpr int kVrLds = kVrTz + kTzTableDwords * 4;               // 78.5 KiB: two workgroups per CU
 static_assert(2 * kVrLds <= 160 * 1024, "two workgroups per CU");
-// length-binned records (BIN): the same area and layout
+// length-binned records (BIN): the same area and layout, plus the x^(-8 c) tables for
+// c < 8 (tz_small_addr) -- 106.5 KiB: one workgroup per CU, the records entries' default
 constexpr uint32_t kVrMetaWaveBin = kVrMetaWave;
 constexpr uint32_t kVrCtrBin = kVrCtr;
-constexpr int kVrLdsBin = kVrLds;                                // two workgroups per CU as well
+constexpr uint32_t kVrTz7 = kVrLds;
+constexpr int kVrLdsBin = kVrTz7 + kTzSmallDwords * 4;
+static_assert(kVrLdsBin <= 160 * 1024, "records instance LDS");
 // BIN's index stash (two slots of kPk dwords per wave) fits the basis staging area
 static_assert(kVrW * 2 * 16 * 4 <= kVrBasisRows * 256, "index stash over the basis staging area");
 
@@ -298,10 +301,28 @@ __device__ __forceinline__ uint32_t vr_tz_mul(uint32_t reg, uint32_t tzbase) {
     return reg;
 }
 
+// reg x^(-8 c), 0 < c < 8: four lookups in the records instance's small tables
+// (kVrTz7, tz_small_addr); the unsteps they replace were one U-column lookup each,
+// every active lane on one bank (up to seven 16-way conflicts per group at 4 lanes)
+__device__ __forceinline__ uint32_t vr_tz7_mul(uint32_t reg, uint32_t c) {
+    const uint32_t base = kVrTz7 + 4096u * (c - 1u);
+    const uint32_t x0 = lds_load(base + 4u * (reg & 0xFFu));
+    const uint32_t x1 = lds_load(base + 1024u + 4u * ((reg >> 8) & 0xFFu));
+    const uint32_t x2 = lds_load(base + 2048u + 4u * ((reg >> 16) & 0xFFu));
+    const uint32_t x3 = lds_load(base + 3072u + 4u * (reg >> 24));
+    return xor3(x0, x1, x2) ^ x3;
+}
+
 // reg x^(-8 tz), tz < 32: the 16- and 8-byte parts by the tables, the rest by unsteps
+// (SMALL, the records instance: by the small tables)
+template <bool SMALL = false>
 __device__ __forceinline__ uint32_t vr_unstep_tz(uint32_t reg, uint32_t tz, uint32_t tzbase) {
     if (tz & 16u) reg = vr_tz_mul<0>(reg, tzbase);
     if (tz & 8u) reg = vr_tz_mul<1>(reg, tzbase);
+    if constexpr (SMALL) {
+        if (tz & 7u) reg = vr_tz7_mul(reg, tz & 7u);
+        return reg;
+    }
     if (tz & 4u) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) reg = unstep_byte(reg);
@@ -589,6 +610,11 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
              kVrStaging + 256u * wave);
     // waves 0..7: one KiB each of the zero-byte multiplier tables
     if (wave < static_cast<uint32_t>(kTzTableDwords / 256)) dma16(tb.tz + 256u * wave + 4u * lane, kVrTz + 1024u * wave);
+    if constexpr (BIN) {                                     // the small x^(-8 c) tables: 28 one-KiB chunks
+#pragma unroll
+        for (uint32_t c = wave; c < static_cast<uint32_t>(kTzSmallDwords / 256); c += kVrW)
+            dma16(tb.tz + kTzTableDwords + 256u * c + 4u * lane, kVrTz7 + 1024u * c);
+    }
     const uint32_t mbase = kVrMeta + (BIN ? kVrMetaWaveBin : kVrMetaWave) * wave;   // the wave's metadata area
     uint32_t mL = 0;                                         // metadata (read out at group switches)
     uint64_t moff = 0;
@@ -939,7 +965,7 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
             // lookup and about 6 VALU each).  All unsteps (round 2) cost 96 VALU for cfg2's
             // tz = 16, run whenever any of the wave's packets had a ragged end.
             if constexpr (!(ABL & 16))
-                if (lane_k() == 0u) reg = vr_unstep_tz(reg, tz, kVrTz);
+                if (lane_k() == 0u) reg = vr_unstep_tz<BIN != 0>(reg, tz, kVrTz);
             if constexpr (VF) {
                 desired = xor_lanes<0>(LG, desired);         // the slot's bytes, from at most two lanes
                 if (lane_k() == 0u && lane_p() < crem) {

@@ -775,7 +775,13 @@ def tz_tables() -> list[list[list[int]]]:
             for k in range(2)]
 
 
-def vr_unstep_tz(reg: int, tz: int, tabs=None) -> int:
+def tz_small_tables() -> list[list[list[int]]]:
+    """The records instance's small tables (HostTables::tz after the two above,
+    tz_small_addr): table c (1..7) byte b, entry v = (v << 8b) x^(-8 c)."""
+    return [[[mulmod(v << (8 * b), CINV[c]) for v in range(256)] for b in range(4)] for c in range(1, 8)]
+
+
+def vr_unstep_tz(reg: int, tz: int, tabs=None, small=None) -> int:
     """vr_unstep_tz: reg x^(-8 tz), tz < 32 -- the 16- and 8-byte parts as four
     table lookups each, the rest as zero-byte unsteps."""
     tabs = tabs or tz_tables()
@@ -783,6 +789,9 @@ def vr_unstep_tz(reg: int, tz: int, tabs=None) -> int:
         if tz & z:
             reg = tabs[k][0][reg & 0xFF] ^ tabs[k][1][(reg >> 8) & 0xFF] ^ tabs[k][2][(reg >> 16) & 0xFF] ^ \
                 tabs[k][3][reg >> 24]
+    if small is not None and tz & 7:                    # (the records instance: vr_tz7_mul)
+        t = small[(tz & 7) - 1]
+        return t[0][reg & 0xFF] ^ t[1][(reg >> 8) & 0xFF] ^ t[2][(reg >> 16) & 0xFF] ^ t[3][reg >> 24]
     for _ in range(tz & 7):
         reg = unstep_zero(reg)
     return reg

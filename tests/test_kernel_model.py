@@ -352,6 +352,17 @@ def test_tz_tables_equal_unsteps():
         assert km.vr_unstep_tz(reg, tz, tabs) == slow == km.mulmod(reg, km.CINV[tz]), (hex(reg), tz)
 
 
+def test_tz_small_tables_equal_unsteps():
+    """The records instance's tz correction: the 16 / 8 tables, then four lookups in the
+    x^(-8 c) table of c = tz mod 8 (vr_tz7_mul), equal tz zero-byte unsteps (= CINV[tz])."""
+    rng = random.Random(0x545B)
+    tabs, small = km.tz_tables(), km.tz_small_tables()
+    for tz in range(32):
+        for _ in range(12):
+            reg = rng.getrandbits(32)
+            assert km.vr_unstep_tz(reg, tz, tabs, small) == km.mulmod(reg, km.CINV[tz]), (hex(reg), tz)
+
+
 def _edge_mask_slot(regs, hs16, lo, hi):
     """crc32_vring.hip vr_edge_mask_slot on one lane: register R of (A, B) holds block
     bytes [oR, oR + 16), oA = hs16, oB = 16 - hs16; per dword i and bound b,
