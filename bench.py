@@ -139,6 +139,8 @@ class GpuEngine:
         import enethip
         if not torch.cuda.is_available():
             raise SystemExit("bench.py: no GPU visible -- the HIP path has no CPU fallback")
+        # one rank per GPU; more ranks than GPUs (the 2-rank test on a 1-GPU box) share them
+        device %= torch.cuda.device_count()
         torch.cuda.set_device(device)
         self.torch = torch
         self.ctx = enethip.Context(device, lanes, wgs, diag=diag)
