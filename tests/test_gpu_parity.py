@@ -539,6 +539,15 @@ def test_gather_binned(ctx, golden, oracle_lib):
         so = rng.integers(0, len(payload) - 100, size=4000).astype(np.uint64)
         f = np.arange(0, 4001, 4, dtype=np.uint32)
         cases.append((payload, so, sl, f, oracle_lib.gather(payload, so, sl, f)))
+    # an average of exactly 3 segments per DGRAM that only every other DGRAM has (2, 4, 2,
+    # 4, ...): the join's guess of DGRAM d's first segment (3 d) is wrong half the time
+    cnt2 = np.tile(np.array([2, 4], np.uint32), 1500)
+    sf2 = np.zeros(len(cnt2) + 1, np.uint32)
+    np.cumsum(cnt2, out=sf2[1:])
+    ns2 = int(sf2[-1])
+    sl2 = rng.integers(1, 1500, size=ns2).astype(np.uint32)
+    so2 = rng.integers(0, len(payload) - 1500, size=ns2).astype(np.uint64)
+    cases.append((payload, so2, sl2, sf2, oracle_lib.gather(payload, so2, sl2, sf2)))
     try:
         for lanes, wgs in ((0, 0), (4, 0), (8, 0), (0, 1), (0, 2)):
             ctx.set_tuning(lanes, wgs)
