@@ -463,7 +463,7 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
     probe = probe_bytes / (p_ms * 1e-3) / 1e9
 
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:    # (the CPU baseline: rank 0 at N = 1 only)
         cpu = (cpu_factory or cpu_baseline)(batches[0], args.cpu_seconds, args.cpu_threads)
 
     if rank == 0:

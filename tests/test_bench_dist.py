@@ -91,8 +91,24 @@ def test_two_rank_gloo_harness():
     per_rank = 6 * 2048 * 1200
     assert d["value"] == pytest.approx(2 * per_rank / (d["ms_per_step"] * 6e-3) / 2**30, rel=0.02)
     assert d["roofline"]["bound"] == "hbm" and d["roofline"]["peak"] == 8000.0
-    assert d["cpu_baseline"]["cores"] == 2 and d["cpu_baseline"]["kind"] == "port"
+    assert d["cpu_baseline"] is None                   # (timed at N = 1 only, on rank 0)
     assert d["config"]["workgroups_per_cu"] == ("default (2)" if d["config"]["steps_per_launch"] > 1 else "default (1)") and d["config"]["kernel_path"] == 0
+
+
+def test_one_rank_line_carries_the_cpu_baseline(monkeypatch):
+    """At N = 1 rank 0 times the CPU baseline and the line carries it (cores, kind)."""
+    import io
+    import contextlib
+    import bench
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE"):
+        monkeypatch.delenv(k, raising=False)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        bench.main(["--config", "small", "--rotate", "2", "--steps", "4", "--warmup", "1"],
+                   engine_factory=FakeEngine, cpu_factory=fake_cpu)
+    d = json.loads([l for l in buf.getvalue().splitlines() if l.startswith("{")][0])
+    assert d["n_gpus"] == 1
+    assert d["cpu_baseline"]["cores"] == 2 and d["cpu_baseline"]["kind"] == "port"
 
 
 def test_cpu_baseline_uses_the_affinity_cores():
