@@ -906,11 +906,11 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
         uint32_t d[8];
         if (cs == nedge) {                                   // head / tail pieces: keep [clz, ce) only
             const uint32_t q0 = 32u * (lane_k() + P * cst);              // windows < 2 GiB: differences fit int32
-            if constexpr (VF) {                              // (values: the slot fix-up works on copies)
+            if constexpr (VF) {                              // masked in place, then the slot fix-up on copies
+                if constexpr (!(ABL & 1))
+                    vr_edge_mask_slot<S>(lane & 16u, static_cast<int32_t>(clz - q0), static_cast<int32_t>(ce - q0));
                 u32x4 A, B;
                 vr_read_stage<S>(A, B);
-                if constexpr (!(ABL & 1))
-                    vr_edge_mask(A, B, make_vr_sched(lane).hs, static_cast<int32_t>(clz - q0), static_cast<int32_t>(ce - q0));
                 if (cps != ~0u) vr_slot_fix(A, B, make_vr_sched(lane).hs, static_cast<int32_t>(cps - q0), cconn, desired);
                 nedge = next_edge_m(cs + 1u);
                 vr_shuffle(rin, lane, A, B, d);
