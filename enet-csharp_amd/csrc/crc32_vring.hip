@@ -145,7 +145,7 @@ __device__ __forceinline__ void vr_wait_meta(uint32_t base, uint32_t p, uint32_t
 // Receive verify (protocol.cs:1052-1068) in the lane folding the slot: the slot's
 // bytes [rel, rel + 4) of this block (block byte offsets, may lie partly outside)
 // are collected into `desired` (at their byte positions of the slot) and replaced
-// by connectID's.  A, B in lane order (swapped when hs), as vr_edge_mask.
+// by connectID's.  A, B in lane order (swapped when hs: A holds block bytes [16, 32)).
 __device__ __forceinline__ void vr_slot_fix(u32x4& A, u32x4& B, uint32_t hs, int32_t rel, uint32_t conn,
                                             uint32_t& desired) {
     const bool sw = hs != 0;
@@ -188,22 +188,8 @@ __device__ __forceinline__ uint32_t vr_lane() {
     return l;
 }
 
-// Zero the bytes of a block that lie outside the packet, [lo, hi) kept (block
-// byte offsets, may lie outside [0, 32)).  A, B in lane order (swapped when hs).
-__device__ __forceinline__ void vr_edge_mask(u32x4& A, u32x4& B, uint32_t hs, int32_t lo, int32_t hi) {
-    const bool sw = hs != 0;
-    const u32x4 h0 = sw ? B : A, h1 = sw ? A : B;
-    uint32_t v[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-    const int l = max(-4, min(lo, 36));
-    const int h = max(-4, min(hi, 36));
-#pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] &= keep_mask(l, h, q);
-    const u32x4 n0 = {v[0], v[1], v[2], v[3]}, n1 = {v[4], v[5], v[6], v[7]};
-    A = sw ? n1 : n0;
-    B = sw ? n0 : n1;
-}
-
-// The same masking in place, on the landed slot registers themselves (the edge
+// Zero the bytes of a block that lie outside the packet, [lo, hi) kept (block byte
+// offsets, may lie outside [0, 32)), in place on the landed slot registers (the edge
 // path then folds them like any stage, vr_shuffle_slot): register R of the slot's
 // pair (A, B) holds block bytes [oR, oR + 16), oR = 0 or 16 by the lane's half swap
 // (hs16 = lane & 16: A holds [16, 32) when set).  Dword i of R keeps bytes j with
@@ -333,21 +319,6 @@ __device__ __forceinline__ uint32_t vr_unstep_tz(uint32_t reg, uint32_t tz, uint
     }
     if (tz & 1u) reg = unstep_byte(reg);
     return reg;
-}
-
-// mulmod (crc32_device.hpp) as a rolled loop: once per packet, so the few
-// cycles of loop overhead buy registers (the unrolled form set the kernel's peak)
-__device__ __forceinline__ uint32_t vr_mulmod(uint32_t a, uint32_t b) {
-    uint32_t p = 0;
-#pragma unroll 4
-    for (int j = 0; j < 32; ++j) {
-        const uint32_t m = static_cast<uint32_t>(static_cast<int32_t>(a) >> 31);
-        p = __builtin_amdgcn_bitop3_b32(p, b, m, 0x78);                 // p ^ (b & m)
-        const uint32_t r = static_cast<uint32_t>(static_cast<int32_t>(b << 31) >> 31);
-        b = __builtin_amdgcn_bitop3_b32(b >> 1, kPoly, r, 0x78);         // (b>>1) ^ (P & r)
-        a <<= 1;
-    }
-    return p;
 }
 
 template <int G>
