@@ -70,26 +70,27 @@ def _rank(rank, ws, port, q):
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_gloo_harness():
+@pytest.mark.parametrize("ws", [2, 4])
+def test_multi_rank_gloo_harness(ws):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_rank, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_rank, args=(r, ws, port, q)) for r in range(ws)]
     for p in ps:
         p.start()
     outs = dict(q.get(timeout=240) for _ in ps)
     for p in ps:
         p.join(60)
         assert p.exitcode == 0
-    assert outs[1].strip() == ""                       # only rank 0 prints
+    assert all(outs[r].strip() == "" for r in range(1, ws))   # only rank 0 prints
     lines = [l for l in outs[0].splitlines() if l.startswith("{")]
     assert len(lines) == 1
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["steps"] == 6 and d["scaling"] == "weak"
+    assert d["n_gpus"] == ws and d["steps"] == 6 and d["scaling"] == "weak"
     assert d["unit"] == "GiB/s" and d["higher_is_better"] is True and d["dtype"] == "u8"
-    # whole-job value: both ranks' bytes over the max-over-ranks span
+    # whole-job value: every rank's bytes over the max-over-ranks span
     per_rank = 6 * 2048 * 1200
-    assert d["value"] == pytest.approx(2 * per_rank / (d["ms_per_step"] * 6e-3) / 2**30, rel=0.02)
+    assert d["value"] == pytest.approx(ws * per_rank / (d["ms_per_step"] * 6e-3) / 2**30, rel=0.02)
     assert d["roofline"]["bound"] == "hbm" and d["roofline"]["peak"] == 8000.0
     assert d["cpu_baseline"] is None                   # (timed at N = 1 only, on rank 0)
     assert d["config"]["workgroups_per_cu"] == ("default (2)" if d["config"]["steps_per_launch"] > 1 else "default (1)") and d["config"]["kernel_path"] == 0
