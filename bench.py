@@ -282,39 +282,88 @@ class GpuEngine:
 # ------------------------------------------------------------------ CPU baseline
 
 def host_cores() -> int:
-    """The cores this process may run on (its affinity mask: cgroup / taskset limits
-    included), not the machine's count."""
+    """The cores this process may run on (its affinity mask: taskset limits included),
+    not the machine's count.  A cgroup CPU quota is not visible here: see
+    cgroup_cpu_quota()."""
     try:
         return len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         return os.cpu_count() or 1
 
 
-def cpu_baseline(batch, budget_s: float, threads: int = 0):
+def cgroup_cpu_quota():
+    """(CPUs the cgroup's CPU quota allows = quota / period, the file it came from), or
+    (None, file) when unlimited or unreadable.  cgroup v2 cpu.max of this process's own
+    group (then the root's), else v1 cfs_quota_us / cfs_period_us.  The affinity mask
+    can list far more cores than the quota lets the process use at once (a 16-CPU
+    share of a 256-thread host), and a thread count above the quota only time-slices."""
+    cands = []
+    try:
+        for line in open("/proc/self/cgroup"):
+            parts = line.strip().split(":", 2)
+            if len(parts) == 3 and parts[0] == "0":
+                cands.append(f"/sys/fs/cgroup{parts[2]}/cpu.max")
+    except OSError:
+        pass
+    cands.append("/sys/fs/cgroup/cpu.max")
+    for p in cands:
+        try:
+            q, per = open(p).read().split()[:2]
+        except (OSError, ValueError):
+            continue
+        return (None if q == "max" else float(q) / float(per)), p
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return (None if q <= 0 else q / per), "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"
+    except (OSError, ValueError):
+        return None, None
+
+
+def baseline_threads(requested: int = 0) -> tuple[int, dict]:
+    """Threads for the all-cores CPU leg: the affinity mask's cores, capped by the
+    cgroup quota (rounded up), unless `requested` says otherwise; plus what was read."""
+    aff = host_cores()
+    quota, src = cgroup_cpu_quota()
+    th = requested or (min(aff, max(1, int(np.ceil(quota)))) if quota else aff)
+    return th, {"affinity_cores": aff, "cgroup_cpu_quota": None if quota is None else round(quota, 2),
+                "cgroup_file": src}
+
+
+def cpu_baseline(batch, budget_s: float, threads: int = 0, runs: int = 5):
     """The oracle's C restatement of packet.cs:142-160 (kind "port": the C# reference
-    cannot run here), timed on this host on a bounded sample of the same batch: one
-    thread, and every core of the affinity mask (static packet partition, pthreads)."""
+    cannot run here), timed on this host on a bounded sample of the same batch, as
+    SURVEY §8d asks: one thread, and all the cores the process may use (static
+    contiguous packet partition, one pthread per core); the median of `runs` timed
+    runs each.  A run is one call over a sample sized to budget_s / runs seconds, so
+    every thread gets one contiguous multi-MB range (thread start is noise)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     lib = oracle.OracleLib()
-    threads = threads or host_cores()
-    res = {}
+    threads, info = baseline_threads(threads)
+    res = {"host": info}
     for label, th in (("1thread", 1), ("all", threads)):
-        # sample: the first packets of the batch, sized to ~budget_s of work
+        # calibration: the first packets of the batch, then a sample sized to one run
         n = batch.n
+        k = min(n, 4096 * th)
         t0 = time.perf_counter()
-        out = lib.batch(batch.payload, batch.off[: min(n, 4096)], batch.lens[: min(n, 4096)], threads=th)
+        out = lib.batch(batch.payload, batch.off[:k], batch.lens[:k], threads=th)
         dt = max(time.perf_counter() - t0, 1e-6)
-        rate = float(batch.lens[: min(n, 4096)].astype(np.uint64).sum()) / dt
-        sample_n = int(min(n, max(4096, rate * budget_s / max(1.0, float(batch.lens.mean())))))
-        reps = max(1, int(rate * budget_s / max(1.0, float(batch.lens[:sample_n].astype(np.uint64).sum()))))
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            out = lib.batch(batch.payload, batch.off[:sample_n], batch.lens[:sample_n], threads=th)
-        dt = time.perf_counter() - t0
-        nbytes = float(batch.lens[:sample_n].astype(np.uint64).sum()) * reps
-        res[label] = dict(gibps=nbytes / dt / GIB, threads=th, packets=sample_n, reps=reps, seconds=dt)
+        rate = float(batch.lens[:k].astype(np.uint64).sum()) / dt
+        per_run = budget_s / max(1, runs)
+        sample_n = int(min(n, max(k, rate * per_run / max(1.0, float(batch.lens.mean())))))
+        nb = float(batch.lens[:sample_n].astype(np.uint64).sum())
+        reps = max(1, int(rate * per_run / max(1.0, nb)))       # (the whole batch is shorter than a run)
+        rates = []
+        for _ in range(max(1, runs)):
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                out = lib.batch(batch.payload, batch.off[:sample_n], batch.lens[:sample_n], threads=th)
+            rates.append(nb * reps / (time.perf_counter() - t0) / GIB)
+        res[label] = dict(gibps=float(np.median(rates)), threads=th, packets=sample_n, reps=reps, runs=len(rates),
+                          spread=[round(min(rates), 3), round(max(rates), 3)])
         del out
+    res["speedup"] = res["all"]["gibps"] / max(res["1thread"]["gibps"], 1e-9)
     return res
 
 
@@ -372,9 +421,10 @@ def kernel_name(args, list_launch: bool = False) -> str:
 
 def load_traffic(cfg: str, binned: bool = False):
     """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/), or None
-    when there is none for this entry (a file marked "binned" is the length-binned
-    entry's; unmarked ones are the plain / batch-list entry's)."""
-    p = os.path.join(ROOT, "profiles", f"traffic_{cfg}.json")
+    when there is none for this entry: profiles/traffic_<cfg>.json is the plain /
+    batch-list entry's, traffic_<cfg>_binned.json the length-binned entry's, and each
+    file's "binned" tag must agree with its name."""
+    p = os.path.join(ROOT, "profiles", f"traffic_{cfg}{'_binned' if binned else ''}.json")
     try:
         doc = json.load(open(p))
     except (OSError, ValueError):
@@ -382,10 +432,70 @@ def load_traffic(cfg: str, binned: bool = False):
     return doc if bool(doc.get("binned", False)) == bool(binned) else None
 
 
+def cpu_line(cpu: dict) -> dict:
+    """The bench line's cpu_baseline object from cpu_baseline()'s result."""
+    a, one, host = cpu["all"], cpu["1thread"], cpu["host"]
+    quota = host.get("cgroup_cpu_quota")
+    return {
+        "value": round(a["gibps"], 3),
+        "unit": "GiB/s",
+        "cores": a["threads"],
+        "kind": "port",
+        "sample": (f"oracle C restatement of packet.cs:142-160 (byte-serial loop, one ENetBuffer per packet), "
+                   f"first {a['packets']} packets of the cfg batch x {a['reps']} per run, median of {a['runs']} "
+                   f"runs (spread {a['spread'][0]}-{a['spread'][1]} GiB/s) on {a['threads']} threads; "
+                   f"1 thread: {one['gibps']:.3f} GiB/s (median of {one['runs']}); measured speed-up "
+                   f"{cpu['speedup']:.1f}x over 1 thread; host: {host['affinity_cores']} cores in the affinity "
+                   f"mask, cgroup CPU quota {quota if quota is not None else 'none'}"
+                   f"{' (' + host['cgroup_file'] + ')' if host.get('cgroup_file') else ''}"),
+        "speedup_vs_1thread": round(cpu["speedup"], 2),
+        "one_thread": round(one["gibps"], 3),
+        "cgroup_cpu_quota": quota,
+        "affinity_cores": host["affinity_cores"],
+    }
+
+
+def _rank_main(rank: int, n: int, port: int, argv, engine_factory, cpu_factory):
+    """One self-launched rank (spawn start method: a fresh interpreter that has not
+    touched the GPU)."""
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.exit(main(argv, engine_factory, cpu_factory))
+
+
+def spawn_ranks(n: int, argv, engine_factory=None, cpu_factory=None) -> int:
+    """`bench.py --gpus N` with no launcher around it: start N rank processes (one per
+    GPU, as torch.distributed.run would: RANK / LOCAL_RANK / WORLD_SIZE, rendezvous on
+    127.0.0.1) and return the worst exit code.  This process never initialises the GPU,
+    and the ranks are children (no exec).  Rank 0 prints the one line."""
+    import socket
+    import multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=_rank_main, args=(r, n, port, argv, engine_factory, cpu_factory)) for r in range(n)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join()
+    codes = [p.exitcode for p in ps]
+    bad = [c for c in codes if c != 0]
+    if bad:
+        print(f"bench.py: self-launched ranks exited with {codes}", file=sys.stderr)
+        return 1
+    return 0
+
+
 def main(argv=None, engine_factory=None, cpu_factory=None):
     args = parse(argv)
     ws, rank, local = dist_env()
+    if ws <= 1 and args.gpus > 1:
+        # no launcher: measure N GPUs by starting the N ranks here (never print a
+        # one-rank line for --gpus N)
+        return spawn_ranks(args.gpus, argv if argv is not None else sys.argv[1:], engine_factory, cpu_factory)
     if ws > 1 and args.gpus != ws:
+        print(f"bench.py: --gpus {args.gpus} under a launcher of {ws} ranks: measuring {ws}", file=sys.stderr)
         args.gpus = ws
     dist = dist_init(ws)
     batches = make_batches(args.config, args.rotate, rank, ws)
@@ -517,15 +627,7 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
                 "read_probe_GBps": round(probe, 1),
             },
             "sustained": sus,
-            "cpu_baseline": None if cpu is None else {
-                "value": round(cpu["all"]["gibps"], 3),
-                "unit": "GiB/s",
-                "cores": cpu["all"]["threads"],
-                "kind": "port",
-                "sample": f"oracle C restatement of packet.cs:142-160, first {cpu['all']['packets']} packets "
-                          f"of the cfg batch x {cpu['all']['reps']} reps on {cpu['all']['threads']} threads "
-                          f"(the affinity mask's cores); 1 thread: {cpu['1thread']['gibps']:.3f} GiB/s",
-            },
+            "cpu_baseline": None if cpu is None else cpu_line(cpu),
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

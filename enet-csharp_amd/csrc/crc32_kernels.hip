@@ -1253,12 +1253,13 @@ int setup_stream() {
 }
 
 // vring workgroups per CU of one launch (enet_hip_set_tuning's workgroups_per_cu,
-// at most 2: the LDS and 64-VGPR budget of two 16-wave workgroups).  Default (0):
-// two for a launch of several batches, one for a single batch.  Measured on one box
-// (profiles/r03_wgs_ab/): 5-batch lists 5270-5360 GiB/s at two against 5153-5213 at
-// one; single-batch launches 5183 at one against 4301-4918 at two.
+// clamped to 2: the LDS and 64-VGPR budget of two 16-wave workgroups; values 3..8
+// are for the direct and gather grids and mean 2 here, as they did before round 3).
+// Default (0): two for a launch of several batches, one for a single batch.  Measured
+// on one box (profiles/r03_wgs_ab/): 5-batch lists 5270-5360 GiB/s at two against
+// 5153-5213 at one; single-batch launches 5183 at one against 4301-4918 at two.
 int vring_wgs(const enet_hip_context* ctx, size_t batches) {
-    if (ctx->wgs_per_cu == 1 || ctx->wgs_per_cu == 2) return ctx->wgs_per_cu;
+    if (ctx->wgs_per_cu >= 1) return std::min(ctx->wgs_per_cu, 2);
     return batches > 1 ? 2 : 1;
 }
 bool vring_path(const enet_hip_context* ctx) {

@@ -60,7 +60,9 @@ static_assert(2 * kVrLds <= 160 * 1024, "two workgroups per CU");
 constexpr uint32_t kVrMetaWaveBin = kVrMetaWave;
 constexpr uint32_t kVrCtrBin = kVrCtr;
 constexpr uint32_t kVrTz7 = kVrLds;
-constexpr int kVrLdsBin = kVrTz7 + kTzSmallDwords * 4;
+// ... and the workgroup's 16 partial maxima of the binned gather's tile counts
+constexpr uint32_t kVrTileMax = kVrTz7 + kTzSmallDwords * 4;
+constexpr int kVrLdsBin = kVrTileMax + kVrW * 4;
 static_assert(kVrLdsBin <= 160 * 1024, "records instance LDS");
 // BIN's index stash (two slots of kPk dwords per wave) fits the basis staging area
 static_assert(kVrW * 2 * 16 * 4 <= kVrBasisRows * 256, "index stash over the basis staging area");
@@ -493,14 +495,26 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     const uint64_t zero = reinterpret_cast<uint64_t>(tb.zero);
     // batch b's packets and the launch's groups; BIN with tile counts (the binned
     // gather): the ranks up to the fullest tile's, R = ceil(max_t count_t / kPk), i.e.
-    // R x tiles groups, every record of them valid (kept or empty padding).  Each wave
-    // reduces the counts itself (a few KiB, from L2): no barrier, no global atomic.
+    // R x tiles groups, every record of them valid (kept or empty padding).  The
+    // workgroup reduces the counts once: wave w takes tiles w, w + 16, ... (from L2),
+    // its maximum goes to LDS, one raw barrier, every wave reads the 16 maxima (no
+    // global atomic; a launch over tens of millions of segments reads each count
+    // once per workgroup, not once per wave).
     uint64_t n0 = bl.b[0].n, ngroups_all = bl.groups;
     if constexpr (BIN) {
         if (bl.tile_counts) {
             uint32_t m = 0;
-            for (uint32_t t = threadIdx.x & 63u; t < bl.tiles; t += 64u) m = max(m, bl.tile_counts[t]);
-            const uint32_t r = (wave_max_u(m) + kPk - 1u) / kPk;
+            for (uint32_t t = wave * 64u + (threadIdx.x & 63u); t < bl.tiles; t += 64u * kVrW)
+                m = max(m, bl.tile_counts[t]);
+            m = wave_max_u(m);
+            if ((threadIdx.x & 63u) == 0u) *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(
+                static_cast<uintptr_t>(kVrTileMax + 4u * wave)) = m;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the store is in LDS
+            __builtin_amdgcn_s_barrier();
+            uint32_t mm = 0;
+#pragma unroll
+            for (uint32_t w = 0; w < kVrW; ++w) mm = max(mm, lds_load(kVrTileMax + 4u * w));
+            const uint32_t r = (mm + kPk - 1u) / kPk;
             ngroups_all = static_cast<uint64_t>(r) * bl.tiles;
             n0 = ngroups_all * kPk;
         }

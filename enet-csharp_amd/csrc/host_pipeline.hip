@@ -70,7 +70,12 @@ struct Chunk {
 
 // Consecutive packets, about kChunkBytes of span each.  Offsets that are not
 // ascending (spans overlapping or far apart) fall back to one chunk over the
-// whole arena (every byte copied once either way).
+// whole arena (every byte copied once either way).  So do plans of many small
+// chunks -- packets alternating between distant regions make every chunk one
+// packet long while the summed spans stay near byteCount, and a chunk is a launch,
+// three copies and (from chunk 2 on) an event wait: more chunks than a plan of
+// full chunks would need (2 ceil(byteCount / kChunkBytes) + 2, or an average under
+// 64 packets per chunk) take the one-chunk plan.
 std::vector<Chunk> plan_chunks(const uint64_t* off, const uint32_t* len, size_t n, size_t byteCount) {
     std::vector<Chunk> ch;
     uint64_t covered = 0;
@@ -88,7 +93,9 @@ std::vector<Chunk> plan_chunks(const uint64_t* off, const uint32_t* len, size_t 
         ch.push_back(c);
         p = c.p1;
     }
-    if (covered > byteCount + byteCount / 8 + 4096) return {Chunk{0, n, 0, byteCount}};
+    const size_t full = 2 * ((byteCount + kChunkBytes - 1) / kChunkBytes) + 2;
+    if (covered > byteCount + byteCount / 8 + 4096 || (ch.size() > full && ch.size() * 64 > n))
+        return {Chunk{0, n, 0, byteCount}};
     return ch;
 }
 
@@ -200,32 +207,47 @@ int enet_hip_crc32_gather_binned_host(enet_hip_context* ctx, const uint8_t* byte
         if (segOffsets[s] > byteCount || segLengths[s] > byteCount - segOffsets[s])
             return -static_cast<int>(hipErrorInvalidValue);
     const size_t ns = s_hi - s_lo;
+    // only the arena span the used segments cover crosses PCIe ([lo, hi), 16-byte
+    // aligned start so the device copy keeps the host's alignment mod 16); their
+    // offsets are rebased onto it.  A send loop that stamps a long arena in slices
+    // then copies each slice's bytes, not the whole arena per call.
+    uint64_t lo = byteCount, hi = 0;
+    for (size_t s = s_lo; s < s_hi; ++s)
+        if (segLengths[s]) {
+            lo = std::min<uint64_t>(lo, segOffsets[s]);
+            hi = std::max<uint64_t>(hi, segOffsets[s] + segLengths[s]);
+        }
+    if (hi <= lo) lo = hi = 0;
+    lo &= ~uint64_t(15);
+    const size_t span = static_cast<size_t>(hi - lo);
     std::lock_guard<std::mutex> lk(ctx->mu);
     ENH_CHECK(hipSetDevice(ctx->device));
     int rc;
     if ((rc = pipeline_init(ctx))) return rc;
-    // device: [arena | segOffsets | segLengths | segFirst | out], then the binned workspace
-    const size_t a = align16(byteCount + 16), so = align16(8 * ns + 8), sl = align16(4 * ns + 4);
+    // device: [arena span | segOffsets | segLengths | segFirst | out], then the binned workspace
+    const size_t a = align16(span + 16), so = align16(8 * ns + 8), sl = align16(4 * ns + 4);
     const size_t sf = align16(4 * (dgramCount + 1)), ob = align16(4 * dgramCount);
     if ((rc = ensure_device(&ctx->d_pipe[0], &ctx->d_pipe_cap[0], a + so + sl + sf + ob))) return rc;
     const size_t wsb = enet_hip_gather_binned_workspace_size(ns);
     if ((rc = ensure_device(&ctx->d_ws, &ctx->d_ws_cap, wsb + 16))) return rc;
-    // pinned staging: segFirst rebased to s_lo
-    if ((rc = ensure_pinned(&ctx->h_pipe[1], &ctx->h_pipe_cap[1], sf))) return rc;
+    // pinned staging: segFirst rebased to s_lo, then the segment offsets rebased to lo
+    if ((rc = ensure_pinned(&ctx->h_pipe[1], &ctx->h_pipe_cap[1], sf + so))) return rc;
     uint32_t* h_sf = reinterpret_cast<uint32_t*>(ctx->h_pipe[1]);
+    uint64_t* h_so = reinterpret_cast<uint64_t*>(ctx->h_pipe[1] + sf);
     for (size_t d = 0; d <= dgramCount; ++d) h_sf[d] = static_cast<uint32_t>(segFirst[d] - s_lo);
+    for (size_t s = 0; s < ns; ++s) h_so[s] = segLengths[s_lo + s] ? segOffsets[s_lo + s] - lo : 0u;
     uint8_t* d = ctx->d_pipe[0];
     uint64_t* d_so = reinterpret_cast<uint64_t*>(d + a);
     uint32_t* d_sl = reinterpret_cast<uint32_t*>(d + a + so);
     uint32_t* d_sf = reinterpret_cast<uint32_t*>(d + a + so + sl);
     uint32_t* d_out = reinterpret_cast<uint32_t*>(d + a + so + sl + sf);
     hipStream_t s0 = ctx->pipe[0], s1 = ctx->pipe[1];
-    // the arena in two halves on two streams (two copy engines), the metadata behind
-    const size_t half = (byteCount / 2 + 4095) & ~size_t(4095);
-    ENH_CHECK(hipMemcpyAsync(d, bytes, std::min(half, byteCount), hipMemcpyHostToDevice, s0));
-    if (byteCount > half) ENH_CHECK(hipMemcpyAsync(d + half, bytes + half, byteCount - half, hipMemcpyHostToDevice, s1));
+    // the span in two halves on two streams (two copy engines), the metadata behind
+    const size_t half = (span / 2 + 4095) & ~size_t(4095);
+    if (span) ENH_CHECK(hipMemcpyAsync(d, bytes + lo, std::min(half, span), hipMemcpyHostToDevice, s0));
+    if (span > half) ENH_CHECK(hipMemcpyAsync(d + half, bytes + lo + half, span - half, hipMemcpyHostToDevice, s1));
     if (ns) {
-        ENH_CHECK(hipMemcpyAsync(d_so, segOffsets + s_lo, 8 * ns, hipMemcpyHostToDevice, s1));
+        ENH_CHECK(hipMemcpyAsync(d_so, h_so, 8 * ns, hipMemcpyHostToDevice, s1));
         ENH_CHECK(hipMemcpyAsync(d_sl, segLengths + s_lo, 4 * ns, hipMemcpyHostToDevice, s1));
     }
     ENH_CHECK(hipMemcpyAsync(d_sf, h_sf, 4 * (dgramCount + 1), hipMemcpyHostToDevice, s1));

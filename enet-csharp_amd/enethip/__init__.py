@@ -247,12 +247,19 @@ class Context:
         kernel; the other paths (tuning sweeps) exist in the diagnostics library only."""
         _check("enet_hip_set_kernel_path", self.lib.enet_hip_set_kernel_path(self.handle, int(path)))
 
+    def _need_diag(self, what: str) -> None:
+        if not self.lib.enet_hip_is_diagnostics_build():
+            raise ENetHipError(f"{what}: diagnostics entry point; open the Context with diag=True "
+                               "(libenethip_diag.so) -- libenethip.so does not export it")
+
     def diag_ablation(self, mode: int) -> None:
         """Diagnostics only: 1 = no lookups, 2 = no DMA (wrong CRCs by design)."""
+        self._need_diag("enet_hip_diag_ablation")
         _check("enet_hip_diag_ablation", self.lib.enet_hip_diag_ablation(self.handle, int(mode)))
 
     def diag_trace(self, device_ptr) -> None:
         """Diagnostics only: per-wave timeline buffer (4 x u64 per wave) or None."""
+        self._need_diag("enet_hip_diag_trace")
         p = _ptr(device_ptr) if device_ptr is not None else None
         _check("enet_hip_diag_trace", self.lib.enet_hip_diag_trace(self.handle, p))
 

@@ -72,15 +72,18 @@ ENET_HIP_API const char* enet_hip_error_string(int code);
 
 /* Tuning knobs (0 = automatic).  lanes_per_packet: 1,2,4,...,64 lanes share one
  * packet (a power of two; default 8, and 4 for the length-binned entries);
- * workgroups_per_cu: resident workgroups per CU (the VGPR-ring kernel runs 1 or
- * 2; default 2 for a launch of several batches, 1 for a single batch; the direct /
- * gather grids are sized for it). */
+ * workgroups_per_cu (0..8): resident workgroups per CU.  The VGPR-ring kernel runs
+ * 1 or 2 (values above 2 mean 2 there; default 2 for a launch of several batches,
+ * 1 for a single batch); the direct and gather grids use the value as given. */
 ENET_HIP_API int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgroups_per_cu);
 
 /* Kernel path for the packet batch entry points (0 = default): checksum batches
- * at 4 or 8 lanes per packet run the VGPR-ring kernel (crc32_vring.hip), receive
- * verify and the length-binned entries the lean LDS-DMA kernel (crc32_lean.hip),
- * 16 lanes the LDS-ring stream kernel, other lane counts the direct kernel.
+ * at 4 or 8 lanes per packet run the VGPR-ring kernel (crc32_vring.hip); so do
+ * receive verify at 8 lanes (its verify instance) and the length-binned checksum
+ * and gather entries (its records instance, 4 lanes by default).  The lean LDS-DMA
+ * kernel (crc32_lean.hip) serves receive verify at 4 lanes and the length-binned
+ * verify; 16 lanes run the LDS-ring stream kernel, other lane counts the direct
+ * kernel.
  * Every path gives the same (correct) checksums.  Built in every library: 1 =
  * direct loads only, 2 = the stream kernel, 13 = the lean kernel, 17 = the vring
  * kernel (for the length-binned entries: its records instance).  Tuning sweeps,
@@ -166,9 +169,9 @@ ENET_HIP_API int enet_hip_verify_batch_device(enet_hip_context* ctx, const uint8
  * each entry names one batch exactly as enet_hip_verify_batch_device's arguments
  * do (device pointers; computed may be NULL).  Same ok[] / computed[] as one
  * enet_hip_verify_batch_device call per batch, in one kernel launch per 32
- * batches (4 or 8 lanes per packet: the lean kernel's list instance; other lane
- * counts: one launch per batch), so the per-launch start and drain are paid once
- * per launch.  Batches may not share ok / computed ranges.  Async;
+ * batches (8 lanes per packet, the default: the VGPR-ring kernel's verify
+ * instance; 4 lanes: the lean kernel's list instance; other lane counts: one
+ * launch per batch), so the per-launch start and drain are paid once per launch.  Batches may not share ok / computed ranges.  Async;
  * graph-capturable. */
 typedef struct {
     const uint8_t* bytes;

@@ -53,6 +53,13 @@ def test_batch_host_chunks_and_orders(ctx, oracle_lib):  # noqa: F811
     perm = np.random.default_rng(63).permutation(b.n)
     assert (ctx.crc32_batch_host(b.payload, b.off[perm], b.lens[perm]) == exp[perm]).all()
     assert (ctx.crc32_batch_host(b.payload, b.off[7:8], b.lens[7:8]) == exp[7:8]).all()
+    # packets alternating between two regions 24 MiB apart: every span
+    # chunk would hold one packet; the plan takes the one-chunk form instead
+    H, n2 = 24 << 20, 4000
+    arena = np.frombuffer(np.random.default_rng(67).bytes(H + 64 * n2), dtype=np.uint8)
+    off2 = np.array([(i // 2) * 64 + (H if i & 1 else 0) for i in range(n2)], np.uint64)
+    len2 = np.full(n2, 64, np.uint32)
+    assert (ctx.crc32_batch_host(arena, off2, len2) == oracle_lib.batch(arena, off2, len2)).all()
     with pytest.raises(enethip.ENetHipError):                # a packet past the arena: rejected
         ctx.crc32_batch_host(b.payload[:100], b.off[:2], np.array([50, 60], np.uint32) + 50)
 

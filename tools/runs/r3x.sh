@@ -29,10 +29,10 @@ python3 tools/traffic.py $out/cfg2_fetch 78643200 5 $out/traffic_cfg2.json || ex
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $out/cfg3b_fetch -o run --output-format csv \
   -- python3 tools/profile_one.py --config cfg3 --binned --reps 8 --probe > $out/cfg3b_fetch.log 2>&1 || exit 1
 python3 tools/traffic_sum.py $out/cfg3b_fetch --bytes 192275835 --calls 8 --probe-bytes 192275824 \
-  --what "cfg3 binned (enet_hip_crc32_batch_device_binned, default: vring records, 4 lanes)" --out $out/traffic_cfg3.json || exit 1
+  --what "cfg3 binned (enet_hip_crc32_batch_device_binned, default: vring records, 4 lanes)" --out $out/traffic_cfg3_binned.json || exit 1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $out/cfg5_fetch -o run --output-format csv \
   -- python3 tools/gather_bench.py --only gather_binned --reps 8 --probe 4 > $out/cfg5_fetch.log 2>&1 || exit 1
 python3 tools/traffic_sum.py $out/cfg5_fetch --bytes 274857984 --calls 12 --probe-bytes 274857984 \
-  --what "cfg5 binned gather (enet_hip_crc32_gather_binned_device, default: split, tile counts)" --out $out/traffic_cfg5.json || exit 1
+  --what "cfg5 binned gather (enet_hip_crc32_gather_binned_device, default: split, tile counts)" --out $out/traffic_cfg5_binned.json || exit 1
 bash tools/pmc_mix.sh $out/pmc_cfg3b --config cfg3 --binned --reps 8 > $out/pmc_cfg3b.log 2>&1 || exit 1
 bash tools/pmc_mix.sh $out/pmc_cfg2 --list 5 --wgs 2 --reps 20 > $out/pmc_cfg2.log 2>&1 || exit 1

@@ -52,7 +52,9 @@ def main():
         "per_kernel_dispatches": {k: len(v) for k, v in per_kernel.items()},
         "hbm_bytes_per_call": round(hbm),
         "hbm_bytes_per_batch": round(hbm),                 # (one batch per call)
-        "binned": a.binned,
+        # the length-binned entries run bin_tile_kernel: tag them whatever the flag said
+        # (bench.py --binned reads traffic_<cfg>_binned.json and checks this tag)
+        "binned": bool(a.binned or any("bin_tile_kernel" in k for k in per_kernel)),
         "traffic_over_algorithmic": round(hbm / a.bytes, 4),
         "probe_calibration": (round(sum(probe) / len(probe) * 2048 / a.probe_bytes, 4)
                               if probe and a.probe_bytes else None),
