@@ -25,11 +25,29 @@ def main():
     rows = [r for r in csv.DictReader(open(path)) if a.match in r["Kernel_Name"]
             and (not a.grid or int(r["Grid_Size_X"]) == a.grid)]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    us = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows[a.skip:]]
+    kept = rows[a.skip:]
+    us = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in kept]
+    # overlap: dispatches on several streams run concurrently, so each one's own
+    # duration counts the time it shared with its neighbours; the union of the
+    # intervals is the time the kernel occupied the GPU at all
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in kept)
+    union, cur = 0, None
+    for s0, e0 in iv:
+        if cur is None or s0 > cur[1]:
+            if cur is not None:
+                union += cur[1] - cur[0]
+            cur = [s0, e0]
+        else:
+            cur[1] = max(cur[1], e0)
+    if cur is not None:
+        union += cur[1] - cur[0]
     doc = {"trace": path, "match": a.match, "skipped": a.skip, "dispatches": len(us),
            "mean_us": round(statistics.mean(us), 3) if us else None,
            "median_us": round(statistics.median(us), 3) if us else None,
-           "min_us": round(min(us), 3) if us else None, "max_us": round(max(us), 3) if us else None}
+           "min_us": round(min(us), 3) if us else None, "max_us": round(max(us), 3) if us else None,
+           "union_us": round(union / 1e3, 3) if iv else None,
+           "union_per_dispatch_us": round(union / 1e3 / len(iv), 3) if iv else None,
+           "span_us": round((max(e for _, e in iv) - iv[0][0]) / 1e3, 3) if iv else None}
     print(json.dumps(doc))
     if a.out:
         json.dump(doc, open(a.out, "w"), indent=1)
