@@ -396,13 +396,15 @@ def make_batches(cfg: str, rotate: int, rank: int, world: int = 1):
     return out
 
 
-PRODUCT_PATHS = (0, 1, 2, 13, 17)          # built in libenethip.so (the rest: libenethip_diag.so)
+PRODUCT_PATHS = (0, 1, 2, 13, 17, 22, 23)  # built in libenethip.so (the rest: libenethip_diag.so)
 
 
 def kernel_name(args, list_launch: bool = False) -> str:
     """The dominant kernel of the measured entry point (as rocprofv3 names it:
     crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT>)."""
     path = getattr(args, "path", 0)
+    if path in (22, 23) and not args.binned:
+        return f"crc32_lin_kernel<{lin_abl(args.ablate)}, {1 if path == 22 else 0}>"
     if list_launch and path == 13 and args.lanes in (0, 4, 8) and not args.binned:
         # batch lists: the lean kernel's list instance, 8 lanes per packet unless set
         return f"crc32_lean_list_kernel<{3 if args.lanes in (0, 8) else 2}, 16, 2>"
@@ -417,6 +419,12 @@ def kernel_name(args, list_launch: bool = False) -> str:
         return "crc32_stream_kernel / crc32_direct_kernel"
     nt, rot = (1 if path == 18 else 0), (1 if path == 21 else 0)
     return f"crc32_vring_kernel<{lg}, 0, {nt}, 0, 0, 0, {rot}, 0>"
+
+
+def lin_abl(ablate: int) -> int:
+    """The linear kernel's ablation instance for an enet_hip_diag_ablation value."""
+    v = (ablate >> 11) & 255
+    return (3 if v & 2 else 1) if v & 1 else 0
 
 
 def load_traffic(cfg: str, binned: bool = False):

@@ -29,6 +29,7 @@
 
 #include "crc32_device.hpp"
 #include "crc32_math.hpp"
+#include "crc32_lin.hpp"
 #include "crc32_lean.hpp"
 #include "crc32_vring.hpp"
 #include "crc32_stream_common.hpp"
@@ -974,12 +975,13 @@ constexpr int kImages = 4;                             // P = 1, 4, 8, 16
 constexpr int kImageP[kImages] = {1, 4, 8, 16};
 
 struct HostTables {
-    std::vector<uint32_t> image, xn, init, basis, basis2, tz;
+    std::vector<uint32_t> image, xn, init, basis, basis2, tz, lin;
     bool basis_ok = true;   // the bases rebuild every image dword the lean / vring kernels read
     HostTables()
         : image(static_cast<size_t>(kImages) * kImageDwords), xn(2 * kXnEntries), init(64),
           basis(static_cast<size_t>(kImages) * kBasisDwords), basis2(static_cast<size_t>(kImages) * kVrBasisDwords),
-          tz(kTzTableDwords + kTzSmallDwords) {
+          tz(kTzTableDwords + kTzSmallDwords), lin(kImageDwords) {
+        if (lin_image(lin.data())) basis_ok = false;
         init[0] = 0xFFFFFFFFu;
         for (int r = 1; r < 64; ++r) init[r] = unstep_zero(init[r - 1]);
         std::vector<uint32_t> cinv(kCinvEntries);
@@ -1190,7 +1192,9 @@ constexpr int kVringAltPath = kVringPath + 1;           // the same with nontemp
 constexpr int kVringWalkPath = kVringAltPath + 1;       // vring, workgroups walking contiguous group ranges
 constexpr int kVringWalkAltPath = kVringWalkPath + 1;   // the same with nontemporal stage loads
 constexpr int kVringTailFirstPath = kVringWalkAltPath + 1;   // vring, the tail-first stage order
-constexpr int kMaxPath = kVringTailFirstPath;
+constexpr int kLinPath = kVringTailFirstPath + 1;      // crc32_lin.hip: linear stream, nontemporal tile DMA
+constexpr int kLinPlainPath = kLinPath + 1;            // the same with default-policy tile DMA
+constexpr int kMaxPath = kLinPlainPath;
 
 // Paths this library builds: all in the diagnostics library; in the product one
 // the default (0), direct (1), stream geometry 0 (2), lean geometry 0 and vring.
@@ -1198,8 +1202,16 @@ bool path_built(int path) {
 #ifdef ENET_HIP_DIAG
     return path >= 0 && path <= kMaxPath;
 #else
-    return path == 0 || path == 1 || path == 2 || path == kLeanPath0 || path == kVringPath;
+    return path == 0 || path == 1 || path == 2 || path == kLeanPath0 || path == kVringPath || path == kLinPath ||
+           path == kLinPlainPath;
 #endif
+}
+bool lin_path(const enet_hip_context* ctx) { return ctx->path == kLinPath || ctx->path == kLinPlainPath; }
+// the linear kernel's ablation (diagnostics: enet_hip_diag_ablation 2048 = no boundary
+// passes, + 4096 = no fold lookups either; wrong CRCs by design)
+int lin_abl(const enet_hip_context* ctx) { return (ctx->vr_abl & 1) ? ((ctx->vr_abl & 2) ? 3 : 1) : 0; }
+int lin_list(enet_hip_context* ctx, const VrBatches& bl, hipStream_t st) {
+    return lin_launch_list(ctx->num_cus, st, bl, ctx->d_lin, ctx->d_zero, lin_abl(ctx), ctx->path == kLinPath);
 }
 
 template <size_t I = 0>
@@ -1311,6 +1323,12 @@ int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStr
     // length-binned records (its records instance: cfg3 at 4 lanes 59.4 us against the
     // lean kernel's 63.3 since the in-place edge masks, profiles/r03_cfg3_binned/;
     // the lean kernel on paths 13-16)
+    if (mode == 0 && !pa.meta4 && ctx->ablation == 0 && lin_path(ctx)) {
+        VrBatches bl{};
+        bl.count = 1;
+        bl.b[0] = VrBatch{pa.bytes, pa.off, pa.len, pa.out, pa.n, 0u};
+        return lin_list(ctx, bl, st);
+    }
     if (mode == 0 && (pa.lg == 2 || pa.lg == 3) && ctx->ablation == 0 && vring_path(ctx))
         return vring_launch(pa.lg, ctx->num_cus * vring_wgs(ctx, 1),
                             pa.meta4 ? VrVariant{} : vring_variant(ctx, false), st, pa, tb, ctx->d_basis2);
@@ -1404,7 +1422,10 @@ int enet_hip_context_create(int device, enet_hip_context** out) {
         if ((rc = herr(hipMemcpy(ctx->d_tz, ht.tz.data(), ht.tz.size() * 4, hipMemcpyHostToDevice)))) break;
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_basis2), ht.basis2.size() * 4)))) break;
         if ((rc = herr(hipMemcpy(ctx->d_basis2, ht.basis2.data(), ht.basis2.size() * 4, hipMemcpyHostToDevice)))) break;
+        if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_lin), ht.lin.size() * 4)))) break;
+        if ((rc = herr(hipMemcpy(ctx->d_lin, ht.lin.data(), ht.lin.size() * 4, hipMemcpyHostToDevice)))) break;
         if ((rc = vring_setup())) break;
+        if ((rc = lin_setup())) break;
         if ((rc = setup_stream())) break;
 #ifdef ENET_HIP_DIAG
         if ((rc = setup_vstream())) break;
@@ -1436,6 +1457,7 @@ int enet_hip_context_destroy(enet_hip_context* ctx) {
     (void)hipFree(ctx->d_basis);
     (void)hipFree(ctx->d_basis2);
     (void)hipFree(ctx->d_tz);
+    (void)hipFree(ctx->d_lin);
     pipeline_release(ctx);
     (void)hipFree(ctx->d_claim);
     (void)hipFree(ctx->d_frag_desc);
@@ -1527,6 +1549,17 @@ int enet_hip_crc32_batch_list_device(enet_hip_context* ctx, const ENetHipBatch* 
         for (size_t b0 = 0; b0 < batchCount; b0 += kLeanMaxBatches) {
             const int rc = lean_launch_list(llg, ctx->num_cus, st, batches + b0,
                                             std::min<size_t>(batchCount - b0, kLeanMaxBatches), tb);
+            if (rc) return rc;
+        }
+        return 0;
+    }
+    if (ctx->ablation == 0 && lin_path(ctx)) {
+        for (size_t b0 = 0; b0 < batchCount; b0 += kVrMaxBatches) {
+            VrBatches bl{};
+            for (size_t b = b0; b < std::min(batchCount, b0 + kVrMaxBatches); ++b)
+                bl.b[bl.count++] = VrBatch{batches[b].bytes, batches[b].offsets, batches[b].lengths, batches[b].out,
+                                           static_cast<uint64_t>(batches[b].count), 0u};
+            const int rc = lin_list(ctx, bl, st);
             if (rc) return rc;
         }
         return 0;

@@ -1,14 +1,29 @@
 set -o pipefail
-# round 3 (4b): validation at HEAD -- -m gpu, smoke, driver-form bench, cfg3 binned, gather
+# round 4 (b): first GPU run of the linear-stream kernel (paths 22/23) -- its parity
+# tests first (a fault stops the call), then the probe numbers (ablations) and the
+# bench at path 22/23 beside the default; then the r4a evidence.
 out=gpurun_out/r4b
 mkdir -p $out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-tools/gpu_step.sh 1000 $out/pytest.log python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread || exit 1
-grep -q " passed" $out/pytest.log || exit 1
-grep -q "FAILED" $out/pytest.log && exit 1
-tools/gpu_step.sh 300 $out/smoke.log python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
-grep -q "smoke ok" $out/smoke.log || exit 1
-tools/gpu_step.sh 300 $out/bench_driver.json python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1
+( cat /proc/self/cgroup; cat /sys/fs/cgroup/cpu.max; nproc; python3 -c "import os; print(len(os.sched_getaffinity(0)))" ) > $out/host.txt 2>&1
+tools/gpu_step.sh 400 $out/pytest_lin.log python -u -m pytest tests/test_gpu_lin.py -m gpu -v -x --timeout 120 --timeout-method thread || exit 1
 B="python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --sustain-ms 0"
+tools/gpu_step.sh 300 $out/lin22.json $B --path 22 || exit 1
+tools/gpu_step.sh 300 $out/lin23.json $B --path 23 || exit 1
+tools/gpu_step.sh 300 $out/lin22_s1.json $B --path 22 --streams 1 || exit 1
+tools/gpu_step.sh 300 $out/lin22_abl1.json $B --path 22 --ablate 2048 || exit 1
+tools/gpu_step.sh 300 $out/lin22_abl3.json $B --path 22 --ablate 6144 || exit 1
+tools/gpu_step.sh 300 $out/vring.json $B || exit 1
+tools/gpu_step.sh 300 $out/lin22_cfg3.json $B --path 22 --config cfg3 || exit 1
+tools/gpu_step.sh 300 $out/lin22_cfg4.json $B --path 22 --config cfg4 || exit 1
+grep -q " passed" $out/pytest_lin.log || exit 1
+grep -q "FAILED" $out/pytest_lin.log && exit 1
+tools/gpu_step.sh 1000 $out/pytest.log python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread || exit 1
+tools/gpu_step.sh 300 $out/smoke.log python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
+tools/gpu_step.sh 300 $out/bench_driver_1.json python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1
+tools/gpu_step.sh 300 $out/bench_gpus2.json python bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu-baseline || exit 1
 tools/gpu_step.sh 300 $out/cfg3b.json $B --config cfg3 --binned || exit 1
-tools/gpu_step.sh 300 $out/gather.log python -u tools/gather_bench.py --only gather_binned || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/driver_trace -o run --output-format csv \
+  -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --sustain-ms 0 > $out/driver_bench.json 2>&1 || exit 1
+python3 tools/trace_stats.py $out/driver_trace --match "crc32_vring_kernel<3" --skip 1 --out $out/driver_trace_stats.json || exit 1
+echo done > $out/done
