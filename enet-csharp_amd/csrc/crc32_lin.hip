@@ -51,8 +51,9 @@ static_assert(kLnLds <= 160 * 1024, "LDS");
 // Free columns of the lin image (free_col(c), 256 rows, byte-indexed): the
 // multipliers M_k = x^(8 32 k) (k = 1..4, columns 4 (k-1) + b: entry v = (v << 8 b) M_k),
 // the zero-byte divisors x^(-8 16), x^(-8 8), x^(-8 4) (columns 16 + 4 j + b), U (the
-// one-zero-byte unstep, column 28) and INITS[n] = ~0 through n zero bytes (column 29).
-constexpr uint32_t kLnMulCol = 0, kLnTzCol = 16, kLnUCol = 28, kLnInitCol = 29;
+// one-zero-byte unstep, column 28), INITS[n] = ~0 through n zero bytes (column 29) and
+// INIT[r], the register r zero bytes carry to ~0 (column 30: the direct-fold path).
+constexpr uint32_t kLnMulCol = 0, kLnTzCol = 16, kLnUCol = 28, kLnInitCol = 29, kLnInitInvCol = 30;
 static_assert(kLnUCol == kUnstepCol, "the U column of the vring images");
 
 // ------------------------------------------------------------------ host: the image
@@ -89,10 +90,12 @@ int lin_image(uint32_t* img) {
         const uint32_t t = crc_table_entry(v);            // U: reg x^(-8) = (reg << 8) ^ U[reg >> 24]
         img[(256u * (t >> 24) + free_col(kLnUCol)) / 4] = (t << 8) | v;
     }
-    uint32_t init = 0xFFFFFFFFu;
+    uint32_t init = 0xFFFFFFFFu, inv = 0xFFFFFFFFu;
     for (uint32_t n = 0; n < 256; ++n) {
         img[(256u * n + free_col(kLnInitCol)) / 4] = init;
+        img[(256u * n + free_col(kLnInitInvCol)) / 4] = inv;
         init = sarwate_step(init, 0);
+        inv = unstep_zero(inv);
     }
     return 0;
 }
@@ -386,8 +389,12 @@ __global__ void __launch_bounds__(64 * kLnW) crc32_lin_kernel(VrBatches bl, cons
                 const VrBatch B = batch(un.b);
                 uint32_t r = 0u;
                 if (!un.fast) {
+                    // fold_window reads an end-aligned window: rp = 32 nb - L zero bytes in
+                    // front, so it starts from INIT[rp], the register they carry to ~0
                     const uint64_t i = un.p0 + lane;
-                    r = finalize(fold_window(0xFFFFFFFFu, B.bytes + B.off[i], B.len[i], sch, zero));
+                    const uint32_t Lp = B.len[i];
+                    const uint32_t rp = ((Lp + 31u) & ~31u) - Lp;
+                    r = finalize(fold_window(lds_load(256u * rp + free_col(kLnInitInvCol)), B.bytes + B.off[i], Lp, sch, zero));
                 }
                 B.out[un.p0 + lane] = r;                  // (empty packets: finalize(~0) = 0)
             }
@@ -514,12 +521,15 @@ __global__ void __launch_bounds__(64 * kLnW) crc32_lin_kernel(VrBatches bl, cons
                 hs = head ? Xs + 1u : 0u;
                 he = tail ? (ep == 128u ? Xe + 1u : Xe) : 64u;   // (exclusive)
             }
-            const uint32_t jlo = wave_min_u(hs < he ? hs : 64u);
-            const uint32_t jhi = wave_max_u(hs < he ? he : 0u);
-            for (uint32_t j = jlo; j < jhi; ++j) {
+            // each lane walks its own range (the wave's trip count is the longest range,
+            // not the union of the ranges: that is the whole tile at every tile)
+            const uint32_t cnt = hs < he ? he - hs : 0u;
+            const uint32_t trips = wave_max_u(cnt);
+            for (uint32_t t = 0; t < trips; ++t) {
+                const uint32_t j = min(hs + t, 63u);
                 const uint32_t c = lds_load(stbase + 16u * j + 12u);
                 const uint32_t r = ln_tab4(acc, ln_colw(kLnMulCol + 12u)) ^ c;
-                acc = (j >= hs && j < he) ? r : acc;
+                acc = t < cnt ? r : acc;
             }
             // tails: W = Y ^ acc x^(8 32 (q_e + 1)) (one super-block: Y ^ Zs x^(8 32 (q_e - q_s))
             // ^ INITS[32 (q_e + 1) - s']), then x^(-8 (32 - m_e))
