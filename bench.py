@@ -396,7 +396,7 @@ def make_batches(cfg: str, rotate: int, rank: int, world: int = 1):
     return out
 
 
-PRODUCT_PATHS = (0, 1, 2, 13, 17, 22, 23)  # built in libenethip.so (the rest: libenethip_diag.so)
+PRODUCT_PATHS = (0, 1, 2, 13, 17)          # built in libenethip.so (the rest: libenethip_diag.so)
 
 
 def kernel_name(args, list_launch: bool = False) -> str:

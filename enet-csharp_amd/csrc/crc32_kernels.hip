@@ -1202,8 +1202,7 @@ bool path_built(int path) {
 #ifdef ENET_HIP_DIAG
     return path >= 0 && path <= kMaxPath;
 #else
-    return path == 0 || path == 1 || path == 2 || path == kLeanPath0 || path == kVringPath || path == kLinPath ||
-           path == kLinPlainPath;
+    return path == 0 || path == 1 || path == 2 || path == kLeanPath0 || path == kVringPath;
 #endif
 }
 bool lin_path(const enet_hip_context* ctx) { return ctx->path == kLinPath || ctx->path == kLinPlainPath; }

@@ -595,10 +595,14 @@ int ln_set() {
 }
 }  // namespace
 
+// The linear kernel is a diagnostics-library path (kernel paths 22 / 23; DESIGN.md
+// 6.0e): correct on every input, slower than the VGPR-ring kernel, so the product
+// library builds no instance of it.
 int lin_setup() {
-    int rc = ln_set<0, 1>();
-    if (!rc) rc = ln_set<0, 0>();
+    int rc = 0;
 #ifdef ENET_HIP_DIAG
+    rc = ln_set<0, 1>();
+    if (!rc) rc = ln_set<0, 0>();
     if (!rc) rc = ln_set<1, 1>();
     if (!rc) rc = ln_set<3, 1>();
 #endif
@@ -622,11 +626,14 @@ int lin_launch_list(int max_wgs, hipStream_t st, const VrBatches& bl, const uint
     a.groups = U;
     const unsigned grid = static_cast<unsigned>(std::min<uint64_t>(static_cast<uint64_t>(max_wgs), (U + kLnW - 1) / kLnW));
     const void* fn = nullptr;
+#ifdef ENET_HIP_DIAG
     if (abl == 0) fn = nt ? reinterpret_cast<const void*>(crc32_lin_kernel<0, 1>)
                           : reinterpret_cast<const void*>(crc32_lin_kernel<0, 0>);
-#ifdef ENET_HIP_DIAG
     else if (abl == 1) fn = reinterpret_cast<const void*>(crc32_lin_kernel<1, 1>);
     else if (abl == 3) fn = reinterpret_cast<const void*>(crc32_lin_kernel<3, 1>);
+#else
+    (void)abl;
+    (void)nt;
 #endif
     if (!fn) return -static_cast<int>(hipErrorInvalidValue);
     void* args[] = {&a, const_cast<uint32_t**>(&image), const_cast<uint8_t**>(&zero)};

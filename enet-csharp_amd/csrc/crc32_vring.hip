@@ -527,40 +527,8 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     // the arena front to back (the access shape of tools/streamprobe.hip's chunk
     // and sub-stream probes) instead of a round of 16 groups every wt groups
     const uint64_t gw = WK ? (ngroups_all + gridDim.x - 1u) / gridDim.x : 0u;
-    // BIN (records, one batch): the XCD-aware deal (round 4).  The records of tile t
-    // (1024 neighbouring packets, sorted by length) are the groups q T + t of every
-    // rank q; neighbours in memory land in different ranks, and a line two of them
-    // share is fetched by both.  Workgroup w runs on XCD w mod 8 (the dispatcher deals
-    // workgroups round-robin over the XCDs: a speed assumption only, never
-    // correctness), so the tiles t = x mod 8 go to the workgroups w = x mod 8,
-    // tile-major (a tile's ranks, then the next tile's): a tile is read by the
-    // workgroups of one XCD at about the same time, its shared lines in one 4 MiB L2.
-    // Groups past the interleaved tiles (the binned entry's ragged last tile) are
-    // dealt round-robin over the XCDs.
-    uint64_t bT = 0, bR = 1, bTx = 0, bN = 0;
-    uint32_t bx = 0, ba = 0, bGx = 1;
-    if constexpr (BIN && !WK) {
-        bT = bl.tile_counts ? bl.tiles : bl.b[0].n / 1024u;  // interleaved tiles
-        bR = bl.tile_counts ? (bT ? ngroups_all / bT : 1u) : 1024u / kPk;
-        bx = blockIdx.x & 7u;
-        ba = blockIdx.x >> 3;
-        bGx = (gridDim.x - bx + 7u) / 8u;
-        bTx = bT > bx ? (bT - bx + 7u) / 8u : 0u;
-        const uint64_t tail = ngroups_all - bR * bT;
-        bN = bR * bTx + (tail > bx ? (tail - bx + 7u) / 8u : 0u);
-    }
     auto slot_group = [&](uint32_t sl) __attribute__((always_inline)) -> uint64_t {
         if constexpr (WK) return sl < gw ? static_cast<uint64_t>(blockIdx.x) * gw + sl : ~0ull;
-        if constexpr (BIN) {
-            const uint64_t item = static_cast<uint64_t>(ba) * kVrW + (sl & (kVrW - 1u)) +
-                                  static_cast<uint64_t>(sl / kVrW) * kVrW * bGx;
-            if (item >= bN) return ~0ull;
-            if (item < bR * bTx) {
-                const uint64_t tl = item / bR, q = item - tl * bR;
-                return q * bT + bx + 8u * tl;
-            }
-            return bR * bT + 8u * (item - bR * bTx) + bx;
-        }
         return static_cast<uint64_t>(blockIdx.x) * kVrW + (sl & (kVrW - 1u)) + static_cast<uint64_t>(sl / kVrW) * wt;
     };
     // `it` moved to global group gg (its batch found from it.b on: a wave's groups

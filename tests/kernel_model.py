@@ -916,27 +916,3 @@ def lin_unit(arena: bytes, offs, lens, base: int = 0):
         out[i] = finalize(state)
     return out
 
-
-def vring_bin_deal(T: int, R: int, tail: int, grid: int, W: int = 16, slots: int = 4096):
-    """crc32_vring.hip's XCD-aware deal of the records instance (round 4): workgroup
-    w (XCD w mod 8) maps its slot s to an item of its XCD's list -- tiles t = w mod 8,
-    tile-major, then every 8th tail group -- and the item to the global group.
-    Returns {workgroup: [groups in slot order]} for slots below `slots` per workgroup."""
-    out = {}
-    for w in range(grid):
-        x, a = w & 7, w >> 3
-        gx = (grid - x + 7) // 8
-        tx = (T - x + 7) // 8 if T > x else 0
-        n_items = R * tx + ((tail - x + 7) // 8 if tail > x else 0)
-        gs = []
-        for sl in range(slots):
-            item = a * W + (sl % W) + (sl // W) * W * gx
-            if item >= n_items:
-                continue
-            if item < R * tx:
-                tl, q = divmod(item, R)
-                gs.append(q * T + x + 8 * tl)
-            else:
-                gs.append(R * T + 8 * (item - R * tx) + x)
-        out[w] = gs
-    return out

@@ -23,7 +23,7 @@ def lctx():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     torch.cuda.init()
-    c = enethip.Context(0)
+    c = enethip.Context(0, diag=True)         # (a diagnostics-library path)
     c.set_kernel_path(LIN)
     yield c
     c.close()

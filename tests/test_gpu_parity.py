@@ -36,7 +36,7 @@ def dctx():
     c.close()
 
 
-PRODUCT_PATHS = (0, 1, 2, 13, 17, 22, 23)   # built in libenethip.so; every other path: libenethip_diag.so only
+PRODUCT_PATHS = (0, 1, 2, 13, 17)   # built in libenethip.so; every other path: libenethip_diag.so only
 
 
 def on(ctx, dctx, path):
@@ -641,7 +641,7 @@ def test_vring_many_groups(ctx, dctx, oracle_lib, path, wgs):
 
 def test_product_library_rejects_sweep_paths(ctx):
     """libenethip.so builds no sweep path (they exist in libenethip_diag.so only)."""
-    for path in (3, 8, 14, 18, 19, 20, 21, 24):
+    for path in (3, 8, 14, 18, 19, 20, 21, 22, 23):
         with pytest.raises(enethip.ENetHipError):
             ctx.set_kernel_path(path)
     ctx.set_kernel_path(0)

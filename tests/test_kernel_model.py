@@ -440,17 +440,3 @@ def test_lin_model_matches_oracle():
         got = km.lin_unit(arena, off, lens, rng.randint(0, 127))
         assert got == [ref(arena[o:o + L]) for o, L in zip(off, lens)], trial
 
-
-@pytest.mark.parametrize("T,R,tail,grid", [(256, 64, 0, 256), (256, 64, 37, 512), (588, 86, 0, 256), (3, 64, 10, 256),
-                                           (0, 64, 50, 256), (17, 5, 3, 40)])
-def test_vring_bin_deal_covers_every_group_once_on_its_tiles_xcd(T, R, tail, grid):
-    """The records instance's XCD-aware deal: every group of the launch is taken
-    exactly once, and every group of interleaved tile t by a workgroup w with
-    w = t (mod 8) (one XCD's L2 under round-robin dispatch)."""
-    deal = km.vring_bin_deal(T, R, tail, grid)
-    seen = [g for gs in deal.values() for g in gs]
-    assert sorted(seen) == list(range(R * T + tail))
-    for w, gs in deal.items():
-        for g in gs:
-            if g < R * T:
-                assert (g % T) % 8 == w % 8 if T else True
