@@ -1,17 +1,19 @@
 set -o pipefail
-# round 3 (4d): receive verify (VF): partly covered pieces masked in place (as the other
-# instances), the slot fix-up on copies after -- verify tests, A/B of verify lists
+# round 4 (d): where a serial launch loses against overlapped ones (per-wave end
+# times of 1-, 5- and 20-batch launches), and the sustained-rate cause (VERDICT r3
+# #6): the product, its no-lookup ablation and its skeleton beside the read probe,
+# with the amdsmi refresh logged.
 out=gpurun_out/r4d
 mkdir -p $out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-tools/gpu_step.sh 600 $out/pytest.log python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_harness.py -m gpu -v --timeout 240 --timeout-method thread -k "verify" || exit 1
-grep -q " passed" $out/pytest.log || exit 1
-grep -q "FAILED" $out/pytest.log && exit 1
-cp enet-csharp_amd/libenethip.so ab/libenethip_new.so
-for r in 1 2 3; do
-  for v in new prev; do
-    cp ab/libenethip_$v.so enet-csharp_amd/libenethip.so
-    tools/gpu_step.sh 300 $out/verify_${v}_$r.log python -u tools/verify_bench.py --list 20 || exit 1
-  done
-done
-cp ab/libenethip_new.so enet-csharp_amd/libenethip.so
+tools/gpu_step.sh 200 $out/timeline_l5_w2.log python -u tools/list_timeline.py 5 2 || exit 1
+tools/gpu_step.sh 200 $out/timeline_l20_w2.log python -u tools/list_timeline.py 20 2 || exit 1
+tools/gpu_step.sh 200 $out/timeline_l1_w1.log python -u tools/list_timeline.py 1 1 || exit 1
+tools/gpu_step.sh 300 $out/sustain_vring.log python -u tools/sustain.py --kernel vring --launches 3000 || exit 1
+tools/gpu_step.sh 300 $out/sustain_abl4096.log python -u tools/sustain.py --kernel vring --launches 3000 --ablate 4096 || exit 1
+tools/gpu_step.sh 300 $out/sustain_skel.log python -u tools/sustain.py --kernel vring --launches 3000 --ablate 38912 || exit 1
+tools/gpu_step.sh 300 $out/sustain_probe.log python -u tools/sustain.py --kernel probe --launches 3000 || exit 1
+B="python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --sustain-ms 0"
+tools/gpu_step.sh 200 $out/bench_s2.json $B --streams 2 || exit 1
+tools/gpu_step.sh 200 $out/bench_s4.json $B --streams 4 || exit 1
+echo done > $out/done

@@ -62,11 +62,24 @@ class Sampler(threading.Thread):
             self.samples.append((time.perf_counter(), {k: m.get(k) for k in self.FIELDS}))
 
 
+def refresh_ms(samples, t0, t1):
+    """Median host-time gap between samples whose firmware timestamp changed."""
+    ts, last = [], object()
+    for t, m in samples:
+        if t0 <= t <= t1 and m.get("firmware_timestamp") != last:
+            ts.append(t)
+            last = m.get("firmware_timestamp")
+    return round(float(np.median(np.diff(ts)) * 1e3), 3) if len(ts) > 2 else None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kernel", choices=["vring", "probe"], default="vring")
     ap.add_argument("--launches", type=int, default=3000)
     ap.add_argument("--list", type=int, default=5)
+    ap.add_argument("--ablate", type=int, default=0,
+                    help="vring: enet_hip_diag_ablation value (diagnostics library; 4096 = no table lookups, "
+                         "2048+4096+32768 = the memory/control skeleton: WRONG CRCs by design)")
     a = ap.parse_args()
     nb = 10
     big = torch.randint(0, 255, (nb * BATCH + 4096,), dtype=torch.uint8, device="cuda")
@@ -75,7 +88,9 @@ def main():
     outs = [torch.zeros(65536, dtype=torch.int32, device="cuda") for _ in range(nb)]
     descs = [(big[j * BATCH:], off, lens, 65536, outs[j]) for j in range(nb)]
     sink = torch.zeros(4, dtype=torch.int32, device="cuda")
-    ctx = enethip.Context(0)
+    ctx = enethip.Context(0, diag=bool(a.ablate))
+    if a.ablate:
+        ctx.diag_ablation(a.ablate)
     st = torch.cuda.Stream()
     L = a.list
 
@@ -141,7 +156,11 @@ def main():
                                               (ends[starts < 2][-1] * 1e-3) / 1e12, 3),
                       "TBps_whole": round(nbytes * a.launches / (ends[-1] * 1e-3) / 1e12, 3),
                       "TBps_1ms_buckets_first_40ms": [min(early, default=None), max(early, default=None)],
-                      "smi_samples_run": len(run), "smi_error": smp.error,
+                      "smi_samples_run": len(run), "smi_error": smp.error, "ablate": a.ablate,
+                      # do the metrics refresh?  distinct firmware timestamps over the run
+                      # and the median gap between them (ms of host time)
+                      "smi_distinct_fw_timestamps": len({m.get("firmware_timestamp") for m in run}),
+                      "smi_refresh_ms_median": refresh_ms(smp.samples, t_gpu0, t_end),
                       "ppt_residency_delta": delta("ppt_residency_acc"),
                       "socket_thm_residency_delta": delta("socket_thm_residency_acc"),
                       "hbm_thm_residency_delta": delta("hbm_thm_residency_acc"),
