@@ -887,6 +887,9 @@ __device__ __forceinline__ uint32_t fold_small(uint32_t reg, uint32_t sh, uint32
     return reg;
 }
 
+// JV (diagnostics, wrong CRCs by design): bit 0 = no short-segment fold (its dwords
+// XORed in), bit 1 = no multiply (XOR), bit 2 = no short-segment loads
+template <int JV = 0>
 __global__ void __launch_bounds__(kThreads) crc32_gather_join_kernel(GatherArgs ga, const uint32_t* seg_crc,
                                                                      KernelTables tb, uint32_t small) {
     constexpr int kQ = 4;                                    // segments in flight per thread
@@ -915,7 +918,7 @@ __global__ void __launch_bounds__(kThreads) crc32_gather_join_kernel(GatherArgs 
             uint32_t D[kQ][kSmallDwords + 1], C[kQ], X[kQ];
 #pragma unroll
             for (int i = 0; i < kQ; ++i) {
-                const bool sm = L[i] != 0u && L[i] <= small;
+                const bool sm = L[i] != 0u && L[i] <= small && !(JV & 4);
                 if (sm) load_small(A[i], L[i], D[i]);
                 else
 #pragma unroll
@@ -927,7 +930,14 @@ __global__ void __launch_bounds__(kThreads) crc32_gather_join_kernel(GatherArgs 
             for (int i = 0; i < kQ; ++i) {
                 if (L[i] == 0u) continue;
                 if (L[i] <= small) {
-                    reg = fold_small(reg, static_cast<uint32_t>(reinterpret_cast<uintptr_t>(A[i])) & 3u, L[i], D[i], t4);
+                    if constexpr (JV & 1) {
+#pragma unroll
+                        for (int k = 0; k <= kSmallDwords; ++k) reg ^= D[i][k];
+                    } else {
+                        reg = fold_small(reg, static_cast<uint32_t>(reinterpret_cast<uintptr_t>(A[i])) & 3u, L[i], D[i], t4);
+                    }
+                } else if constexpr (JV & 2) {
+                    reg ^= X[i] ^ ~bswap32(C[i]);
                 } else {
                     const uint32_t x = (L[i] >> 16) ? mulmod(X[i], tb.xn_hi[L[i] >> 16]) : X[i];
                     reg = (reg == 0xFFFFFFFFu ? 0u : mulmod(reg ^ 0xFFFFFFFFu, x)) ^ ~bswap32(C[i]);
@@ -936,6 +946,86 @@ __global__ void __launch_bounds__(kThreads) crc32_gather_join_kernel(GatherArgs 
         }
         ga.out[d] = finalize(reg);
     }
+}
+
+// The join, segment-parallel (diagnostics A/B against the thread-per-DGRAM join
+// above): a workgroup takes kJT DGRAMs and the window of their segments, kJT segments
+// at a time.  Lane j of a window step takes segment q = one of them: its length and
+// offset (coalesced), then its contribution -- a short segment's reg(0, B) folded
+// from its bytes, a long one's reg(0xFFFFFFFF, B) from seg_crc -- and x^(8 |B|), into
+// LDS.  Then DGRAM d's lane walks its segments of the step in order:
+// reg' = (reg ^ f) x^(8 |B|) ^ v, f = 0 for a short segment (reg(s, B) = adv(s) ^
+// reg(0, B)), f = 0xFFFFFFFF for a long one (as in the join above); an empty segment
+// is the identity (x^0 = 0x80000000 in the reflected order, v = 0).  Segment ranges
+// that are not nondecreasing in d still give the per-DGRAM results (the window is
+// the union of the ranges), only more window steps.
+constexpr int kJT = 256;
+constexpr uint32_t kGfOne = 0x80000000u;                    // x^0, reflected
+__global__ void __launch_bounds__(kJT) crc32_gather_join_seg_kernel(GatherArgs ga, const uint32_t* seg_crc,
+                                                                    KernelTables tb, uint32_t small) {
+    __shared__ uint32_t t4[4][256];
+    __shared__ uint32_t sv[kJT], sx[kJT], sf[kJT];
+    __shared__ uint32_t win[2];
+    const uint32_t t = threadIdx.x;
+    const uint64_t d = static_cast<uint64_t>(blockIdx.x) * kJT + t;
+    // this DGRAM's segment range (clamped as in the join above); lanes past n: empty
+    uint32_t s0 = 0xFFFFFFFFu, s1 = 0u;
+    if (d < ga.n) {
+        s1 = static_cast<uint32_t>(min<uint64_t>(ga.seg_first[d + 1], ga.segs));
+        s0 = min(ga.seg_first[d], s1);
+    }
+    if (small)
+        for (uint32_t i = t; i < 1024u; i += kJT) t4[i >> 8][i & 255u] = tb.image[64u * (i & 255u) + 2u * (i >> 8)];
+    // the window [min s0, max s1): wave reductions, then one LDS min / max
+    uint32_t lo = s0, hi = s1;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        lo = min(lo, static_cast<uint32_t>(__shfl_xor(static_cast<int>(lo), m)));
+        hi = max(hi, static_cast<uint32_t>(__shfl_xor(static_cast<int>(hi), m)));
+    }
+    if (t == 0u) {
+        win[0] = 0xFFFFFFFFu;
+        win[1] = 0u;
+    }
+    __syncthreads();
+    if ((t & 63u) == 0u) {
+        atomicMin(&win[0], lo);
+        atomicMax(&win[1], hi);
+    }
+    __syncthreads();
+    const uint32_t w0 = win[0], w1 = win[1];
+    uint32_t reg = 0xFFFFFFFFu;
+    for (uint32_t c = w0; c < w1; c += kJT) {                // (w0 = ~0: no segment in the workgroup)
+        const uint32_t q = c + t;
+        uint32_t v = 0u, x = kGfOne, f = 0u;
+        if (q < w1) {
+            const uint32_t L = ga.seg_len[q];
+            const uint8_t* a = ga.bytes + ga.seg_off[q];
+            if (L != 0u && L <= small) {
+                uint32_t D[kSmallDwords + 1];
+                load_small(a, L, D);
+                v = fold_small(0u, static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a)) & 3u, L, D, t4);
+                x = tb.xn_lo[L];
+            } else if (L != 0u) {
+                v = ~bswap32(seg_crc[q]);
+                x = tb.xn_lo[L & 0xFFFFu];
+                if (L >> 16) x = mulmod(x, tb.xn_hi[L >> 16]);
+                f = 0xFFFFFFFFu;
+            }
+        }
+        sv[t] = v;
+        sx[t] = x;
+        sf[t] = f;
+        __syncthreads();
+        const uint32_t a0 = max(s0, c), a1 = min(s1, c + kJT);
+        for (uint32_t k = a0; k < a1; ++k) {
+            const uint32_t i = k - c;
+            const uint32_t r = reg ^ sf[i];
+            reg = (r == 0u ? 0u : mulmod(r, sx[i])) ^ sv[i];
+        }
+        __syncthreads();
+    }
+    if (d < ga.n) ga.out[d] = finalize(reg);
 }
 
 // Read-roofline probe: every byte loaded once by 16-byte coalesced loads,
@@ -1276,6 +1366,19 @@ int vring_wgs(const enet_hip_context* ctx, size_t batches) {
 bool vring_path(const enet_hip_context* ctx) {
     return ctx->path == 0 || (ctx->path >= kVringPath && ctx->path <= kVringTailFirstPath);
 }
+// The claim line of the next vring launch (dynamic rounds), or null (static deal).
+// Lines are handed out in turn: a line is reused kVrClaimLines launches later, when
+// the launch that used it has ended (the context's launches run on at most a few
+// streams at once).
+constexpr uint32_t kVrClaimLines = 256;
+uint32_t* vring_claim(enet_hip_context* ctx) {
+    if (!ctx->vr_dynamic || !ctx->d_rounds) return nullptr;
+    return ctx->d_rounds + static_cast<size_t>(kVrClaimWords) * (ctx->rounds_next.fetch_add(1u) % kVrClaimLines);
+}
+VrVariant with_claim(enet_hip_context* ctx, VrVariant v) {
+    if (!v.walk) v.claim = vring_claim(ctx);
+    return v;
+}
 VrVariant vring_variant(const enet_hip_context* ctx, bool lists) {
     VrVariant v;
     v.nt = ctx->path == kVringAltPath || ctx->path == kVringWalkAltPath;
@@ -1305,7 +1408,7 @@ int verify_vring_list(enet_hip_context* ctx, const ENetHipVerifyBatch* batches, 
             bl.b[bl.count++] = VrVBatch{e.bytes, e.offsets, e.lengths, e.computed, static_cast<uint64_t>(e.count), 0u,
                                         e.slotOffsets, e.connectIds, e.ok};
         }
-        const int rc = vring_launch_vlist(ctx->num_cus * vring_wgs(ctx, bl.count), v, st, bl, tb, ctx->d_basis2,
+        const int rc = vring_launch_vlist(ctx->num_cus * vring_wgs(ctx, bl.count), with_claim(ctx, v), st, bl, tb, ctx->d_basis2,
                                           v.abl ? ctx->trace : nullptr);
         if (rc) return rc;
     }
@@ -1330,7 +1433,8 @@ int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStr
     }
     if (mode == 0 && (pa.lg == 2 || pa.lg == 3) && ctx->ablation == 0 && vring_path(ctx))
         return vring_launch(pa.lg, ctx->num_cus * vring_wgs(ctx, 1),
-                            pa.meta4 ? VrVariant{} : vring_variant(ctx, false), st, pa, tb, ctx->d_basis2);
+                            with_claim(ctx, pa.meta4 ? VrVariant{} : vring_variant(ctx, false)), st, pa, tb,
+                            ctx->d_basis2);
     if (ctx->path != 1 && pa.lg >= 2 && pa.lg <= 4) {
         const bool lean_path = (ctx->path >= kLeanPath0 && ctx->path < kVringPath) || (ctx->path == 0 && ctx->ablation == 0);
         if (lean_path && pa.lg <= 3)
@@ -1423,6 +1527,9 @@ int enet_hip_context_create(int device, enet_hip_context** out) {
         if ((rc = herr(hipMemcpy(ctx->d_basis2, ht.basis2.data(), ht.basis2.size() * 4, hipMemcpyHostToDevice)))) break;
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_lin), ht.lin.size() * 4)))) break;
         if ((rc = herr(hipMemcpy(ctx->d_lin, ht.lin.data(), ht.lin.size() * 4, hipMemcpyHostToDevice)))) break;
+        const size_t claim_bytes = static_cast<size_t>(kVrClaimLines) * kVrClaimWords * 4;
+        if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_rounds), claim_bytes)))) break;
+        if ((rc = herr(hipMemset(ctx->d_rounds, 0, claim_bytes)))) break;
         if ((rc = vring_setup())) break;
         if ((rc = lin_setup())) break;
         if ((rc = setup_stream())) break;
@@ -1457,6 +1564,7 @@ int enet_hip_context_destroy(enet_hip_context* ctx) {
     (void)hipFree(ctx->d_basis2);
     (void)hipFree(ctx->d_tz);
     (void)hipFree(ctx->d_lin);
+    (void)hipFree(ctx->d_rounds);
     pipeline_release(ctx);
     (void)hipFree(ctx->d_claim);
     (void)hipFree(ctx->d_frag_desc);
@@ -1478,7 +1586,9 @@ int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgro
 
 #ifdef ENET_HIP_DIAG
 int enet_hip_diag_ablation(enet_hip_context* ctx, int mode) {
-    if (!ctx || mode < 0 || mode >= (1 << 19)) return -static_cast<int>(hipErrorInvalidValue);
+    if (!ctx || mode < 0 || mode >= (1 << 24)) return -static_cast<int>(hipErrorInvalidValue);
+    ctx->join_abl = (mode >> 20) & 15;                       // 1048576 x (1..7): gather-join ablations, x 8: segment-parallel join
+    ctx->vr_dynamic = (mode >> 19) & 1;                      // 524288: vring dynamic rounds
     const int prio = (mode & 1024) ? 2 : (mode >> 3) & 1;    // 8: static / 1024: progress priority
     ctx->vr_abl = (mode >> 11) & 255;                        // 2048 ... 262144: vring ablations / end records
     mode &= 511;
@@ -1571,8 +1681,9 @@ int enet_hip_crc32_batch_list_device(enet_hip_context* ctx, const ENetHipBatch* 
             for (size_t b = b0; b < std::min(batchCount, b0 + kVrMaxBatches); ++b)
                 bl.b[bl.count++] = VrBatch{batches[b].bytes, batches[b].offsets, batches[b].lengths, batches[b].out,
                                            static_cast<uint64_t>(batches[b].count), 0u};
-            const int rc = vring_launch_list(lg, ctx->num_cus * vring_wgs(ctx, bl.count), vring_variant(ctx, true), st, bl, tb,
-                                             ctx->d_basis2, ctx->trace);
+            const int rc = vring_launch_list(lg, ctx->num_cus * vring_wgs(ctx, bl.count),
+                                             with_claim(ctx, vring_variant(ctx, true)), st, bl, tb, ctx->d_basis2,
+                                             ctx->trace);
             if (rc) return rc;
         }
         return 0;
@@ -1764,8 +1875,8 @@ int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* by
         bl.tiles = static_cast<uint32_t>(gather_tiles(segCount));
         bl.tile_counts = counts;
         bl.b[0] = VrBatch{bytes, static_cast<const uint64_t*>(workspace), nullptr, seg_crc, 1024ull * bl.tiles, 0u};
-        if ((rc = vring_launch_list(lanes == 4 ? 2 : 3, ctx->num_cus * vring_wgs(ctx, 1), VrVariant{}, st, bl, tb,
-                                    ctx->d_basis2, nullptr, true)))
+        if ((rc = vring_launch_list(lanes == 4 ? 2 : 3, ctx->num_cus * vring_wgs(ctx, 1), with_claim(ctx, VrVariant{}),
+                                    st, bl, tb, ctx->d_basis2, nullptr, true)))
             return rc;
     } else if (segCount) {                                   // every segment's CRC, mixed lengths: length-binned
         const int rc = enet_hip_crc32_batch_device_binned(ctx, bytes, segOffsets, segLengths, segCount, seg_crc,
@@ -1774,8 +1885,23 @@ int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* by
     }
     GatherArgs ga{bytes, segOffsets, segLengths, segFirst, dgramCount, out, segCount};
     const unsigned grid = grid_for(ctx, dgramCount);
-    hipLaunchKernelGGL(crc32_gather_join_kernel, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx),
-                       split ? kGatherSmall : 0u);
+    const uint32_t small = split ? kGatherSmall : 0u;
+#ifdef ENET_HIP_DIAG
+    switch (ctx->join_abl) {
+        case 1: hipLaunchKernelGGL(crc32_gather_join_kernel<1>, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx), small); break;
+        case 2: hipLaunchKernelGGL(crc32_gather_join_kernel<2>, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx), small); break;
+        case 3: hipLaunchKernelGGL(crc32_gather_join_kernel<3>, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx), small); break;
+        case 5: hipLaunchKernelGGL(crc32_gather_join_kernel<5>, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx), small); break;
+        case 7: hipLaunchKernelGGL(crc32_gather_join_kernel<7>, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx), small); break;
+        case 8:
+            hipLaunchKernelGGL(crc32_gather_join_seg_kernel, dim3(static_cast<unsigned>((dgramCount + kJT - 1) / kJT)),
+                               dim3(kJT), 0, st, ga, seg_crc, tables_of(ctx), small);
+            break;
+        default: hipLaunchKernelGGL(crc32_gather_join_kernel<0>, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx), small);
+    }
+#else
+    hipLaunchKernelGGL(crc32_gather_join_kernel<0>, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx), small);
+#endif
     return herr(hipGetLastError());
 }
 

@@ -53,7 +53,15 @@ constexpr uint32_t kVrMetaWave = 256;
 constexpr uint32_t kVrCtr = kVrMeta + kVrW * kVrMetaWave;       // the workgroup's slot counter (16 B)
 // the zero-byte multiplier tables (tz_addr, KernelTables::tz), DMA'd once per workgroup
 constexpr uint32_t kVrTz = kVrCtr + 16;
-constexpr int kVrLds = kVrTz + kTzTableDwords * 4;               // 78.5 KiB: two workgroups per CU
+// the workgroup's round table (dynamic rounds, VrBatches::claim): entry r % 64 =
+// {tag r, chunk of round r}, 8 B each.  An entry is rewritten 64 rounds (1024
+// slot takes of the workgroup) after it was published; its readers read it right
+// after their own take of a slot of its round
+constexpr uint32_t kVrRound = kVrTz + kTzTableDwords * 4;
+constexpr int kVrRounds = 64;
+// ... and the launch's claim words (VrBatches::claim), kept here, not in SGPRs
+constexpr uint32_t kVrClaimPtr = kVrRound + kVrRounds * 8;
+constexpr int kVrLds = kVrClaimPtr + 16;                         // 79 KiB: two workgroups per CU
 static_assert(2 * kVrLds <= 160 * 1024, "two workgroups per CU");
 // length-binned records (BIN): the same area and layout, plus the x^(-8 c) tables for
 // c < 8 (tz_small_addr) -- 106.5 KiB: one workgroup per CU, the records entries' default
@@ -427,6 +435,69 @@ __device__ __forceinline__ uint32_t vr_lookups(const uint32_t (&d)[8], const VrS
 // take more groups and the workgroup's waves end together: with a static deal the
 // waves of a 20-batch launch ended between 40 % and 100 % of its span
 // (tools/list_timeline.py, profiles/r02d_list_timeline_*).
+// Dynamic rounds (VrBatches::claim set): a round is a chunk of 16 groups, workgroup
+// k's rounds 0 and 1 are chunks k and G + k (G workgroups) as above, and each later
+// round is claimed from the launch's round counter (chunk 2 G + c), so the
+// workgroups the chip favours take more chunks and the launch's workgroups end
+// together too.  The wave taking the first slot of round r >= 1 claims round r + 1
+// (after round r's claim is published: a workgroup's chunks ascend) and publishes
+// it in the LDS round table; a wave taking a slot of round r >= 2 reads round r's
+// entry (polled: published at least 16 slots earlier).  Live slots stay a prefix of
+// the slot sequence (chunks ascend, a chunk's dead groups are its last ones), so the
+// waves stop at the first dead slot as before and no claimed live chunk is left.
+// Dynamic rounds.  The helpers take wave-uniform (SGPR) operands and build their
+// VGPR operands inside the asm: constants the compiler could see (LDS addresses, the
+// atomic's 1) were hoisted out of the ring loop into VGPRs held across it.
+// vr_claim_next: lane 0 adds 1 to the launch's round counter (its address stored at
+// kVrClaimPtr) and waits for the old value -- a returning device-scope atomic; the
+// wait retires the wave's ring loads too, once per round of 16 groups per workgroup.
+__device__ __forceinline__ uint32_t vr_claim_next() {
+    uint32_t c = 0;
+    if ((threadIdx.x & 63u) == 0u) {
+        uint32_t t;
+        uint64_t p;
+        asm volatile("v_mov_b32 %1, %3\n\t"
+                     "ds_read_b64 %2, %1\n\t"
+                     "s_waitcnt lgkmcnt(0)\n\t"
+                     "v_mov_b32 %1, 1\n\t"
+                     "global_atomic_add %0, %2, %1, off sc0\n\t"
+                     "s_waitcnt vmcnt(0)"
+                     : "=&v"(c), "=&v"(t), "=&v"(p) : "i"(kVrClaimPtr) : "memory");
+    }
+    return __builtin_amdgcn_readfirstlane(c);
+}
+// the round table entry of round r: its chunk once published (tag == r), polled.  One
+// 8-byte read takes {tag, chunk}: the chunk was written before the tag
+__device__ __forceinline__ uint32_t vr_round_chunk(uint32_t r) {
+    const uint32_t e = kVrRound + 8u * (r & (kVrRounds - 1u));
+    for (;;) {
+        uint64_t tc;
+        uint32_t a;
+        asm volatile("v_mov_b32 %1, %2\n\t"
+                     "ds_read_b64 %0, %1\n\t"
+                     "s_waitcnt lgkmcnt(0)"
+                     : "=&v"(tc), "=&v"(a) : "s"(e) : "memory");
+        if (__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(tc)) == r)
+            return __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(tc >> 32));
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+// publish round r's chunk: the chunk first, then (after it is written) the tag
+__device__ __forceinline__ void vr_round_publish(uint32_t r, uint32_t chunk) {
+    const uint32_t e = kVrRound + 8u * (r & (kVrRounds - 1u));
+    if ((threadIdx.x & 63u) == 0u) {
+        uint32_t a, v;
+        asm volatile("v_mov_b32 %0, %2\n\t"
+                     "v_mov_b32 %1, %3\n\t"
+                     "ds_write_b32 %0, %1 offset:4\n\t"
+                     "s_waitcnt lgkmcnt(0)\n\t"
+                     "v_mov_b32 %1, %4\n\t"
+                     "ds_write_b32 %0, %1\n\t"
+                     "s_waitcnt lgkmcnt(0)"
+                     : "=&v"(a), "=&v"(v) : "s"(e), "s"(chunk), "s"(r) : "memory");
+    }
+}
+
 struct VrIt {
     uint32_t b;         // batch
     uint64_t g;         // global group
@@ -452,7 +523,9 @@ struct VrIt {
 // VF = 1: receive verify (protocol.cs:1052-1068) over a VrVBatches list, 8 lanes per
 // packet: the slot's lane substitutes connectID in registers (vr_slot_fix), and the
 // packet's lane 0 writes ok[] and computed[].
-template <int LG, int TR = 0, int NT = 0, int ABL = 0, int BIN = 0, int WK = 0, int ROT = 0, int VF = 0>
+// DYN = 1: dynamic rounds (above); built for the product-shaped instances (TR != 1,
+// no ablation, nt, walks or tail-first order)
+template <int LG, int TR = 0, int NT = 0, int ABL = 0, int BIN = 0, int WK = 0, int ROT = 0, int VF = 0, int DYN = 0>
 __global__ void __launch_bounds__(64 * kVrW) __attribute__((amdgpu_waves_per_eu(8, 8), amdgpu_num_vgpr(24)))
 crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, KernelTables tb, const uint32_t* basis,
                    uint64_t* trace) {
@@ -490,6 +563,17 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t wv = static_cast<uint64_t>(blockIdx.x) * kVrW + wave;
     const uint64_t wt = static_cast<uint64_t>(gridDim.x) * kVrW;
+    constexpr bool kDyn = DYN != 0 && !WK;
+    if constexpr (kDyn) {                                    // wave 0, before its takes: no round published
+        if (threadIdx.x < static_cast<uint32_t>(kVrRounds)) lds_store(kVrRound + 8u * threadIdx.x, ~0u);
+        if (threadIdx.x < 2u)
+            lds_store(kVrClaimPtr + 4u * threadIdx.x,
+                      static_cast<uint32_t>(reinterpret_cast<uint64_t>(bl.claim) >> (32u * threadIdx.x)));
+    }
+    // the claim words (read where used: a pointer held across the ring loop costs SGPRs)
+    auto claim_ptr = [&]() __attribute__((always_inline)) -> uint32_t* {
+        return reinterpret_cast<uint32_t*>(lds_load(kVrClaimPtr) | (static_cast<uint64_t>(lds_load(kVrClaimPtr + 4u)) << 32));
+    };
     auto lane_k = [&]() __attribute__((always_inline)) { return lane & (P - 1u); };   // block lane
     auto lane_p = [&]() __attribute__((always_inline)) { return lane >> LG; };         // packet of the group
     const uint64_t zero = reinterpret_cast<uint64_t>(tb.zero);
@@ -529,13 +613,15 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     const uint64_t gw = WK ? (ngroups_all + gridDim.x - 1u) / gridDim.x : 0u;
     auto slot_group = [&](uint32_t sl) __attribute__((always_inline)) -> uint64_t {
         if constexpr (WK) return sl < gw ? static_cast<uint64_t>(blockIdx.x) * gw + sl : ~0ull;
+        if (kDyn && sl >= 2u * kVrW) return static_cast<uint64_t>(vr_round_chunk(sl / kVrW)) * kVrW + (sl & (kVrW - 1u));
         return static_cast<uint64_t>(blockIdx.x) * kVrW + (sl & (kVrW - 1u)) + static_cast<uint64_t>(sl / kVrW) * wt;
     };
     // `it` moved to global group gg (its batch found from it.b on: a wave's groups
-    // ascend); false past the launch's last group
+    // ascend -- with dynamic rounds too); false past the launch's last group
     auto locate = [&](VrIt& it, uint64_t gg) __attribute__((always_inline)) -> bool {
         if (gg >= ngroups_all) return false;
-        while (it.b + 1u < bl.count && gg >= bl.b[it.b + 1u].g0) ++it.b;
+        if constexpr (!BIN)                                  // (BIN: one batch, vring_launch_list)
+            while (it.b + 1u < bl.count && gg >= bl.b[it.b + 1u].g0) ++it.b;
         it.g = gg;
         return true;
     };
@@ -543,19 +629,40 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     // the next slot: the first two static, later ones from the workgroup's counter
     uint32_t last_slot = 0;                                  // (TR 2: the last slot taken)
     auto take = [&]() __attribute__((always_inline)) -> uint32_t {
-        if (taken++ < 2u) return wave + kVrW * (taken - 1u);
-        // ds_add_rtn as inline asm: as a C++ atomic, hipcc put an s_waitcnt vmcnt(0)
-        // in front of it (an LDS atomic that may alias an LDS-DMA in flight), which
-        // drained the ring at every group switch.  The counter is no DMA's target.
         uint32_t sl = 0;
-        if ((threadIdx.x & 63u) == 0u)
-            asm volatile("v_mov_b32 %0, 1\n\t"
-                         "ds_add_rtn_u32 %0, %1, %0\n\t"
-                         "s_waitcnt lgkmcnt(0)"
-                         : "=&v"(sl) : "v"(BIN ? kVrCtrBin : kVrCtr) : "memory");
-        sl = __builtin_amdgcn_readfirstlane(sl);
-        if constexpr (TR == 2) last_slot = sl;
+        if (taken < 2u) {
+            sl = wave + kVrW * taken;
+        } else {
+            // ds_add_rtn as inline asm: as a C++ atomic, hipcc put an s_waitcnt vmcnt(0)
+            // in front of it (an LDS atomic that may alias an LDS-DMA in flight), which
+            // drained the ring at every group switch.  The counter is no DMA's target.
+            if ((threadIdx.x & 63u) == 0u)
+                asm volatile("v_mov_b32 %0, 1\n\t"
+                             "ds_add_rtn_u32 %0, %1, %0\n\t"
+                             "s_waitcnt lgkmcnt(0)"
+                             : "=&v"(sl) : "v"(BIN ? kVrCtrBin : kVrCtr) : "memory");
+            sl = __builtin_amdgcn_readfirstlane(sl);
+            if constexpr (TR == 2) last_slot = sl;
+        }
+        ++taken;
+        if (kDyn && sl >= kVrW && (sl & (kVrW - 1u)) == 0u) {   // the first slot of round r >= 1: claim r + 1
+            const uint32_t r = sl / kVrW;
+            if (r >= 2u) (void)vr_round_chunk(r);            // round r's claim is published (chunks ascend)
+            vr_round_publish(r + 1u, static_cast<uint32_t>(wt / (kVrW / 2u)) + vr_claim_next());   // 2 G + c
+        }
         return sl;
+    };
+    // every wave at its end: the last of the launch zeroes the claim words for the
+    // next launch using them (every claim of the launch is retired by then)
+    auto rounds_exit = [&]() __attribute__((always_inline)) {
+        if (kDyn && (threadIdx.x & 63u) == 0u) {
+            uint32_t* const claim = claim_ptr();
+            const uint32_t k = __hip_atomic_fetch_add(claim + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (k == static_cast<uint32_t>(wt) - 1u) {
+                __hip_atomic_store(claim, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(claim + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
     };
     auto advance = [&](VrIt& it) __attribute__((always_inline)) -> bool { return locate(it, slot_group(take())); };
     auto group_base = [&](const VrIt& it) __attribute__((always_inline)) -> uint64_t {   // its first packet
@@ -792,6 +899,7 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     }
     if (!any) {
         trace_end();                                         // (the prologue's loads are retired)
+        rounds_exit();
         return;
     }
 
@@ -983,24 +1091,31 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
         if (done) break;
     }
     trace_end();
+    rounds_exit();
 }
 
 // ---------------------------------------------------------------- host side
 
+// the instance; dyn = its dynamic-rounds twin where one is built
 template <int LG, int TR = 0, int NT = 0, int ABL = 0, int BIN = 0, int WK = 0, int ROT = 0, int VF = 0>
-const void* vring_fn() {
+const void* vring_fn(bool dyn = false) {
+    if constexpr (TR != 1 && NT == 0 && ABL == 0 && WK == 0 && ROT == 0)
+        if (dyn) return reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT, VF, 1>);
     return reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT, VF>);
 }
 // receive verify (8 lanes per packet): the product instance; diagnostics: tail first, end records
 const void* vring_pick_v(bool trace, const VrVariant& v) {
-    if (!trace && !v.nt && !v.abl && !v.walk && !v.tail_first) return vring_fn<3, 0, 0, 0, 0, 0, 0, 1>();
+    const bool dyn = v.claim != nullptr;
+    if (!trace && !v.nt && !v.abl && !v.walk && !v.tail_first) return vring_fn<3, 0, 0, 0, 0, 0, 0, 1>(dyn);
 #ifdef ENET_HIP_DIAG
     if (!trace && !v.nt && !v.abl && !v.walk && v.tail_first) return vring_fn<3, 0, 0, 0, 0, 0, 1, 1>();
-    if (trace && v.abl == 128 && !v.nt && !v.walk && !v.tail_first) return vring_fn<3, 2, 0, 0, 0, 0, 0, 1>();
+    if (trace && v.abl == 128 && !v.nt && !v.walk && !v.tail_first) return vring_fn<3, 2, 0, 0, 0, 0, 0, 1>(dyn);
 #endif
     return nullptr;
 }
-const void* vring_pick_bin(int lg) { return lg == 2 ? vring_fn<2, 0, 0, 0, 1>() : vring_fn<3, 0, 0, 0, 1>(); }
+const void* vring_pick_bin(int lg, bool dyn) {
+    return lg == 2 ? vring_fn<2, 0, 0, 0, 1>(dyn) : vring_fn<3, 0, 0, 0, 1>(dyn);
+}
 
 // The product instances: 64 VGPRs (WPE 8), one or two workgroups per CU, stages in
 // window order.  The diagnostics library (ENET_HIP_DIAG) adds the sweep variants: a
@@ -1011,7 +1126,8 @@ const void* vring_pick_bin(int lg) { return lg == 2 ? vring_fn<2, 0, 0, 0, 1>() 
 const void* vring_pick(int lg, bool trace, const VrVariant& v) {
     if (lg != 2 && lg != 3) return nullptr;
     const bool plain = !trace && !v.nt && !v.abl && !v.walk && !v.tail_first;
-    if (plain) return lg == 2 ? vring_fn<2>() : vring_fn<3>();
+    const bool dyn = v.claim != nullptr;
+    if (plain) return lg == 2 ? vring_fn<2>(dyn) : vring_fn<3>(dyn);
 #ifdef ENET_HIP_DIAG
     const bool nt = v.nt;
     const int abl = v.abl;
@@ -1027,7 +1143,7 @@ const void* vring_pick(int lg, bool trace, const VrVariant& v) {
                        : (nt ? vring_fn<3, 0, 1, 0, 0, 1>() : vring_fn<3, 0, 0, 0, 0, 1>());
     }
     if (trace) {
-        if (abl == 128 && !nt) return lg == 2 ? vring_fn<2, 2>() : vring_fn<3, 2>();   // end records only
+        if (abl == 128 && !nt) return lg == 2 ? vring_fn<2, 2>(dyn) : vring_fn<3, 2>(dyn);   // end records only
         if (abl) return nullptr;
         return lg == 2 ? (nt ? vring_fn<2, 1, 1>() : vring_fn<2, 1>()) : (nt ? vring_fn<3, 1, 1>() : vring_fn<3, 1>());
     }
@@ -1058,28 +1174,34 @@ int vring_setup() {
         return e == hipSuccess ? 0 : -static_cast<int>(e);
     };
     static const int kAbl[] = {0, 1, 2, 3, 4, 6, 8, 19, 27, 32, 128};
-    for (int t = 0; t < 2; ++t)
-        for (int w = 0; w < 2; ++w) {
-            VrVariant v;
-            v.tail_first = w != 0;
-            v.abl = t ? 128 : 0;
-            const int rc = set(vring_pick_v(t != 0, v), kVrLds);
-            if (rc) return rc;
-        }
-    for (int lg = 2; lg <= 3; ++lg) {
-        int rc;
-        if ((rc = set(vring_pick_bin(lg), kVrLdsBin))) return rc;
+    static uint32_t any_line;                                // (a non-null claim selects the DYN twins)
+    for (int d = 0; d < 2; ++d) {
+        uint32_t* const claim = d ? &any_line : nullptr;
         for (int t = 0; t < 2; ++t)
-            for (int nt = 0; nt < 2; ++nt)
-                for (int abl : kAbl)
-                    for (int w = 0; w < 4; ++w) {
-                        VrVariant v;
-                        v.nt = nt != 0;
-                        v.abl = abl;
-                        v.walk = (w & 1) != 0;
-                        v.tail_first = (w & 2) != 0;
-                        if ((rc = set(vring_pick(lg, t != 0, v), kVrLds))) return rc;
-                    }
+            for (int w = 0; w < 2; ++w) {
+                VrVariant v;
+                v.tail_first = w != 0;
+                v.abl = t ? 128 : 0;
+                v.claim = claim;
+                const int rc = set(vring_pick_v(t != 0, v), kVrLds);
+                if (rc) return rc;
+            }
+        for (int lg = 2; lg <= 3; ++lg) {
+            int rc;
+            if ((rc = set(vring_pick_bin(lg, d != 0), kVrLdsBin))) return rc;
+            for (int t = 0; t < 2; ++t)
+                for (int nt = 0; nt < 2; ++nt)
+                    for (int abl : kAbl)
+                        for (int w = 0; w < 4; ++w) {
+                            VrVariant v;
+                            v.nt = nt != 0;
+                            v.abl = abl;
+                            v.walk = (w & 1) != 0;
+                            v.tail_first = (w & 2) != 0;
+                            v.claim = claim;
+                            if ((rc = set(vring_pick(lg, t != 0, v), kVrLds))) return rc;
+                        }
+        }
     }
     return 0;
 }
@@ -1088,11 +1210,12 @@ int vring_launch_list(int lg, int max_wgs, const VrVariant& v, hipStream_t st, c
                       const KernelTables& tb, const uint32_t* basis2, uint64_t* trace, bool bin) {
     if ((lg != 2 && lg != 3) || bl.count > static_cast<uint32_t>(kVrMaxBatches))
         return -static_cast<int>(hipErrorInvalidValue);
-    const void* fn = bin ? vring_pick_bin(lg) : vring_pick(lg, trace != nullptr, v);
+    const void* fn = bin ? vring_pick_bin(lg, v.claim != nullptr) : vring_pick(lg, trace != nullptr, v);
     if (!fn) return -static_cast<int>(hipErrorInvalidValue);   // a variant this library does not build
     // empty batches dropped: the kernel may then read any batch's packet n - 1
     VrBatches a{};
-    if (bin && bl.tile_counts && (bl.count != 1 || bl.b[0].n != 1024ull * bl.tiles))
+    a.claim = v.claim;
+    if (bin && (bl.count != 1 || (bl.tile_counts && bl.b[0].n != 1024ull * bl.tiles)))   // records: one batch
         return -static_cast<int>(hipErrorInvalidValue);
     a.tile_counts = bin ? bl.tile_counts : nullptr;
     a.tiles = bin ? bl.tiles : 0u;
@@ -1120,6 +1243,7 @@ int vring_launch_vlist(int max_wgs, const VrVariant& v, hipStream_t st, const Vr
     const void* fn = vring_pick_v(trace != nullptr, v);
     if (!fn) return -static_cast<int>(hipErrorInvalidValue);
     VrVBatches a{};                                          // empty batches dropped
+    a.claim = v.claim;
     for (uint32_t b = 0; b < bl.count; ++b)
         if (bl.b[b].n) a.b[a.count++] = bl.b[b];
     if (a.count == 0) return 0;

@@ -38,6 +38,9 @@ struct VrBatches {
     // and tile_counts[t] = tile t's kept records.  The kernel runs the groups of the
     // ranks q < ceil(max_t tile_counts[t] / kpk): a count the host does not know.
     const uint32_t* tile_counts;
+    // the launch's claim words {round counter, finished waves} (VrVariant::claim), or
+    // null for the static deal; zero between launches (the launch's last wave resets them)
+    uint32_t* claim;
     VrBatch b[kVrMaxBatches];
 };
 static_assert(sizeof(VrBatches) <= 3072, "kernel arguments");
@@ -61,6 +64,7 @@ struct VrVBatches {
     uint32_t count;
     uint32_t pad;
     uint64_t groups;
+    uint32_t* claim;    // as VrBatches::claim
     VrVBatch b[kVrMaxVBatches];
 };
 static_assert(sizeof(VrVBatches) <= 3072, "kernel arguments");
@@ -75,7 +79,11 @@ struct VrVariant {
     int abl = 0;
     bool walk = false;
     bool tail_first = false;
+    // dynamic rounds: the launch's claim words (VrBatches::claim; kVrClaimWords, zero,
+    // used by no other launch in flight), or null = the static deal
+    uint32_t* claim = nullptr;
 };
+constexpr int kVrClaimWords = 16;     // one 64-byte line per launch
 
 // Set the dynamic-LDS attribute of every vring kernel instance built (once per context).
 int vring_setup();

@@ -500,13 +500,8 @@ def _run_gather_binned(ctx, payload, seg_off, seg_len, seg_first):
     return out.cpu().numpy().view(np.uint32)[:n]
 
 
-def test_gather_binned(ctx, golden, oracle_lib):
-    """enet_hip_crc32_gather_binned_device (send-side gather lists, protocol.cs:1690-1698):
-    the golden multi-buffer vectors, cfg5's 3-segment DGRAMs, random gather lists of 0-65
-    segments (empty segments and empty DGRAMs among them, arbitrary byte alignment,
-    segments shared between DGRAMs), a list of only empty DGRAMs, lists of only short
-    segments (folded by the join) and of lengths around the join's 48-byte split, each
-    against the oracle's gather, at the default, 4 and 8 lanes and 1 / 2 workgroups per CU."""
+def _gather_cases(golden, oracle_lib):
+    """test_gather_binned's gather lists: (payload, seg_off, seg_len, seg_first, expected)."""
     vecs, blob = golden
     seg_off, seg_len, first, exp = [], [], [0], []
     for v in vecs:
@@ -548,6 +543,17 @@ def test_gather_binned(ctx, golden, oracle_lib):
     sl2 = rng.integers(1, 1500, size=ns2).astype(np.uint32)
     so2 = rng.integers(0, len(payload) - 1500, size=ns2).astype(np.uint64)
     cases.append((payload, so2, sl2, sf2, oracle_lib.gather(payload, so2, sl2, sf2)))
+    return cases
+
+
+def test_gather_binned(ctx, golden, oracle_lib):
+    """enet_hip_crc32_gather_binned_device (send-side gather lists, protocol.cs:1690-1698):
+    the golden multi-buffer vectors, cfg5's 3-segment DGRAMs, random gather lists of 0-65
+    segments (empty segments and empty DGRAMs among them, arbitrary byte alignment,
+    segments shared between DGRAMs), a list of only empty DGRAMs, lists of only short
+    segments (folded by the join) and of lengths around the join's 48-byte split, each
+    against the oracle's gather, at the default, 4 and 8 lanes and 1 / 2 workgroups per CU."""
+    cases = _gather_cases(golden, oracle_lib)
     try:
         for lanes, wgs in ((0, 0), (4, 0), (8, 0), (0, 1), (0, 2)):
             ctx.set_tuning(lanes, wgs)
@@ -826,3 +832,85 @@ def test_verify_dgrams_over_64k(ctx, oracle_lib):
         torch.cuda.synchronize()
         assert (d_ok.cpu().numpy() == exp_ok).all(), ("binned", lanes)
     ctx.set_tuning(0, 0)
+
+
+# ---- dynamic rounds (crc32_vring.hip: rounds >= 2 claimed from a per-launch counter)
+
+def test_dynamic_rounds_claim_lines_reused_across_streams(dctx, oracle_lib):
+    """More launches than the context's 256 claim lines, spread over three streams at
+    once, batch sizes from one group to several rounds per workgroup and lanes 4 / 8:
+    every launch's CRCs are exact (a claim line left non-zero, or shared by two
+    running launches, would skip or repeat chunks)."""
+    rng = np.random.default_rng(0xD1)
+    sizes = [1, 7, 9, 300, 4096, 20000, 65536]
+    batches = []
+    for i, n in enumerate(sizes):
+        lens = rng.integers(0, 1500, n).astype(np.uint32)
+        off = np.zeros(n, np.uint64)
+        off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+        payload = np.frombuffer(rng.bytes(int(lens.sum()) + 64), np.uint8).copy()
+        batches.append((dev(payload), dev(off), dev(lens), n, oracle_lib.batch(payload, off, lens, threads=16)))
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    ctx = dctx
+    try:
+        ctx.diag_ablation(524288)                     # the dynamic rounds
+        for lanes in (8, 4):
+            ctx.set_tuning(lanes, 0)
+            outs = []
+            for k in range(300):
+                d_p, d_o, d_l, n, exp = batches[k % len(batches)]
+                st = streams[k % 3]
+                out = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+                st.wait_stream(torch.cuda.current_stream())      # (the fill first: the side streams do not wait)
+                with torch.cuda.stream(st):
+                    ctx.crc32_batch_device(d_p, d_o, d_l, n, out, stream=st.cuda_stream)
+                outs.append((out, exp, k))
+            torch.cuda.synchronize()
+            for out, exp, k in outs:
+                assert (out.cpu().numpy().view(np.uint32) == exp).all(), (lanes, k)
+    finally:
+        ctx.diag_ablation(0)
+        ctx.set_tuning(0, 0)
+
+
+def test_dynamic_rounds_match_static_deal(dctx, oracle_lib):
+    """The dynamic rounds (diagnostics ablation 524288: CRCs still exact) and the static
+    deal give the same CRCs on cfg3's mixed lengths, single batches and lists."""
+    b = workloads.mixed(262144, 64, 1400, seed=0x44594E, name="cfg3")
+    exp = oracle_lib.batch(b.payload, b.off, b.lens, threads=16)
+    try:
+        for mode in (0, 524288):
+            dctx.diag_ablation(mode)
+            dctx.set_kernel_path(0)
+            got = run_batch(dctx, b.payload, b.off, b.lens)
+            assert (got == exp).all(), mode
+    finally:
+        dctx.diag_ablation(0)
+        dctx.set_tuning(0, 0)
+
+
+def test_gather_segment_parallel_join(dctx, golden, oracle_lib):
+    """The segment-parallel join (diagnostics A/B candidate, enet_hip_diag_ablation
+    8 x 1048576): test_gather_binned's lists, plus segment ranges that are not
+    nondecreasing in the DGRAM index (ranges overlapping and out of order)."""
+    cases = _gather_cases(golden, oracle_lib)
+    rng = np.random.default_rng(78)
+    payload = rng.integers(0, 256, size=1 << 20, dtype=np.uint8)
+    ns = 5000
+    sl = np.where(rng.integers(0, 6, size=ns) == 0, rng.integers(1, 48, size=ns),
+                  rng.integers(0, 3000, size=ns)).astype(np.uint32)
+    so = rng.integers(0, len(payload) - 3000, size=ns).astype(np.uint64)
+    sf = rng.integers(0, ns + 1, size=1201).astype(np.uint32)           # any order
+    cases.append((payload, so, sl, sf, oracle_lib.gather(payload, so, sl, np.maximum.accumulate(sf))))
+    try:
+        dctx.diag_ablation(8 << 20)
+        for i, (p, so, sl, f, e) in enumerate(cases):
+            got = _run_gather_binned(dctx, p, so, sl, f)
+            if i == len(cases) - 1:         # the unordered ranges: per DGRAM, [min(sf[d], s1), s1)
+                s1 = np.minimum(f[1:], len(sl))
+                s0 = np.minimum(f[:-1], s1)
+                e = np.array([oracle_lib.gather(p, so, sl, np.array([a, b], np.uint32))[0]
+                              for a, b in zip(s0, s1)], np.uint32)
+            assert (got == e).all(), (i, np.nonzero(got != e)[0][:5])
+    finally:
+        dctx.diag_ablation(0)

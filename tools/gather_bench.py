@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--lanes", type=int, default=0)
     ap.add_argument("--path", type=int, default=0, help="kernel path (enet_hip_set_kernel_path; 17 = vring records)")
     ap.add_argument("--only", choices=["gather", "gather_binned"], help="time one entry only")
+    ap.add_argument("--ablate", type=int, default=0, help="diagnostics: enet_hip_diag_ablation after the oracle "
+                                                               "check (wrong CRCs by design)")
     ap.add_argument("--probe", type=int, default=0, help="then run the read probe N times over the arena "
                                                               "(FETCH_SIZE calibration)")
     a = ap.parse_args()
@@ -38,7 +40,7 @@ def main():
     from enethip import workloads
     import oracle as orc
     g = workloads.cfg5(a.messages)
-    ctx = enethip.Context(0, a.lanes, 0, diag=a.path not in (0, 1, 2, 13, 17))
+    ctx = enethip.Context(0, a.lanes, 0, diag=a.path not in (0, 1, 2, 13, 17) or a.ablate != 0)
     if a.path:
         ctx.set_kernel_path(a.path)
     st = torch.cuda.Stream()
@@ -66,6 +68,9 @@ def main():
         torch.cuda.synchronize()
         ok = bool((out.cpu().numpy().view(np.uint32) == exp).all())
         assert ok, name + " differs from the oracle"
+        if a.ablate:
+            ctx.diag_ablation(a.ablate)
+            res["ablation"] = a.ablate
         for i in range(3):
             fn(i)
         torch.cuda.synchronize()
@@ -82,6 +87,8 @@ def main():
         res[name + "_GBps"] = round(g.dgram_bytes / us / 1e3, 1)
         res[name + "_GiBps"] = round(g.dgram_bytes / us * 1e6 / 2 ** 30, 1)
         res[name + "_bit_exact"] = ok
+        if a.ablate:
+            ctx.diag_ablation(0)
     if a.probe:
         sink = torch.zeros(4, dtype=torch.int32, device="cuda")
         for _ in range(a.probe):
