@@ -29,11 +29,11 @@ struct enet_hip_context {
     int ablation_prio = 0;       // diagnostics library: lean-kernel lagging-wave priority
     int ablation = 0;            // diagnostics library: ablations (wrong CRCs by design)
     int vr_abl = 0;              // diagnostics library: vring batch-list ablations
-    // vring dynamic rounds: a ring of claim lines (kVrClaimLines x kVrClaimWords, zero
-    // between launches), one per launch in turn; vr_dynamic = use them (diagnostics
-    // library A/B; the static deal is the default)
+    // vring dynamic rounds: a ring of claim lines (kVrClaimLines x kVrClaimWords, zeroed
+    // at creation), one per launch in turn, generation = the line's use count + 1;
+    // vr_dynamic = use them (diagnostics library A/B; the static deal is the default)
     uint32_t* d_rounds = nullptr;
-    std::atomic<uint32_t> rounds_next{0};
+    std::atomic<uint64_t> rounds_next{0};
     bool vr_dynamic = false;
     int join_abl = 0;            // diagnostics library: gather-join ablations
     // host-memory entry points (host_pipeline.hip): calls on one context serialize on mu

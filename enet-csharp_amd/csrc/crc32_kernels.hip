@@ -860,6 +860,13 @@ __global__ void __launch_bounds__(kThreads) crc32_gather_kernel(GatherArgs ga, K
 // offset, its last L mod 4 bytes Sarwate steps (T_3 .. T_0 = columns 6, 4, 2, 0 of
 // the P = 1 image, 4 KiB in LDS).  Restated in tests/kernel_model.py (fold_small).
 constexpr int kSmallDwords = (3 + static_cast<int>(kGatherSmall) + 3) / 4;
+static_assert(15 + kGatherSmall <= 16 * ((kSmallDwords + 1 + 3) / 4), "a short segment's aligned lines fit the join's loads");
+
+// p[i] as a GLOBAL load (a generic pointer makes hipcc emit a flat load)
+template <class T>
+__device__ __forceinline__ T gload(const T* p, uint64_t i) {
+    return *reinterpret_cast<__attribute__((address_space(1))) const T*>(reinterpret_cast<uintptr_t>(p + i));
+}
 
 __device__ __forceinline__ void load_small(const uint8_t* a, uint32_t L, uint32_t (&d)[kSmallDwords + 1]) {
     const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a)) & 3u;
@@ -889,52 +896,91 @@ __device__ __forceinline__ uint32_t fold_small(uint32_t reg, uint32_t sh, uint32
 
 // JV (diagnostics, wrong CRCs by design): bit 0 = no short-segment fold (its dwords
 // XORed in), bit 1 = no multiply (XOR), bit 2 = no short-segment loads
+// Global loads only (generic pointers made hipcc emit flat loads, which it waits for
+// with vmcnt(0) + lgkmcnt(0)), and no load under a branch: a load whose slot or
+// segment does not exist reads a valid stand-in address instead (the segment index
+// clamped into the DGRAM's range, the 256 zero bytes), so hipcc issues every load of
+// a chunk back to back and waits once.  (Round 3 form: per-dword flat loads under
+// branches, and seg_crc / x^(8 len) under branches each waited for at once -- 9.6 us
+// on cfg5 against 7.3 without the short-segment fold's loads and work.)
 template <int JV = 0>
 __global__ void __launch_bounds__(kThreads) crc32_gather_join_kernel(GatherArgs ga, const uint32_t* seg_crc,
                                                                      KernelTables tb, uint32_t small) {
     constexpr int kQ = 4;                                    // segments in flight per thread
+    constexpr int kC = (kSmallDwords + 1 + 3) / 4;           // 16-byte loads per short segment
     __shared__ uint32_t t4[4][256];
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
+    uint64_t d = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x;
+    // segFirst lives in device memory, so the host cannot check segFirst[n] ==
+    // segCount: clamp to the segments the binned pass filled (a short segCount then
+    // gives wrong CRCs for the DGRAMs past it, never a read past seg_crc).  The first
+    // DGRAM's bounds are loaded before the table fill's barrier.
+    auto bounds = [&](uint64_t dd, uint32_t& s0, uint32_t& s1) __attribute__((always_inline)) {
+        const uint64_t dc = min<uint64_t>(dd, ga.n - 1u);
+        const uint32_t a = gload(ga.seg_first, dc);
+        const uint32_t b = gload(ga.seg_first, dc + 1u);
+        s1 = static_cast<uint32_t>(min<uint64_t>(b, ga.segs));
+        s0 = min(a, s1);
+    };
+    uint32_t s0, s1;
+    bounds(d, s0, s1);
     if (small) {
         for (uint32_t i = threadIdx.x; i < 1024u; i += kThreads) t4[i >> 8][i & 255u] = tb.image[64u * (i & 255u) + 2u * (i >> 8)];
         __syncthreads();
     }
-    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
-    for (uint64_t d = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; d < ga.n; d += stride) {
-        // segFirst lives in device memory, so the host cannot check segFirst[n] ==
-        // segCount: clamp to the segments the binned pass filled (a short segCount
-        // then gives wrong CRCs for the DGRAMs past it, never a read past seg_crc)
-        const uint32_t s1 = static_cast<uint32_t>(min<uint64_t>(ga.seg_first[d + 1], ga.segs));
-        const uint32_t s0 = min(ga.seg_first[d], s1);
+    const uint64_t zero = reinterpret_cast<uint64_t>(tb.zero);
+    for (; d < ga.n; d += stride) {
         uint32_t reg = 0xFFFFFFFFu;
         for (uint32_t q0 = s0; q0 < s1; q0 += kQ) {
             uint32_t L[kQ];
-            const uint8_t* A[kQ];
+            uint64_t A[kQ];
 #pragma unroll
             for (int i = 0; i < kQ; ++i) {
-                const bool in = q0 + i < s1;
-                L[i] = in ? ga.seg_len[q0 + i] : 0u;
-                A[i] = ga.bytes + (in ? ga.seg_off[q0 + i] : 0u);
+                const uint32_t q = min(q0 + i, s1 - 1u);     // (s1 > q0: a valid segment)
+                const uint32_t l = gload(ga.seg_len, q);
+                A[i] = reinterpret_cast<uint64_t>(ga.bytes) + gload(ga.seg_off, q);
+                L[i] = q0 + i < s1 ? l : 0u;
             }
-            uint32_t D[kQ][kSmallDwords + 1], C[kQ], X[kQ];
+            uint32_t D[kQ][4 * kC], C[kQ], X[kQ];
 #pragma unroll
             for (int i = 0; i < kQ; ++i) {
                 const bool sm = L[i] != 0u && L[i] <= small && !(JV & 4);
-                if (sm) load_small(A[i], L[i], D[i]);
-                else
+                const uint64_t w = A[i] & ~static_cast<uint64_t>(15);
+                const uint32_t e = (static_cast<uint32_t>(A[i]) & 15u) + L[i];   // the segment's end in the lines
 #pragma unroll
-                    for (int k = 0; k <= kSmallDwords; ++k) D[i][k] = 0u;
-                C[i] = L[i] > small ? seg_crc[q0 + i] : 0u;
-                X[i] = L[i] > small ? tb.xn_lo[L[i] & 0xFFFFu] : 0u;
+                for (int c = 0; c < kC; ++c) {
+                    // 16-byte aligned loads that hold a byte of the segment (so never a page
+                    // the segment does not touch); the others, or not a short segment: zeros
+                    const u32x4 v = ldg16_addr((sm && 16u * c < e) ? w + 16u * c : zero);
+                    D[i][4 * c] = v.x;
+                    D[i][4 * c + 1] = v.y;
+                    D[i][4 * c + 2] = v.z;
+                    D[i][4 * c + 3] = v.w;
+                }
+                const bool lg = L[i] > small;
+                C[i] = gload(seg_crc, lg ? min(q0 + i, s1 - 1u) : 0u);
+                X[i] = gload(tb.xn_lo, L[i] & 0xFFFFu);
             }
 #pragma unroll
             for (int i = 0; i < kQ; ++i) {
                 if (L[i] == 0u) continue;
                 if (L[i] <= small) {
+                    // dwords past the segment's hold bytes of neighbours: fold_small reads only
+                    // the segment's (nf whole dwords, then L mod 4 bytes of the next)
+                    // from the segment's first dword on: o = (A >> 2) & 3 dwords dropped, by
+                    // two selects per dword (fold_small reads d[0 .. kSmallDwords - 1])
+                    const uint32_t o = (static_cast<uint32_t>(A[i]) >> 2) & 3u;
+                    uint32_t E[4 * kC], Dd[kSmallDwords + 1];
+#pragma unroll
+                    for (int k = 0; k < 4 * kC; ++k) E[k] = (o & 1u) ? (k + 1 < 4 * kC ? D[i][k + 1] : 0u) : D[i][k];
+#pragma unroll
+                    for (int k = 0; k < kSmallDwords; ++k) Dd[k] = (o & 2u) ? (k + 2 < 4 * kC ? E[k + 2] : 0u) : E[k];
+                    Dd[kSmallDwords] = 0u;
                     if constexpr (JV & 1) {
 #pragma unroll
-                        for (int k = 0; k <= kSmallDwords; ++k) reg ^= D[i][k];
+                        for (int k = 0; k <= kSmallDwords; ++k) reg ^= Dd[k];
                     } else {
-                        reg = fold_small(reg, static_cast<uint32_t>(reinterpret_cast<uintptr_t>(A[i])) & 3u, L[i], D[i], t4);
+                        reg = fold_small(reg, static_cast<uint32_t>(A[i]) & 3u, L[i], Dd, t4);
                     }
                 } else if constexpr (JV & 2) {
                     reg ^= X[i] ^ ~bswap32(C[i]);
@@ -944,88 +990,9 @@ __global__ void __launch_bounds__(kThreads) crc32_gather_join_kernel(GatherArgs 
                 }
             }
         }
-        ga.out[d] = finalize(reg);
+        *reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(reinterpret_cast<uintptr_t>(ga.out + d)) = finalize(reg);
+        bounds(d + stride, s0, s1);
     }
-}
-
-// The join, segment-parallel (diagnostics A/B against the thread-per-DGRAM join
-// above): a workgroup takes kJT DGRAMs and the window of their segments, kJT segments
-// at a time.  Lane j of a window step takes segment q = one of them: its length and
-// offset (coalesced), then its contribution -- a short segment's reg(0, B) folded
-// from its bytes, a long one's reg(0xFFFFFFFF, B) from seg_crc -- and x^(8 |B|), into
-// LDS.  Then DGRAM d's lane walks its segments of the step in order:
-// reg' = (reg ^ f) x^(8 |B|) ^ v, f = 0 for a short segment (reg(s, B) = adv(s) ^
-// reg(0, B)), f = 0xFFFFFFFF for a long one (as in the join above); an empty segment
-// is the identity (x^0 = 0x80000000 in the reflected order, v = 0).  Segment ranges
-// that are not nondecreasing in d still give the per-DGRAM results (the window is
-// the union of the ranges), only more window steps.
-constexpr int kJT = 256;
-constexpr uint32_t kGfOne = 0x80000000u;                    // x^0, reflected
-__global__ void __launch_bounds__(kJT) crc32_gather_join_seg_kernel(GatherArgs ga, const uint32_t* seg_crc,
-                                                                    KernelTables tb, uint32_t small) {
-    __shared__ uint32_t t4[4][256];
-    __shared__ uint32_t sv[kJT], sx[kJT], sf[kJT];
-    __shared__ uint32_t win[2];
-    const uint32_t t = threadIdx.x;
-    const uint64_t d = static_cast<uint64_t>(blockIdx.x) * kJT + t;
-    // this DGRAM's segment range (clamped as in the join above); lanes past n: empty
-    uint32_t s0 = 0xFFFFFFFFu, s1 = 0u;
-    if (d < ga.n) {
-        s1 = static_cast<uint32_t>(min<uint64_t>(ga.seg_first[d + 1], ga.segs));
-        s0 = min(ga.seg_first[d], s1);
-    }
-    if (small)
-        for (uint32_t i = t; i < 1024u; i += kJT) t4[i >> 8][i & 255u] = tb.image[64u * (i & 255u) + 2u * (i >> 8)];
-    // the window [min s0, max s1): wave reductions, then one LDS min / max
-    uint32_t lo = s0, hi = s1;
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-        lo = min(lo, static_cast<uint32_t>(__shfl_xor(static_cast<int>(lo), m)));
-        hi = max(hi, static_cast<uint32_t>(__shfl_xor(static_cast<int>(hi), m)));
-    }
-    if (t == 0u) {
-        win[0] = 0xFFFFFFFFu;
-        win[1] = 0u;
-    }
-    __syncthreads();
-    if ((t & 63u) == 0u) {
-        atomicMin(&win[0], lo);
-        atomicMax(&win[1], hi);
-    }
-    __syncthreads();
-    const uint32_t w0 = win[0], w1 = win[1];
-    uint32_t reg = 0xFFFFFFFFu;
-    for (uint32_t c = w0; c < w1; c += kJT) {                // (w0 = ~0: no segment in the workgroup)
-        const uint32_t q = c + t;
-        uint32_t v = 0u, x = kGfOne, f = 0u;
-        if (q < w1) {
-            const uint32_t L = ga.seg_len[q];
-            const uint8_t* a = ga.bytes + ga.seg_off[q];
-            if (L != 0u && L <= small) {
-                uint32_t D[kSmallDwords + 1];
-                load_small(a, L, D);
-                v = fold_small(0u, static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a)) & 3u, L, D, t4);
-                x = tb.xn_lo[L];
-            } else if (L != 0u) {
-                v = ~bswap32(seg_crc[q]);
-                x = tb.xn_lo[L & 0xFFFFu];
-                if (L >> 16) x = mulmod(x, tb.xn_hi[L >> 16]);
-                f = 0xFFFFFFFFu;
-            }
-        }
-        sv[t] = v;
-        sx[t] = x;
-        sf[t] = f;
-        __syncthreads();
-        const uint32_t a0 = max(s0, c), a1 = min(s1, c + kJT);
-        for (uint32_t k = a0; k < a1; ++k) {
-            const uint32_t i = k - c;
-            const uint32_t r = reg ^ sf[i];
-            reg = (r == 0u ? 0u : mulmod(r, sx[i])) ^ sv[i];
-        }
-        __syncthreads();
-    }
-    if (d < ga.n) ga.out[d] = finalize(reg);
 }
 
 // Read-roofline probe: every byte loaded once by 16-byte coalesced loads,
@@ -1366,17 +1333,20 @@ int vring_wgs(const enet_hip_context* ctx, size_t batches) {
 bool vring_path(const enet_hip_context* ctx) {
     return ctx->path == 0 || (ctx->path >= kVringPath && ctx->path <= kVringTailFirstPath);
 }
-// The claim line of the next vring launch (dynamic rounds), or null (static deal).
-// Lines are handed out in turn: a line is reused kVrClaimLines launches later, when
-// the launch that used it has ended (the context's launches run on at most a few
-// streams at once).
+// The claim line of the next vring launch (dynamic rounds) and its generation, or
+// null (static deal).  Lines are handed out in turn: a line is reused kVrClaimLines
+// launches later, when the launch that used it has ended (the context's launches run
+// on at most a few streams at once), with a generation one larger, so the kernel
+// needs no reset of it (crc32_vring.hip vr_claim_next).  After 2^32 - 2 uses of a
+// line (2^40 launches) the context falls back to the static deal.
 constexpr uint32_t kVrClaimLines = 256;
-uint32_t* vring_claim(enet_hip_context* ctx) {
-    if (!ctx->vr_dynamic || !ctx->d_rounds) return nullptr;
-    return ctx->d_rounds + static_cast<size_t>(kVrClaimWords) * (ctx->rounds_next.fetch_add(1u) % kVrClaimLines);
-}
 VrVariant with_claim(enet_hip_context* ctx, VrVariant v) {
-    if (!v.walk) v.claim = vring_claim(ctx);
+    if (v.walk || !ctx->vr_dynamic || !ctx->d_rounds) return v;
+    const uint64_t seq = ctx->rounds_next.fetch_add(1u);
+    const uint64_t gen = seq / kVrClaimLines + 1u;
+    if (gen >= 0xFFFFFFFFull) return v;
+    v.claim = reinterpret_cast<uint64_t*>(ctx->d_rounds + static_cast<size_t>(kVrClaimWords) * (seq % kVrClaimLines));
+    v.claim_gen = static_cast<uint32_t>(gen);
     return v;
 }
 VrVariant vring_variant(const enet_hip_context* ctx, bool lists) {
@@ -1586,8 +1556,8 @@ int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgro
 
 #ifdef ENET_HIP_DIAG
 int enet_hip_diag_ablation(enet_hip_context* ctx, int mode) {
-    if (!ctx || mode < 0 || mode >= (1 << 24)) return -static_cast<int>(hipErrorInvalidValue);
-    ctx->join_abl = (mode >> 20) & 15;                       // 1048576 x (1..7): gather-join ablations, x 8: segment-parallel join
+    if (!ctx || mode < 0 || mode >= (1 << 23)) return -static_cast<int>(hipErrorInvalidValue);
+    ctx->join_abl = (mode >> 20) & 7;                        // 1048576 x (1..7): gather-join ablations
     ctx->vr_dynamic = (mode >> 19) & 1;                      // 524288: vring dynamic rounds
     const int prio = (mode & 1024) ? 2 : (mode >> 3) & 1;    // 8: static / 1024: progress priority
     ctx->vr_abl = (mode >> 11) & 255;                        // 2048 ... 262144: vring ablations / end records
@@ -1893,10 +1863,6 @@ int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* by
         case 3: hipLaunchKernelGGL(crc32_gather_join_kernel<3>, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx), small); break;
         case 5: hipLaunchKernelGGL(crc32_gather_join_kernel<5>, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx), small); break;
         case 7: hipLaunchKernelGGL(crc32_gather_join_kernel<7>, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx), small); break;
-        case 8:
-            hipLaunchKernelGGL(crc32_gather_join_seg_kernel, dim3(static_cast<unsigned>((dgramCount + kJT - 1) / kJT)),
-                               dim3(kJT), 0, st, ga, seg_crc, tables_of(ctx), small);
-            break;
         default: hipLaunchKernelGGL(crc32_gather_join_kernel<0>, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx), small);
     }
 #else

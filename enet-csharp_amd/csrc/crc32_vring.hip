@@ -435,34 +435,65 @@ __device__ __forceinline__ uint32_t vr_lookups(const uint32_t (&d)[8], const VrS
 // take more groups and the workgroup's waves end together: with a static deal the
 // waves of a 20-batch launch ended between 40 % and 100 % of its span
 // (tools/list_timeline.py, profiles/r02d_list_timeline_*).
-// Dynamic rounds (VrBatches::claim set): a round is a chunk of 16 groups, workgroup
-// k's rounds 0 and 1 are chunks k and G + k (G workgroups) as above, and each later
-// round is claimed from the launch's round counter (chunk 2 G + c), so the
-// workgroups the chip favours take more chunks and the launch's workgroups end
-// together too.  The wave taking the first slot of round r >= 1 claims round r + 1
-// (after round r's claim is published: a workgroup's chunks ascend) and publishes
-// it in the LDS round table; a wave taking a slot of round r >= 2 reads round r's
-// entry (polled: published at least 16 slots earlier).  Live slots stay a prefix of
+// Dynamic rounds (DYN, VrBatches::claim set): a round is a chunk of 16 groups,
+// workgroup k's rounds 0, 1 and 2 are chunks k, G + k and 2 G + k (G workgroups; all
+// taken statically, so no claim is made in the prologue), and each later round is
+// claimed from the launch's claim word (chunk 3 G + c), so the workgroups the chip
+// favours take more chunks and the launch's workgroups end together too.  The wave
+// taking the first slot of round r >= 2 claims round r + 1 (after round r's claim is
+// published when r >= 3: a workgroup's chunks ascend) and publishes it in the LDS
+// round table; a wave taking a slot of round r >= 3 reads round r's entry (polled:
+// published at least 16 slots earlier).  Live slots stay a prefix of
 // the slot sequence (chunks ascend, a chunk's dead groups are its last ones), so the
 // waves stop at the first dead slot as before and no claimed live chunk is left.
 // Dynamic rounds.  The helpers take wave-uniform (SGPR) operands and build their
 // VGPR operands inside the asm: constants the compiler could see (LDS addresses, the
 // atomic's 1) were hoisted out of the ring loop into VGPRs held across it.
-// vr_claim_next: lane 0 adds 1 to the launch's round counter (its address stored at
-// kVrClaimPtr) and waits for the old value -- a returning device-scope atomic; the
-// wait retires the wave's ring loads too, once per round of 16 groups per workgroup.
+// vr_claim_next: lane 0 takes the next chunk number of the launch from its claim
+// word {generation, count} (address and generation at kVrClaimPtr): a returning
+// 64-bit device-scope add, waited for (which retires the wave's ring loads too, once
+// per round of 16 groups per workgroup).  A word still tagged with an older
+// generation (a launch before this one used the line) is moved to {gen, 0} by a
+// 64-bit max, and the add repeated: no reset between launches, so no end-of-launch
+// atomics.  (Round 4's first form counted the waves ending on one word to reset it:
+// 8192 returning atomics on one address at the launch's end, serialised at the
+// chip's ~88 per us, added 40-90 us.)  A newer generation (not possible while the
+// host hands out the lines in turn) gives ~0: chunks past the end.
 __device__ __forceinline__ uint32_t vr_claim_next() {
     uint32_t c = 0;
     if ((threadIdx.x & 63u) == 0u) {
         uint32_t t;
-        uint64_t p;
-        asm volatile("v_mov_b32 %1, %3\n\t"
-                     "ds_read_b64 %2, %1\n\t"
-                     "s_waitcnt lgkmcnt(0)\n\t"
-                     "v_mov_b32 %1, 1\n\t"
-                     "global_atomic_add %0, %2, %1, off sc0\n\t"
-                     "s_waitcnt vmcnt(0)"
-                     : "=&v"(c), "=&v"(t), "=&v"(p) : "i"(kVrClaimPtr) : "memory");
+        uint64_t p, old;
+        asm volatile("v_mov_b32 %0, %2\n\t"
+                     "ds_read_b64 %1, %0\n\t"
+                     "s_waitcnt lgkmcnt(0)"
+                     : "=&v"(t), "=&v"(p) : "i"(kVrClaimPtr) : "memory");
+        uint32_t gen;
+        asm volatile("v_mov_b32 %0, %1\n\t"
+                     "ds_read_b32 %0, %0 offset:8\n\t"
+                     "s_waitcnt lgkmcnt(0)"
+                     : "=&v"(gen) : "i"(kVrClaimPtr) : "memory");
+        for (;;) {
+            uint32_t one32;                                  // (made here, not a constant hoisted out of the ring loop)
+            asm volatile("v_mov_b32 %0, 1" : "=v"(one32));
+            const uint64_t one = one32;
+            asm volatile("global_atomic_add_x2 %0, %1, %2, off sc0\n\t"
+                         "s_waitcnt vmcnt(0)"
+                         : "=&v"(old) : "v"(p), "v"(one) : "memory");
+            const uint32_t g = static_cast<uint32_t>(old >> 32);
+            if (g == gen) {
+                c = static_cast<uint32_t>(old);
+                break;
+            }
+            if (g > gen) {
+                c = ~0u;
+                break;
+            }
+            const uint64_t tag = static_cast<uint64_t>(gen) << 32;
+            asm volatile("global_atomic_umax_x2 %0, %1, %2, off sc0\n\t"
+                         "s_waitcnt vmcnt(0)"
+                         : "=&v"(old) : "v"(p), "v"(tag) : "memory");
+        }
     }
     return __builtin_amdgcn_readfirstlane(c);
 }
@@ -564,16 +595,17 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     const uint64_t wv = static_cast<uint64_t>(blockIdx.x) * kVrW + wave;
     const uint64_t wt = static_cast<uint64_t>(gridDim.x) * kVrW;
     constexpr bool kDyn = DYN != 0 && !WK;
+    // slots taken statically per wave: rounds 0 .. kStatic - 1 are chunks k + r G
+    constexpr uint32_t kStatic = kDyn ? 3u : 2u;
     if constexpr (kDyn) {                                    // wave 0, before its takes: no round published
         if (threadIdx.x < static_cast<uint32_t>(kVrRounds)) lds_store(kVrRound + 8u * threadIdx.x, ~0u);
-        if (threadIdx.x < 2u)
+        // the claim word's address and generation (read where used: held across the
+        // ring loop they cost SGPRs)
+        if (threadIdx.x < 3u)
             lds_store(kVrClaimPtr + 4u * threadIdx.x,
-                      static_cast<uint32_t>(reinterpret_cast<uint64_t>(bl.claim) >> (32u * threadIdx.x)));
+                      threadIdx.x < 2u ? static_cast<uint32_t>(reinterpret_cast<uint64_t>(bl.claim) >> (32u * threadIdx.x))
+                                       : bl.claim_gen);
     }
-    // the claim words (read where used: a pointer held across the ring loop costs SGPRs)
-    auto claim_ptr = [&]() __attribute__((always_inline)) -> uint32_t* {
-        return reinterpret_cast<uint32_t*>(lds_load(kVrClaimPtr) | (static_cast<uint64_t>(lds_load(kVrClaimPtr + 4u)) << 32));
-    };
     auto lane_k = [&]() __attribute__((always_inline)) { return lane & (P - 1u); };   // block lane
     auto lane_p = [&]() __attribute__((always_inline)) { return lane >> LG; };         // packet of the group
     const uint64_t zero = reinterpret_cast<uint64_t>(tb.zero);
@@ -613,7 +645,7 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     const uint64_t gw = WK ? (ngroups_all + gridDim.x - 1u) / gridDim.x : 0u;
     auto slot_group = [&](uint32_t sl) __attribute__((always_inline)) -> uint64_t {
         if constexpr (WK) return sl < gw ? static_cast<uint64_t>(blockIdx.x) * gw + sl : ~0ull;
-        if (kDyn && sl >= 2u * kVrW) return static_cast<uint64_t>(vr_round_chunk(sl / kVrW)) * kVrW + (sl & (kVrW - 1u));
+        if (kDyn && sl >= kStatic * kVrW) return static_cast<uint64_t>(vr_round_chunk(sl / kVrW)) * kVrW + (sl & (kVrW - 1u));
         return static_cast<uint64_t>(blockIdx.x) * kVrW + (sl & (kVrW - 1u)) + static_cast<uint64_t>(sl / kVrW) * wt;
     };
     // `it` moved to global group gg (its batch found from it.b on: a wave's groups
@@ -626,11 +658,11 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
         return true;
     };
     uint32_t taken = 0;                                      // slots this wave has taken
-    // the next slot: the first two static, later ones from the workgroup's counter
+    // the next slot: the first kStatic static, later ones from the workgroup's counter
     uint32_t last_slot = 0;                                  // (TR 2: the last slot taken)
     auto take = [&]() __attribute__((always_inline)) -> uint32_t {
         uint32_t sl = 0;
-        if (taken < 2u) {
+        if (taken < kStatic) {
             sl = wave + kVrW * taken;
         } else {
             // ds_add_rtn as inline asm: as a C++ atomic, hipcc put an s_waitcnt vmcnt(0)
@@ -645,24 +677,15 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
             if constexpr (TR == 2) last_slot = sl;
         }
         ++taken;
-        if (kDyn && sl >= kVrW && (sl & (kVrW - 1u)) == 0u) {   // the first slot of round r >= 1: claim r + 1
+        // the first slot of round r >= kStatic - 1: claim round r + 1, after round r's
+        // claim is published if r is dynamic (a workgroup's chunks ascend)
+        if (kDyn && sl >= (kStatic - 1u) * kVrW && (sl & (kVrW - 1u)) == 0u) {
             const uint32_t r = sl / kVrW;
-            if (r >= 2u) (void)vr_round_chunk(r);            // round r's claim is published (chunks ascend)
-            vr_round_publish(r + 1u, static_cast<uint32_t>(wt / (kVrW / 2u)) + vr_claim_next());   // 2 G + c
+            if (r >= kStatic) (void)vr_round_chunk(r);
+            const uint32_t c = vr_claim_next();
+            vr_round_publish(r + 1u, c == ~0u ? c : static_cast<uint32_t>(wt / kVrW) * kStatic + c);   // kStatic G + c
         }
         return sl;
-    };
-    // every wave at its end: the last of the launch zeroes the claim words for the
-    // next launch using them (every claim of the launch is retired by then)
-    auto rounds_exit = [&]() __attribute__((always_inline)) {
-        if (kDyn && (threadIdx.x & 63u) == 0u) {
-            uint32_t* const claim = claim_ptr();
-            const uint32_t k = __hip_atomic_fetch_add(claim + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (k == static_cast<uint32_t>(wt) - 1u) {
-                __hip_atomic_store(claim, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(claim + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
     };
     auto advance = [&](VrIt& it) __attribute__((always_inline)) -> bool { return locate(it, slot_group(take())); };
     auto group_base = [&](const VrIt& it) __attribute__((always_inline)) -> uint64_t {   // its first packet
@@ -865,9 +888,9 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     // writes rows w + 16 i: row j = XOR of basis rows b with bit b of j set (Gray
     // order: one XOR per row), except the INIT and CINV dwords (not linear in j),
     // whose rows < 64 come from basis rows 8 and 9.  Raw s_barrier: no vmcnt drain.
-    // the slot counter: slots 0 .. 2 kVrW - 1 are taken statically; the first dynamic
+    // the slot counter: slots 0 .. kStatic kVrW - 1 are taken statically; the first dynamic
     // take comes after barrier B (a wave's second group is entered in the loop)
-    if (threadIdx.x == 0u) lds_store(BIN ? kVrCtrBin : kVrCtr, 2u * kVrW);
+    if (threadIdx.x == 0u) lds_store(BIN ? kVrCtrBin : kVrCtr, kStatic * kVrW);
     __builtin_amdgcn_s_barrier();                            // (A) every basis row has landed
     {
         uint32_t bb[8];
@@ -899,7 +922,6 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     }
     if (!any) {
         trace_end();                                         // (the prologue's loads are retired)
-        rounds_exit();
         return;
     }
 
@@ -1091,7 +1113,6 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
         if (done) break;
     }
     trace_end();
-    rounds_exit();
 }
 
 // ---------------------------------------------------------------- host side
@@ -1174,9 +1195,9 @@ int vring_setup() {
         return e == hipSuccess ? 0 : -static_cast<int>(e);
     };
     static const int kAbl[] = {0, 1, 2, 3, 4, 6, 8, 19, 27, 32, 128};
-    static uint32_t any_line;                                // (a non-null claim selects the DYN twins)
+    static uint64_t any_line;                                // (a non-null claim selects the DYN twins)
     for (int d = 0; d < 2; ++d) {
-        uint32_t* const claim = d ? &any_line : nullptr;
+        uint64_t* const claim = d ? &any_line : nullptr;
         for (int t = 0; t < 2; ++t)
             for (int w = 0; w < 2; ++w) {
                 VrVariant v;
@@ -1215,6 +1236,7 @@ int vring_launch_list(int lg, int max_wgs, const VrVariant& v, hipStream_t st, c
     // empty batches dropped: the kernel may then read any batch's packet n - 1
     VrBatches a{};
     a.claim = v.claim;
+    a.claim_gen = v.claim_gen;
     if (bin && (bl.count != 1 || (bl.tile_counts && bl.b[0].n != 1024ull * bl.tiles)))   // records: one batch
         return -static_cast<int>(hipErrorInvalidValue);
     a.tile_counts = bin ? bl.tile_counts : nullptr;
@@ -1230,7 +1252,7 @@ int vring_launch_list(int lg, int max_wgs, const VrVariant& v, hipStream_t st, c
     const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(
         1, std::min<uint64_t>((a.groups + kVrW - 1) / kVrW, static_cast<uint64_t>(max_wgs))));
     // slots are 32-bit: a workgroup's slot count (rounds x 16) must fit
-    if ((a.groups / (static_cast<uint64_t>(grid) * kVrW) + 2u) * kVrW > 0xFFFFFFF0ull)
+    if ((a.groups / (static_cast<uint64_t>(grid) * kVrW) + 3u) * kVrW > 0xFFFFFFF0ull)
         return -static_cast<int>(hipErrorInvalidValue);
     void* args[] = {&a, const_cast<KernelTables*>(&tb), const_cast<const uint32_t**>(&basis2), &trace};
     const hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(64 * kVrW), args, bin ? kVrLdsBin : kVrLds, st);
@@ -1244,6 +1266,7 @@ int vring_launch_vlist(int max_wgs, const VrVariant& v, hipStream_t st, const Vr
     if (!fn) return -static_cast<int>(hipErrorInvalidValue);
     VrVBatches a{};                                          // empty batches dropped
     a.claim = v.claim;
+    a.claim_gen = v.claim_gen;
     for (uint32_t b = 0; b < bl.count; ++b)
         if (bl.b[b].n) a.b[a.count++] = bl.b[b];
     if (a.count == 0) return 0;
@@ -1253,7 +1276,7 @@ int vring_launch_vlist(int max_wgs, const VrVariant& v, hipStream_t st, const Vr
     }
     const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(
         1, std::min<uint64_t>((a.groups + kVrW - 1) / kVrW, static_cast<uint64_t>(max_wgs))));
-    if ((a.groups / (static_cast<uint64_t>(grid) * kVrW) + 2u) * kVrW > 0xFFFFFFF0ull)
+    if ((a.groups / (static_cast<uint64_t>(grid) * kVrW) + 3u) * kVrW > 0xFFFFFFF0ull)
         return -static_cast<int>(hipErrorInvalidValue);
     void* args[] = {&a, const_cast<KernelTables*>(&tb), const_cast<const uint32_t**>(&basis2), &trace};
     const hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(64 * kVrW), args, kVrLds, st);

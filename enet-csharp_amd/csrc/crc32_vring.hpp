@@ -38,9 +38,11 @@ struct VrBatches {
     // and tile_counts[t] = tile t's kept records.  The kernel runs the groups of the
     // ranks q < ceil(max_t tile_counts[t] / kpk): a count the host does not know.
     const uint32_t* tile_counts;
-    // the launch's claim words {round counter, finished waves} (VrVariant::claim), or
-    // null for the static deal; zero between launches (the launch's last wave resets them)
-    uint32_t* claim;
+    // dynamic rounds (VrVariant::claim): the launch's claim word, or null for the
+    // static deal, and the launch's generation of it
+    uint64_t* claim;
+    uint32_t claim_gen;
+    uint32_t pad;
     VrBatch b[kVrMaxBatches];
 };
 static_assert(sizeof(VrBatches) <= 3072, "kernel arguments");
@@ -62,9 +64,9 @@ struct VrVBatch {
 constexpr int kVrMaxVBatches = 32;
 struct VrVBatches {
     uint32_t count;
-    uint32_t pad;
+    uint32_t claim_gen;  // as VrBatches::claim_gen
     uint64_t groups;
-    uint32_t* claim;    // as VrBatches::claim
+    uint64_t* claim;     // as VrBatches::claim
     VrVBatch b[kVrMaxVBatches];
 };
 static_assert(sizeof(VrVBatches) <= 3072, "kernel arguments");
@@ -79,11 +81,13 @@ struct VrVariant {
     int abl = 0;
     bool walk = false;
     bool tail_first = false;
-    // dynamic rounds: the launch's claim words (VrBatches::claim; kVrClaimWords, zero,
-    // used by no other launch in flight), or null = the static deal
-    uint32_t* claim = nullptr;
+    // dynamic rounds: the launch's claim word {generation, round counter} (64 bits, in
+    // a line no launch in flight shares) and generation -- larger than any generation
+    // the word has seen -- or null = the static deal
+    uint64_t* claim = nullptr;
+    uint32_t claim_gen = 0;
 };
-constexpr int kVrClaimWords = 16;     // one 64-byte line per launch
+constexpr int kVrClaimWords = 16;     // 32-bit words: one 64-byte line per launch
 
 // Set the dynamic-LDS attribute of every vring kernel instance built (once per context).
 int vring_setup();

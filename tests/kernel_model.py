@@ -711,6 +711,90 @@ def vring_dynamic_deal(batch_groups, grid: int, rng, W: int = 16):
     return seen, per_wave, total
 
 
+def vring_dynamic_rounds_deal(batch_groups, grid: int, rng, W: int = 16, K: int = 64, S: int = 3):
+    """Simulate one launch of the vring kernel's dynamic rounds (crc32_vring.hip DYN:
+    take / vr_claim_next / vr_round_publish / vr_round_chunk), all workgroups' waves
+    interleaved at random: rounds r < S (S = 3 static takes) of workgroup k are chunks
+    k + r G; the wave taking slot 16 r (r >= S - 1) waits for round r's entry (r >= S),
+    claims a chunk S G + c from the launch's counter -- the atomic completing at a
+    random later step, the wave blocked meanwhile -- and publishes it as round r + 1; a
+    wave taking a slot of round r >= S waits for round r's entry.  A slot maps to group 16 chunk + slot % 16
+    and a wave stops at its first group past the end.  Checks that no wave waits
+    forever and that no round entry (K of them, r % K) is rewritten while a wave that
+    took a slot of its round has not read it yet; returns {global group: (batch, local
+    group)}, the groups per wave and the launch's groups."""
+    g0, total = [], 0
+    for n in batch_groups:
+        g0.append(total)
+        total += n
+    G = grid
+    counter = 0
+    seen, per_wave = {}, []
+    wgs = [dict(ctr=S * W, pub={}, unread={}) for _ in range(G)]
+    # per wave: wg, wave, slots taken, batch cursor, state, slot, groups
+    waves = [dict(k=k, w=w, taken=0, b=0, st="take", sl=0, n=0) for k in range(G) for w in range(W)]
+    alive = set(range(len(waves)))
+
+    def ready(v):
+        wg, r = wgs[v["k"]], v["sl"] // W
+        if v["st"] in ("take", "claiming"):
+            return True                                     # (claiming: the atomic may complete)
+        if v["st"] == "claim_src":                          # the claimer waits for round r's entry
+            return r < S or r in wg["pub"]
+        if v["st"] == "read":
+            return r < S or r in wg["pub"]
+        raise AssertionError(v["st"])
+
+    steps = 0
+    while alive:
+        steps += 1
+        assert steps < 100 * (total + G * W) + 10000, "no progress"
+        enabled = [i for i in alive if ready(waves[i])]
+        assert enabled, "deadlock: every live wave waits"
+        v = waves[rng.choice(enabled)]
+        wg = wgs[v["k"]]
+        if v["st"] == "take":
+            if v["taken"] < S:
+                v["sl"] = v["w"] + W * v["taken"]
+            else:
+                v["sl"] = wg["ctr"]
+                wg["ctr"] += 1
+            v["taken"] += 1
+            r = v["sl"] // W
+            if r >= S:
+                wg["unread"][r] = wg["unread"].get(r, 0) + 1
+            v["st"] = "claim_src" if (r >= S - 1 and v["sl"] % W == 0) else "read"
+        elif v["st"] == "claim_src":
+            v["st"] = "claiming"
+        elif v["st"] == "claiming":                         # the atomic returns: publish round r + 1
+            r1 = v["sl"] // W + 1
+            assert not wg["unread"].get(r1 - K), "round entry rewritten while still to be read"
+            wg["pub"].pop(r1 - K, None)
+            wg["pub"][r1] = S * G + counter
+            counter += 1
+            v["st"] = "read"
+        else:                                               # read: the slot's group
+            r = v["sl"] // W
+            chunk = v["k"] + r * G if r < S else wg["pub"][r]
+            if r >= S:
+                wg["unread"][r] -= 1
+            gg = W * chunk + v["sl"] % W
+            if gg >= total:
+                alive.discard(id_ := waves.index(v))
+                per_wave.append(v["n"])
+                continue
+            b = v["b"]
+            while b + 1 < len(g0) and gg >= g0[b + 1]:
+                b += 1
+            assert not seen or v["n"] == 0 or gg > v.get("last", -1), "a wave's groups ascend"
+            v["b"], v["last"] = b, gg
+            assert gg not in seen, f"group {gg} taken twice"
+            seen[gg] = (b, gg - g0[b])
+            v["n"] += 1
+            v["st"] = "take"
+    return seen, per_wave, total
+
+
 # ---------------------------------------------------------------- gather join
 def gather_join(seg_crcs, seg_lens) -> int:
     """crc32_gather_join_kernel (enet_hip_crc32_gather_binned_device): a DGRAM's CRC from

@@ -888,29 +888,3 @@ def test_dynamic_rounds_match_static_deal(dctx, oracle_lib):
         dctx.diag_ablation(0)
         dctx.set_tuning(0, 0)
 
-
-def test_gather_segment_parallel_join(dctx, golden, oracle_lib):
-    """The segment-parallel join (diagnostics A/B candidate, enet_hip_diag_ablation
-    8 x 1048576): test_gather_binned's lists, plus segment ranges that are not
-    nondecreasing in the DGRAM index (ranges overlapping and out of order)."""
-    cases = _gather_cases(golden, oracle_lib)
-    rng = np.random.default_rng(78)
-    payload = rng.integers(0, 256, size=1 << 20, dtype=np.uint8)
-    ns = 5000
-    sl = np.where(rng.integers(0, 6, size=ns) == 0, rng.integers(1, 48, size=ns),
-                  rng.integers(0, 3000, size=ns)).astype(np.uint32)
-    so = rng.integers(0, len(payload) - 3000, size=ns).astype(np.uint64)
-    sf = rng.integers(0, ns + 1, size=1201).astype(np.uint32)           # any order
-    cases.append((payload, so, sl, sf, oracle_lib.gather(payload, so, sl, np.maximum.accumulate(sf))))
-    try:
-        dctx.diag_ablation(8 << 20)
-        for i, (p, so, sl, f, e) in enumerate(cases):
-            got = _run_gather_binned(dctx, p, so, sl, f)
-            if i == len(cases) - 1:         # the unordered ranges: per DGRAM, [min(sf[d], s1), s1)
-                s1 = np.minimum(f[1:], len(sl))
-                s0 = np.minimum(f[:-1], s1)
-                e = np.array([oracle_lib.gather(p, so, sl, np.array([a, b], np.uint32))[0]
-                              for a, b in zip(s0, s1)], np.uint32)
-            assert (got == e).all(), (i, np.nonzero(got != e)[0][:5])
-    finally:
-        dctx.diag_ablation(0)

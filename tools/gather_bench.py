@@ -23,6 +23,47 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import numpy as np  # noqa: E402
 
 
+def cpu_gather(lib, g, budget_s: float, runs: int = 5) -> dict:
+    """The oracle's gather (kind "port") on contiguous DGRAM ranges, one Python thread
+    per range (the ctypes call releases the GIL): 1 thread, then bench.py's thread
+    count; GiB/s of DGRAM bytes, the median of `runs` runs over a sample sized to the
+    budget."""
+    import threading
+    import time
+    sys.path.insert(0, ROOT)
+    import bench
+    threads, info = bench.baseline_threads(0)
+    sf = g.seg_first.astype(np.uint64)
+    lens = g.seg_len.astype(np.uint64)
+    csum = np.concatenate([[0], np.cumsum(lens)])
+    dbytes = csum[sf[1:]] - csum[sf[:-1]]                   # bytes per DGRAM
+
+    def run(n_dg: int, th: int) -> float:
+        cuts = np.linspace(0, n_dg, th + 1).astype(np.int64)
+        ts = [threading.Thread(target=lib.gather, args=(g.payload, g.seg_off, g.seg_len,
+                                                         g.seg_first[cuts[i]:cuts[i + 1] + 1]))
+              for i in range(th)]
+        t0 = time.perf_counter()
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        return time.perf_counter() - t0
+
+    res = {"kind": "port", "host": info, "unit": "GiB/s of DGRAM bytes"}
+    for label, th in (("1thread", 1), ("all", threads)):
+        k = min(g.n, 2000 * th)
+        dt = max(run(k, th), 1e-6)
+        rate = float(dbytes[:k].sum()) / dt
+        n_dg = int(min(g.n, max(k, k * (budget_s / 2 / runs) * rate / max(1.0, float(dbytes[:k].sum())))))
+        nb = float(dbytes[:n_dg].sum())
+        rates = [nb / run(n_dg, th) / 2 ** 30 for _ in range(runs)]
+        res[label] = dict(gibps=round(float(np.median(rates)), 3), threads=th, dgrams=n_dg, runs=runs,
+                          spread=[round(min(rates), 3), round(max(rates), 3)])
+    res["speedup"] = round(res["all"]["gibps"] / max(res["1thread"]["gibps"], 1e-9), 2)
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--messages", type=int, default=4096)
@@ -32,6 +73,10 @@ def main():
     ap.add_argument("--only", choices=["gather", "gather_binned"], help="time one entry only")
     ap.add_argument("--ablate", type=int, default=0, help="diagnostics: enet_hip_diag_ablation after the oracle "
                                                                "check (wrong CRCs by design)")
+    ap.add_argument("--cpu-seconds", type=float, default=0.0,
+                    help="also time the oracle's gather (the 3-buffer lists, packet.cs:142-160 over "
+                         "protocol.cs:1690-1698's buffers) on this host: 1 thread and the cores the process may "
+                         "use (quota-capped, bench.py's rule), median of 5 runs, this many seconds in all")
     ap.add_argument("--probe", type=int, default=0, help="then run the read probe N times over the arena "
                                                               "(FETCH_SIZE calibration)")
     a = ap.parse_args()
@@ -89,6 +134,8 @@ def main():
         res[name + "_bit_exact"] = ok
         if a.ablate:
             ctx.diag_ablation(0)
+    if a.cpu_seconds > 0:
+        res["cpu_baseline"] = cpu_gather(orc.OracleLib(), g, a.cpu_seconds)
     if a.probe:
         sink = torch.zeros(4, dtype=torch.int32, device="cuda")
         for _ in range(a.probe):

@@ -11,4 +11,5 @@ for j in 0 1 2 3 5 7 8; do
   tools/gpu_step.sh 200 $out/gather_j$j.log rocprofv3 --kernel-trace --stats -d $out/prof_j$j -o run -- python3 -u tools/gather_bench.py --only gather_binned --reps 20 --ablate $((j * 1048576)) || exit 1
 done
 tools/gpu_step.sh 200 $out/gather_dyn.log python3 -u tools/gather_bench.py --only gather_binned --reps 20 --ablate 524288 || exit 1
+tools/gpu_step.sh 300 $out/gather_cpu.log python3 -u tools/gather_bench.py --only gather_binned --reps 20 --cpu-seconds 20 || exit 1
 echo done > $out/done
