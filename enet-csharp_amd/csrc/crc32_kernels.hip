@@ -862,18 +862,22 @@ __global__ void __launch_bounds__(kThreads) crc32_gather_kernel(GatherArgs ga, K
 constexpr int kSmallDwords = (3 + static_cast<int>(kGatherSmall) + 3) / 4;
 static_assert(15 + kGatherSmall <= 16 * ((kSmallDwords + 1 + 3) / 4), "a short segment's aligned lines fit the join's loads");
 
+
 // p[i] as a GLOBAL load (a generic pointer makes hipcc emit a flat load)
 template <class T>
 __device__ __forceinline__ T gload(const T* p, uint64_t i) {
     return *reinterpret_cast<__attribute__((address_space(1))) const T*>(reinterpret_cast<uintptr_t>(p + i));
 }
 
+template <bool GLOBAL = true>
 __device__ __forceinline__ void load_small(const uint8_t* a, uint32_t L, uint32_t (&d)[kSmallDwords + 1]) {
     const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a)) & 3u;
     const uint32_t* w = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(a) & ~static_cast<uintptr_t>(3));
     const uint32_t nd = (sh + L + 3u) >> 2;
+    // GLOBAL: global loads (through a generic pointer hipcc emits flat loads, counted
+    // in lgkmcnt too: round 3's form, GLOBAL = false)
 #pragma unroll
-    for (int k = 0; k < kSmallDwords; ++k) d[k] = static_cast<uint32_t>(k) < nd ? w[k] : 0u;
+    for (int k = 0; k < kSmallDwords; ++k) d[k] = static_cast<uint32_t>(k) < nd ? (GLOBAL ? gload(w, k) : w[k]) : 0u;
     d[kSmallDwords] = 0u;
 }
 
@@ -896,91 +900,52 @@ __device__ __forceinline__ uint32_t fold_small(uint32_t reg, uint32_t sh, uint32
 
 // JV (diagnostics, wrong CRCs by design): bit 0 = no short-segment fold (its dwords
 // XORed in), bit 1 = no multiply (XOR), bit 2 = no short-segment loads
-// Global loads only (generic pointers made hipcc emit flat loads, which it waits for
-// with vmcnt(0) + lgkmcnt(0)), and no load under a branch: a load whose slot or
-// segment does not exist reads a valid stand-in address instead (the segment index
-// clamped into the DGRAM's range, the 256 zero bytes), so hipcc issues every load of
-// a chunk back to back and waits once.  (Round 3 form: per-dword flat loads under
-// branches, and seg_crc / x^(8 len) under branches each waited for at once -- 9.6 us
-// on cfg5 against 7.3 without the short-segment fold's loads and work.)
 template <int JV = 0>
 __global__ void __launch_bounds__(kThreads) crc32_gather_join_kernel(GatherArgs ga, const uint32_t* seg_crc,
                                                                      KernelTables tb, uint32_t small) {
     constexpr int kQ = 4;                                    // segments in flight per thread
-    constexpr int kC = (kSmallDwords + 1 + 3) / 4;           // 16-byte loads per short segment
     __shared__ uint32_t t4[4][256];
-    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
-    uint64_t d = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x;
-    // segFirst lives in device memory, so the host cannot check segFirst[n] ==
-    // segCount: clamp to the segments the binned pass filled (a short segCount then
-    // gives wrong CRCs for the DGRAMs past it, never a read past seg_crc).  The first
-    // DGRAM's bounds are loaded before the table fill's barrier.
-    auto bounds = [&](uint64_t dd, uint32_t& s0, uint32_t& s1) __attribute__((always_inline)) {
-        const uint64_t dc = min<uint64_t>(dd, ga.n - 1u);
-        const uint32_t a = gload(ga.seg_first, dc);
-        const uint32_t b = gload(ga.seg_first, dc + 1u);
-        s1 = static_cast<uint32_t>(min<uint64_t>(b, ga.segs));
-        s0 = min(a, s1);
-    };
-    uint32_t s0, s1;
-    bounds(d, s0, s1);
     if (small) {
         for (uint32_t i = threadIdx.x; i < 1024u; i += kThreads) t4[i >> 8][i & 255u] = tb.image[64u * (i & 255u) + 2u * (i >> 8)];
         __syncthreads();
     }
-    const uint64_t zero = reinterpret_cast<uint64_t>(tb.zero);
-    for (; d < ga.n; d += stride) {
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
+    for (uint64_t d = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; d < ga.n; d += stride) {
+        // segFirst lives in device memory, so the host cannot check segFirst[n] ==
+        // segCount: clamp to the segments the binned pass filled (a short segCount
+        // then gives wrong CRCs for the DGRAMs past it, never a read past seg_crc)
+        const uint32_t s1 = static_cast<uint32_t>(min<uint64_t>(ga.seg_first[d + 1], ga.segs));
+        const uint32_t s0 = min(ga.seg_first[d], s1);
         uint32_t reg = 0xFFFFFFFFu;
         for (uint32_t q0 = s0; q0 < s1; q0 += kQ) {
             uint32_t L[kQ];
-            uint64_t A[kQ];
+            const uint8_t* A[kQ];
 #pragma unroll
             for (int i = 0; i < kQ; ++i) {
-                const uint32_t q = min(q0 + i, s1 - 1u);     // (s1 > q0: a valid segment)
-                const uint32_t l = gload(ga.seg_len, q);
-                A[i] = reinterpret_cast<uint64_t>(ga.bytes) + gload(ga.seg_off, q);
-                L[i] = q0 + i < s1 ? l : 0u;
+                const bool in = q0 + i < s1;
+                L[i] = in ? ga.seg_len[q0 + i] : 0u;
+                A[i] = ga.bytes + (in ? ga.seg_off[q0 + i] : 0u);
             }
-            uint32_t D[kQ][4 * kC], C[kQ], X[kQ];
+            uint32_t D[kQ][kSmallDwords + 1], C[kQ], X[kQ];
 #pragma unroll
             for (int i = 0; i < kQ; ++i) {
                 const bool sm = L[i] != 0u && L[i] <= small && !(JV & 4);
-                const uint64_t w = A[i] & ~static_cast<uint64_t>(15);
-                const uint32_t e = (static_cast<uint32_t>(A[i]) & 15u) + L[i];   // the segment's end in the lines
+                if (sm) load_small(A[i], L[i], D[i]);   // (global loads: see load_small)
+                else
 #pragma unroll
-                for (int c = 0; c < kC; ++c) {
-                    // 16-byte aligned loads that hold a byte of the segment (so never a page
-                    // the segment does not touch); the others, or not a short segment: zeros
-                    const u32x4 v = ldg16_addr((sm && 16u * c < e) ? w + 16u * c : zero);
-                    D[i][4 * c] = v.x;
-                    D[i][4 * c + 1] = v.y;
-                    D[i][4 * c + 2] = v.z;
-                    D[i][4 * c + 3] = v.w;
-                }
-                const bool lg = L[i] > small;
-                C[i] = gload(seg_crc, lg ? min(q0 + i, s1 - 1u) : 0u);
-                X[i] = gload(tb.xn_lo, L[i] & 0xFFFFu);
+                    for (int k = 0; k <= kSmallDwords; ++k) D[i][k] = 0u;
+                C[i] = L[i] > small ? seg_crc[q0 + i] : 0u;
+                X[i] = L[i] > small ? tb.xn_lo[L[i] & 0xFFFFu] : 0u;
             }
 #pragma unroll
             for (int i = 0; i < kQ; ++i) {
                 if (L[i] == 0u) continue;
                 if (L[i] <= small) {
-                    // dwords past the segment's hold bytes of neighbours: fold_small reads only
-                    // the segment's (nf whole dwords, then L mod 4 bytes of the next)
-                    // from the segment's first dword on: o = (A >> 2) & 3 dwords dropped, by
-                    // two selects per dword (fold_small reads d[0 .. kSmallDwords - 1])
-                    const uint32_t o = (static_cast<uint32_t>(A[i]) >> 2) & 3u;
-                    uint32_t E[4 * kC], Dd[kSmallDwords + 1];
-#pragma unroll
-                    for (int k = 0; k < 4 * kC; ++k) E[k] = (o & 1u) ? (k + 1 < 4 * kC ? D[i][k + 1] : 0u) : D[i][k];
-#pragma unroll
-                    for (int k = 0; k < kSmallDwords; ++k) Dd[k] = (o & 2u) ? (k + 2 < 4 * kC ? E[k + 2] : 0u) : E[k];
-                    Dd[kSmallDwords] = 0u;
                     if constexpr (JV & 1) {
 #pragma unroll
-                        for (int k = 0; k <= kSmallDwords; ++k) reg ^= Dd[k];
+                        for (int k = 0; k <= kSmallDwords; ++k) reg ^= D[i][k];
                     } else {
-                        reg = fold_small(reg, static_cast<uint32_t>(A[i]) & 3u, L[i], Dd, t4);
+                        reg = fold_small(reg, static_cast<uint32_t>(reinterpret_cast<uintptr_t>(A[i])) & 3u, L[i], D[i], t4);
                     }
                 } else if constexpr (JV & 2) {
                     reg ^= X[i] ^ ~bswap32(C[i]);
@@ -990,10 +955,64 @@ __global__ void __launch_bounds__(kThreads) crc32_gather_join_kernel(GatherArgs 
                 }
             }
         }
-        *reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(reinterpret_cast<uintptr_t>(ga.out + d)) = finalize(reg);
-        bounds(d + stride, s0, s1);
+        ga.out[d] = finalize(reg);
     }
 }
+
+#ifdef ENET_HIP_DIAG
+// Round 3's join, flat loads (diagnostics A/B, enet_hip_diag_ablation 8 x 1048576).
+__global__ void __launch_bounds__(kThreads) crc32_gather_join_r3_kernel(GatherArgs ga, const uint32_t* seg_crc,
+                                                                     KernelTables tb, uint32_t small) {
+    constexpr int kQ = 4;                                    // segments in flight per thread
+    __shared__ uint32_t t4[4][256];
+    if (small) {
+        for (uint32_t i = threadIdx.x; i < 1024u; i += kThreads) t4[i >> 8][i & 255u] = tb.image[64u * (i & 255u) + 2u * (i >> 8)];
+        __syncthreads();
+    }
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
+    for (uint64_t d = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; d < ga.n; d += stride) {
+        // segFirst lives in device memory, so the host cannot check segFirst[n] ==
+        // segCount: clamp to the segments the binned pass filled (a short segCount
+        // then gives wrong CRCs for the DGRAMs past it, never a read past seg_crc)
+        const uint32_t s1 = static_cast<uint32_t>(min<uint64_t>(ga.seg_first[d + 1], ga.segs));
+        const uint32_t s0 = min(ga.seg_first[d], s1);
+        uint32_t reg = 0xFFFFFFFFu;
+        for (uint32_t q0 = s0; q0 < s1; q0 += kQ) {
+            uint32_t L[kQ];
+            const uint8_t* A[kQ];
+#pragma unroll
+            for (int i = 0; i < kQ; ++i) {
+                const bool in = q0 + i < s1;
+                L[i] = in ? ga.seg_len[q0 + i] : 0u;
+                A[i] = ga.bytes + (in ? ga.seg_off[q0 + i] : 0u);
+            }
+            uint32_t D[kQ][kSmallDwords + 1], C[kQ], X[kQ];
+#pragma unroll
+            for (int i = 0; i < kQ; ++i) {
+                const bool sm = L[i] != 0u && L[i] <= small;
+                if (sm) load_small<false>(A[i], L[i], D[i]);
+                else
+#pragma unroll
+                    for (int k = 0; k <= kSmallDwords; ++k) D[i][k] = 0u;
+                C[i] = L[i] > small ? seg_crc[q0 + i] : 0u;
+                X[i] = L[i] > small ? tb.xn_lo[L[i] & 0xFFFFu] : 0u;
+            }
+#pragma unroll
+            for (int i = 0; i < kQ; ++i) {
+                if (L[i] == 0u) continue;
+                if (L[i] <= small) {
+                    reg = fold_small(reg, static_cast<uint32_t>(reinterpret_cast<uintptr_t>(A[i])) & 3u, L[i], D[i], t4);
+                } else {
+                    const uint32_t x = (L[i] >> 16) ? mulmod(X[i], tb.xn_hi[L[i] >> 16]) : X[i];
+                    reg = (reg == 0xFFFFFFFFu ? 0u : mulmod(reg ^ 0xFFFFFFFFu, x)) ^ ~bswap32(C[i]);
+                }
+            }
+        }
+        ga.out[d] = finalize(reg);
+    }
+}
+
+#endif  // ENET_HIP_DIAG
 
 // Read-roofline probe: every byte loaded once by 16-byte coalesced loads,
 // 4 loads in flight per lane, XOR-folded so nothing is dead code.
@@ -1556,8 +1575,8 @@ int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgro
 
 #ifdef ENET_HIP_DIAG
 int enet_hip_diag_ablation(enet_hip_context* ctx, int mode) {
-    if (!ctx || mode < 0 || mode >= (1 << 23)) return -static_cast<int>(hipErrorInvalidValue);
-    ctx->join_abl = (mode >> 20) & 7;                        // 1048576 x (1..7): gather-join ablations
+    if (!ctx || mode < 0 || mode >= (1 << 24)) return -static_cast<int>(hipErrorInvalidValue);
+    ctx->join_abl = (mode >> 20) & 15;                       // 1048576 x (1..7): gather-join ablations, x 8: round 3's join
     ctx->vr_dynamic = (mode >> 19) & 1;                      // 524288: vring dynamic rounds
     const int prio = (mode & 1024) ? 2 : (mode >> 3) & 1;    // 8: static / 1024: progress priority
     ctx->vr_abl = (mode >> 11) & 255;                        // 2048 ... 262144: vring ablations / end records
@@ -1863,6 +1882,7 @@ int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* by
         case 3: hipLaunchKernelGGL(crc32_gather_join_kernel<3>, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx), small); break;
         case 5: hipLaunchKernelGGL(crc32_gather_join_kernel<5>, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx), small); break;
         case 7: hipLaunchKernelGGL(crc32_gather_join_kernel<7>, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx), small); break;
+        case 8: hipLaunchKernelGGL(crc32_gather_join_r3_kernel, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx), small); break;
         default: hipLaunchKernelGGL(crc32_gather_join_kernel<0>, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx), small);
     }
 #else

@@ -458,8 +458,12 @@ __device__ __forceinline__ uint32_t vr_lookups(const uint32_t (&d)[8], const VrS
 // atomics.  (Round 4's first form counted the waves ending on one word to reset it:
 // 8192 returning atomics on one address at the launch's end, serialised at the
 // chip's ~88 per us, added 40-90 us.)  A newer generation (not possible while the
-// host hands out the lines in turn) gives ~0: chunks past the end.
-__device__ __forceinline__ uint32_t vr_claim_next() {
+// host hands out the lines in turn) gives ~0: chunks past the end.  dyn = the
+// launch's dynamic chunks: none (a launch the static rounds cover) gives ~0 with no
+// atomic.  (A plain agent-scope load of the word first, to skip the claims past the
+// last chunk, made cfg2 lists 1.6x slower.)
+__device__ __forceinline__ uint32_t vr_claim_next(uint32_t dyn) {
+    if (dyn == 0u) return ~0u;
     uint32_t c = 0;
     if ((threadIdx.x & 63u) == 0u) {
         uint32_t t;
@@ -682,7 +686,9 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
         if (kDyn && sl >= (kStatic - 1u) * kVrW && (sl & (kVrW - 1u)) == 0u) {
             const uint32_t r = sl / kVrW;
             if (r >= kStatic) (void)vr_round_chunk(r);
-            const uint32_t c = vr_claim_next();
+            // (the launch's dynamic chunks: its chunks past the kStatic G static ones)
+            const uint64_t chunks = (ngroups_all + kVrW - 1u) >> 4, stat = (wt >> 4) * kStatic;
+            const uint32_t c = vr_claim_next(chunks > stat ? static_cast<uint32_t>(min<uint64_t>(chunks - stat, ~0u - 1u)) : 0u);
             vr_round_publish(r + 1u, c == ~0u ? c : static_cast<uint32_t>(wt / kVrW) * kStatic + c);   // kStatic G + c
         }
         return sl;
