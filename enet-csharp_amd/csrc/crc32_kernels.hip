@@ -869,15 +869,14 @@ __device__ __forceinline__ T gload(const T* p, uint64_t i) {
     return *reinterpret_cast<__attribute__((address_space(1))) const T*>(reinterpret_cast<uintptr_t>(p + i));
 }
 
-template <bool GLOBAL = true>
 __device__ __forceinline__ void load_small(const uint8_t* a, uint32_t L, uint32_t (&d)[kSmallDwords + 1]) {
     const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a)) & 3u;
     const uint32_t* w = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(a) & ~static_cast<uintptr_t>(3));
     const uint32_t nd = (sh + L + 3u) >> 2;
-    // GLOBAL: global loads (through a generic pointer hipcc emits flat loads, counted
-    // in lgkmcnt too: round 3's form, GLOBAL = false)
+    // global loads (through a generic pointer hipcc emits flat loads, counted in lgkmcnt
+    // too: round 3's form, within noise of this one -- DESIGN.md 4.4)
 #pragma unroll
-    for (int k = 0; k < kSmallDwords; ++k) d[k] = static_cast<uint32_t>(k) < nd ? (GLOBAL ? gload(w, k) : w[k]) : 0u;
+    for (int k = 0; k < kSmallDwords; ++k) d[k] = static_cast<uint32_t>(k) < nd ? gload(w, k) : 0u;
     d[kSmallDwords] = 0u;
 }
 
@@ -959,60 +958,6 @@ __global__ void __launch_bounds__(kThreads) crc32_gather_join_kernel(GatherArgs 
     }
 }
 
-#ifdef ENET_HIP_DIAG
-// Round 3's join, flat loads (diagnostics A/B, enet_hip_diag_ablation 8 x 1048576).
-__global__ void __launch_bounds__(kThreads) crc32_gather_join_r3_kernel(GatherArgs ga, const uint32_t* seg_crc,
-                                                                     KernelTables tb, uint32_t small) {
-    constexpr int kQ = 4;                                    // segments in flight per thread
-    __shared__ uint32_t t4[4][256];
-    if (small) {
-        for (uint32_t i = threadIdx.x; i < 1024u; i += kThreads) t4[i >> 8][i & 255u] = tb.image[64u * (i & 255u) + 2u * (i >> 8)];
-        __syncthreads();
-    }
-    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
-    for (uint64_t d = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; d < ga.n; d += stride) {
-        // segFirst lives in device memory, so the host cannot check segFirst[n] ==
-        // segCount: clamp to the segments the binned pass filled (a short segCount
-        // then gives wrong CRCs for the DGRAMs past it, never a read past seg_crc)
-        const uint32_t s1 = static_cast<uint32_t>(min<uint64_t>(ga.seg_first[d + 1], ga.segs));
-        const uint32_t s0 = min(ga.seg_first[d], s1);
-        uint32_t reg = 0xFFFFFFFFu;
-        for (uint32_t q0 = s0; q0 < s1; q0 += kQ) {
-            uint32_t L[kQ];
-            const uint8_t* A[kQ];
-#pragma unroll
-            for (int i = 0; i < kQ; ++i) {
-                const bool in = q0 + i < s1;
-                L[i] = in ? ga.seg_len[q0 + i] : 0u;
-                A[i] = ga.bytes + (in ? ga.seg_off[q0 + i] : 0u);
-            }
-            uint32_t D[kQ][kSmallDwords + 1], C[kQ], X[kQ];
-#pragma unroll
-            for (int i = 0; i < kQ; ++i) {
-                const bool sm = L[i] != 0u && L[i] <= small;
-                if (sm) load_small<false>(A[i], L[i], D[i]);
-                else
-#pragma unroll
-                    for (int k = 0; k <= kSmallDwords; ++k) D[i][k] = 0u;
-                C[i] = L[i] > small ? seg_crc[q0 + i] : 0u;
-                X[i] = L[i] > small ? tb.xn_lo[L[i] & 0xFFFFu] : 0u;
-            }
-#pragma unroll
-            for (int i = 0; i < kQ; ++i) {
-                if (L[i] == 0u) continue;
-                if (L[i] <= small) {
-                    reg = fold_small(reg, static_cast<uint32_t>(reinterpret_cast<uintptr_t>(A[i])) & 3u, L[i], D[i], t4);
-                } else {
-                    const uint32_t x = (L[i] >> 16) ? mulmod(X[i], tb.xn_hi[L[i] >> 16]) : X[i];
-                    reg = (reg == 0xFFFFFFFFu ? 0u : mulmod(reg ^ 0xFFFFFFFFu, x)) ^ ~bswap32(C[i]);
-                }
-            }
-        }
-        ga.out[d] = finalize(reg);
-    }
-}
-
-#endif  // ENET_HIP_DIAG
 
 // Read-roofline probe: every byte loaded once by 16-byte coalesced loads,
 // 4 loads in flight per lane, XOR-folded so nothing is dead code.
@@ -1575,8 +1520,8 @@ int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgro
 
 #ifdef ENET_HIP_DIAG
 int enet_hip_diag_ablation(enet_hip_context* ctx, int mode) {
-    if (!ctx || mode < 0 || mode >= (1 << 24)) return -static_cast<int>(hipErrorInvalidValue);
-    ctx->join_abl = (mode >> 20) & 15;                       // 1048576 x (1..7): gather-join ablations, x 8: round 3's join
+    if (!ctx || mode < 0 || mode >= (1 << 23)) return -static_cast<int>(hipErrorInvalidValue);
+    ctx->join_abl = (mode >> 20) & 7;                        // 1048576 x (1..7): gather-join ablations
     ctx->vr_dynamic = (mode >> 19) & 1;                      // 524288: vring dynamic rounds
     const int prio = (mode & 1024) ? 2 : (mode >> 3) & 1;    // 8: static / 1024: progress priority
     ctx->vr_abl = (mode >> 11) & 255;                        // 2048 ... 262144: vring ablations / end records
@@ -1882,7 +1827,6 @@ int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* by
         case 3: hipLaunchKernelGGL(crc32_gather_join_kernel<3>, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx), small); break;
         case 5: hipLaunchKernelGGL(crc32_gather_join_kernel<5>, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx), small); break;
         case 7: hipLaunchKernelGGL(crc32_gather_join_kernel<7>, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx), small); break;
-        case 8: hipLaunchKernelGGL(crc32_gather_join_r3_kernel, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx), small); break;
         default: hipLaunchKernelGGL(crc32_gather_join_kernel<0>, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx), small);
     }
 #else

@@ -391,7 +391,14 @@ ENET_HIP_API int enet_hip_read_probe_device(enet_hip_context* ctx, const uint8_t
  * 2048 + 4096 + 32768 (4 lanes): no masks, lookups or end-of-packet
  * corrections (WRONG checksums: the kernel's memory and control skeleton);
  * 65536 (4 lanes, correct checksums): the stage loads with the sc1 (path 17)
- * or sc0 sc1 (path 18) cache policy. */
+ * or sc0 sc1 (path 18) cache policy; 262144: the vring's end-record trace
+ * instance (with enet_hip_diag_trace).  Also on the linear-stream paths 22 / 23:
+ * 2048 = no boundary passes, 2048 + 4096 = no fold lookups either (WRONG
+ * checksums).  524288 (correct checksums): the vring's dynamic rounds (rounds
+ * past the third claimed chip-wide from a per-launch claim line) instead of the
+ * static deal.  1048576 x j, j = 1..7: the gather join without its short-segment
+ * fold (bit 0 of j), its multiplies (bit 1), its short-segment loads (bit 2) --
+ * WRONG checksums. */
 ENET_HIP_API int enet_hip_diag_ablation(enet_hip_context* ctx, int mode);
 
 /* ---- diagnostics: per-wave timeline of the lean stream kernel ----
