@@ -26,7 +26,8 @@ from typing import Sequence
 import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "libenethip.so")
+# ENET_HIP_LIBRARY: another build of the product library (measurement A/B only)
+LIB_PATH = os.environ.get("ENET_HIP_LIBRARY") or os.path.join(PKG_ROOT, "libenethip.so")
 DIAG_LIB_PATH = os.path.join(PKG_ROOT, "libenethip_diag.so")
 
 # Every symbol include/enet_hip.h declares (tests check the .so exports them all).

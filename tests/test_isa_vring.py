@@ -88,3 +88,33 @@ def test_ring_write_check_asm_writes():
     assert chk.check(load + ["s_waitcnt vmcnt(0)"] + mask + ["s_endpgm"], "k") == []
     errs = chk.check(load + mask + ["s_waitcnt vmcnt(0)", "s_endpgm"], "k")
     assert any("may be in flight" in e for e in errs)
+
+
+def test_inflight_check_follows_structurizer_flags():
+    """hipcc's structurizer may lay an if / else out as two conditional blocks joined by
+    a flag pair.  Both arms issue a stage and wait for the previous one; the checker
+    must not report the infeasible path that skips both arms -- but must still report
+    a real miss (an arm that forgets its wait, or a flag it cannot know)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import isa_inflight_check as chk
+
+    def kernel(meta_wait="s_waitcnt vmcnt(2)", else_flag="s_mov_b64 s[10:11], -1"):
+        return [";;#ASMSTART", "global_load_dwordx4 v[48:51], v[0:1], off", ";;#ASMEND",
+                else_flag,
+                "s_cbranch_scc1 .LBB0_2",                    # -> the else arm
+                "s_mov_b64 s[10:11], 0",                     # the if arm
+                ";;#ASMSTART", "global_load_lds_dword v[2:3], off", ";;#ASMEND",
+                ";;#ASMSTART", "global_load_dwordx4 v[56:59], v[4:5], off", ";;#ASMEND",
+                ";;#ASMSTART", meta_wait, ";;#ASMEND",
+                ".LBB0_2:",
+                "s_andn2_b64 vcc, exec, s[10:11]",
+                "s_cbranch_vccnz .LBB0_3",
+                ";;#ASMSTART", "global_load_dwordx4 v[56:59], v[4:5], off", ";;#ASMEND",   # the else arm
+                ";;#ASMSTART", "s_waitcnt vmcnt(1)", ";;#ASMEND",
+                ".LBB0_3:",
+                "v_xor_b32_e32 v1, v48, v2",                 # the fold of the first stage
+                "s_waitcnt vmcnt(0)",
+                "s_endpgm"]
+    assert chk.check(kernel(), "k") == []
+    assert any("may be in flight" in e for e in chk.check(kernel(meta_wait="s_waitcnt vmcnt(3)"), "k"))
+    assert any("may be in flight" in e for e in chk.check(kernel(else_flag="s_mov_b64 s[12:13], -1"), "k"))

@@ -16,6 +16,13 @@ aligned at their youngest end (element-wise union), which over-approximates what
 may be in flight on any path.  Any instruction that names a register of an
 in-flight asm load (other than the waits that tie them) is reported.
 
+hipcc's CFG structurizer can turn an if / else into two conditional blocks joined by a
+flag (`s_mov_b64 s[a:b], 0 / -1` in the arms, then `s_andn2_b64 vcc, exec, s[a:b]` +
+`s_cbranch_vccnz` before the second block).  Path-insensitive, the analysis would also
+follow the infeasible path that skips both arms; so it carries the SGPR pairs known to
+hold 0 or -1 (and vcc's zero-ness derived from them) along every path into a point,
+and follows only the feasible edge of a vcc branch they decide.
+
     python tools/isa_inflight_check.py path/to/kernel.s
 """
 import re
@@ -122,6 +129,54 @@ def step(state, inst):
     return state
 
 
+SPAIR = re.compile(r"^s\[(\d+):(\d+)\]$")
+
+
+def consts_step(consts, inst):
+    """The known flag constants after an instruction: {'s[a:b]': 0 | -1, 'vcc': 'z' | 'nz'}."""
+    kind, line, op, _, _, _ = inst
+    ops = [x.strip() for x in line[len(op):].split(",")] if line[len(op):].strip() else []
+    dst = ops[0] if ops else ""
+    c = dict(consts)
+    if op == "s_mov_b64" and SPAIR.match(dst) and len(ops) == 2 and ops[1] in ("0", "-1"):
+        c[dst] = int(ops[1])
+        return frozenset(c.items())
+    if op in ("s_andn2_b64", "s_and_b64") and dst == "vcc" and len(ops) == 3 and ops[1] == "exec" and ops[2] in c \
+            and isinstance(c[ops[2]], int):
+        v = c[ops[2]]
+        # (exec is non-zero wherever this kernel branches on vcc)
+        nz = (v == 0) if op == "s_andn2_b64" else (v == -1)
+        c["vcc"] = "nz" if nz else "z"
+        return frozenset(c.items())
+    # anything else that may write a tracked register forgets it
+    written = set()
+    if dst:
+        written.add(dst)
+    if op.startswith(("v_cmp", "v_cmpx")) and op.endswith("_e32"):
+        written.add("vcc")
+    if op.startswith("v_"):
+        # a VALU op may also write an SGPR pair or vcc past its first operand (carry-outs
+        # of v_add_co / v_sub_co / v_mad_u64, ...): forget every one it names
+        for x in ops[1:]:
+            if x == "vcc" or SPAIR.match(x) or re.match(r"^s\d+$", x):
+                written.add(x)
+    if "vcc" in dst:
+        written.add("vcc")
+    if written:
+        def clash(key):
+            if key == "vcc":
+                return "vcc" in written
+            a, b = map(int, SPAIR.match(key).groups())
+            for w in written:
+                m = SPAIR.match(w)
+                lo, hi = (int(m.group(1)), int(m.group(2))) if m else ((int(w[1:]),) * 2 if re.match(r"^s\d+$", w) else (-1, -1))
+                if lo <= b and a <= hi:
+                    return True
+            return False
+        c = {k: v for k, v in c.items() if not clash(k)}
+    return frozenset(c.items())
+
+
 def check(lines, name):
     insts, labels = parse(lines)
     n = len(insts)
@@ -137,17 +192,49 @@ def check(lines, name):
         if kind not in ("end",) and op not in ("s_branch", "s_cbranch_execnz") and i + 1 < n:
             s.append(i + 1)
         succ.append(s)
-    state_in = [None] * n
-    state_in[0] = ()
+    # per point: {known flag constants: in-flight list} -- one entry per set of constants
+    # (a disjunction over paths, so an if / else's two arms stay apart), collapsed to one
+    # entry if more than MAXK sets reach a point
+    MAXK = 32
+    sets = [None] * n
+    sets[0] = {frozenset(): ()}
     work = [0]
     while work:
         i = work.pop()
-        out = step(state_in[i], insts[i])
-        for j in succ[i]:
-            m = merge(state_in[j], out)
-            if m != state_in[j]:
-                state_in[j] = m
+        kind, line, op, target, _, _ = insts[i]
+        adds = {}
+        for cin, st in sets[i].items():
+            out = step(st, insts[i])
+            cout = consts_step(cin, insts[i])
+            targets = succ[i]
+            known = dict(cin).get("vcc")
+            if op in ("s_cbranch_vccnz", "s_cbranch_vccz") and known is not None and target in labels:
+                taken = (known == "nz") == (op == "s_cbranch_vccnz")
+                targets = [labels[target]] if taken else [j for j in succ[i] if j == i + 1]
+            for j in targets:
+                adds.setdefault(j, []).append((cout, out))
+        for j, items in adds.items():
+            cur = dict(sets[j]) if sets[j] is not None else {}
+            for cout, out in items:
+                cur[cout] = merge(cur.get(cout), out)
+            if len(cur) > MAXK:
+                meet = frozenset.intersection(*cur.keys())
+                acc = None
+                for v in cur.values():
+                    acc = merge(acc, v)
+                cur = {meet: acc}
+            if sets[j] is None or cur != sets[j]:
+                sets[j] = cur
                 work.append(j)
+    state_in = []
+    for d in sets:
+        if d is None:
+            state_in.append(None)
+            continue
+        acc = None
+        for v in d.values():
+            acc = merge(acc, v)
+        state_in.append(acc)
     errors = []
     # the ring registers v48-v63 are written only by inline asm (the stage loads and
     # the edge path's in-place masking of a landed slot): a compiler instruction
