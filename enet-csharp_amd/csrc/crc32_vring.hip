@@ -599,10 +599,8 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     const uint64_t wv = static_cast<uint64_t>(blockIdx.x) * kVrW + wave;
     const uint64_t wt = static_cast<uint64_t>(gridDim.x) * kVrW;
     constexpr bool kDyn = DYN != 0 && !WK;
-    // slots taken statically per wave: rounds 0 .. kStatic - 1 (DYN: chunks k + r G);
-    // the static deal takes only the first statically, every later one from the
-    // workgroup's counter, late in the wave's current group (below)
-    constexpr uint32_t kStatic = kDyn ? 3u : 1u;
+    // slots taken statically per wave: rounds 0 .. kStatic - 1 are chunks k + r G
+    constexpr uint32_t kStatic = kDyn ? 3u : 2u;
     if constexpr (kDyn) {                                    // wave 0, before its takes: no round published
         if (threadIdx.x < static_cast<uint32_t>(kVrRounds)) lds_store(kVrRound + 8u * threadIdx.x, ~0u);
         // the claim word's address and generation (read where used: held across the
@@ -612,11 +610,6 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
                       threadIdx.x < 2u ? static_cast<uint32_t>(reinterpret_cast<uint64_t>(bl.claim) >> (32u * threadIdx.x))
                                        : bl.claim_gen);
     }
-    // the workgroup's slot counter (slots below kStatic kVrW are taken statically), and a
-    // raw barrier: a wave's first counter take may come in the prologue
-    if (threadIdx.x == 0u) lds_store(BIN ? kVrCtrBin : kVrCtr, kStatic * kVrW);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
     auto lane_k = [&]() __attribute__((always_inline)) { return lane & (P - 1u); };   // block lane
     auto lane_p = [&]() __attribute__((always_inline)) { return lane >> LG; };         // packet of the group
     const uint64_t zero = reinterpret_cast<uint64_t>(tb.zero);
@@ -706,14 +699,8 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     };
     VrIt pit{0u, 0u};                                        // the producer's group
     const bool any = advance(pit);
-    // The wave's next group is taken late in its current one: at stage pmeta = S - 2 of
-    // a group of S >= 3 stages (else at its first), so a wave that runs ahead takes the
-    // next slot sooner, and the slots of a workgroup go to its waves in the order they
-    // near the end of a group rather than one group ahead (round 3: at the current
-    // group's entry, the second slot static).  Two stages still cover the metadata's
-    // latency.  qtaken: this group's take is done.
     VrIt qit = pit;                                          // the group whose metadata is loaded
-    bool qlive = false, qtaken = !any;
+    bool qlive = any && advance(qit);
 
     // diagnostics (enet_hip_diag_trace): per-wave timestamps, tools/timeline.py's
     // 8 x u64 layout [start, metadata, table, barrier B, loop entry, end, HW_ID, groups]
@@ -811,7 +798,7 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
         if constexpr (kEA) return pwl & kEAMask;
         return pwl & ~static_cast<uint64_t>(kAln - 1u);
     };
-    uint32_t pst = 0, pstages = 0, pmeta = 0;
+    uint32_t pst = 0, pstages = 0;
     uint32_t pidx = 0;                                       // BIN: the first group's caller index (prologue)
     // BIN: the caller indices of the producer's group go to an LDS stash, two slots per
     // wave by group parity, over the basis staging area (free once barrier B is
@@ -852,10 +839,6 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
         }
         const uint32_t nb = (pe + 31u) >> 5;
         pstages = max(1u, wave_max_u((nb + P - 1u) >> LG));
-        // (readfirstlane: a wave-uniform value the compiler can see as one, so the stage
-        // issue below stays an if / else on a scalar branch -- the in-flight check
-        // follows both arms -- rather than two exec-masked blocks)
-        pmeta = __builtin_amdgcn_readfirstlane((!VF && pstages >= 3u) ? pstages - 2u : 0u);   // (verify: at the group's entry)
         pst = 0;
     };
     // A produce issues the stage's two pieces, preceded -- on a group's first stage,
@@ -874,8 +857,7 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
                 // once at most those two are in flight (stores do not count: older)
                 vr_wait_meta<2, BIN, VF, kPk>(mbase, lane_p(), mL, moff, midx, mso, mconn);
                 pit = qit;
-                qlive = false;
-                qtaken = false;
+                qlive = advance(qit);
                 producer_enter(std::true_type{});
             } else {
                 pdone = true;
@@ -892,11 +874,7 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
         const uint64_t ws = pws();
         const uint64_t s0 = (a0 < pe && a0 + 16u > lz) ? ws + a0 : zero;
         const uint64_t s1 = (a1 < pe && a1 + 16u > lz) ? ws + a1 : zero;
-        if (!qtaken && !pdone && pst == pmeta) {             // the next group's slot
-            qlive = advance(qit);
-            qtaken = true;
-        }
-        const bool meta = (pst == pmeta) & qlive & !pdone;  // (one branch, no short-circuit flow blocks)
+        const bool meta = (pst == 0u) & qlive & !pdone;     // (one branch, no short-circuit flow blocks)
         if (meta) {
             load_meta(qit);
             vr_issue_stage<slot, NT>(s0, s1);
@@ -916,8 +894,9 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     // writes rows w + 16 i: row j = XOR of basis rows b with bit b of j set (Gray
     // order: one XOR per row), except the INIT and CINV dwords (not linear in j),
     // whose rows < 64 come from basis rows 8 and 9.  Raw s_barrier: no vmcnt drain.
-    // (the slot counter is initialised at the kernel's start: a take may come in the
-    // prologue's first produce)
+    // the slot counter: slots 0 .. kStatic kVrW - 1 are taken statically; the first dynamic
+    // take comes after barrier B (a wave's second group is entered in the loop)
+    if (threadIdx.x == 0u) lds_store(BIN ? kVrCtrBin : kVrCtr, kStatic * kVrW);
     __builtin_amdgcn_s_barrier();                            // (A) every basis row has landed
     {
         uint32_t bb[8];
