@@ -35,6 +35,10 @@ struct enet_hip_context {
     uint32_t* d_rounds = nullptr;
     std::atomic<uint64_t> rounds_next{0};
     bool vr_dynamic = false;
+    // pair rounds (diagnostics A/B): a ring of kVrPairLines arrays of kVrPairWords words
+    uint64_t* d_pairs = nullptr;
+    std::atomic<uint64_t> pairs_next{0};
+    bool vr_pair = false;
     int join_abl = 0;            // diagnostics library: gather-join ablations
     // host-memory entry points (host_pipeline.hip): calls on one context serialize on mu
     std::mutex mu;

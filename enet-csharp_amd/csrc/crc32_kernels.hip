@@ -1304,7 +1304,17 @@ bool vring_path(const enet_hip_context* ctx) {
 // needs no reset of it (crc32_vring.hip vr_claim_next).  After 2^32 - 2 uses of a
 // line (2^40 launches) the context falls back to the static deal.
 constexpr uint32_t kVrClaimLines = 256;
+constexpr uint32_t kVrPairLines = 64;
 VrVariant with_claim(enet_hip_context* ctx, VrVariant v) {
+    if (!v.walk && ctx->vr_pair && ctx->d_pairs) {           // pair rounds (diagnostics)
+        const uint64_t seq = ctx->pairs_next.fetch_add(1u);
+        const uint64_t gen = seq / kVrPairLines + 1u;
+        if (gen >= 0xFFFFFFFFull) return v;
+        v.claim = ctx->d_pairs + static_cast<size_t>(kVrPairWords) * (seq % kVrPairLines);
+        v.claim_gen = static_cast<uint32_t>(gen);
+        v.claim_mode = 2;
+        return v;
+    }
     if (v.walk || !ctx->vr_dynamic || !ctx->d_rounds) return v;
     const uint64_t seq = ctx->rounds_next.fetch_add(1u);
     const uint64_t gen = seq / kVrClaimLines + 1u;
@@ -1464,6 +1474,11 @@ int enet_hip_context_create(int device, enet_hip_context** out) {
         const size_t claim_bytes = static_cast<size_t>(kVrClaimLines) * kVrClaimWords * 4;
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_rounds), claim_bytes)))) break;
         if ((rc = herr(hipMemset(ctx->d_rounds, 0, claim_bytes)))) break;
+#ifdef ENET_HIP_DIAG
+        const size_t pair_bytes = static_cast<size_t>(kVrPairLines) * kVrPairWords * 8;
+        if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_pairs), pair_bytes)))) break;
+        if ((rc = herr(hipMemset(ctx->d_pairs, 0, pair_bytes)))) break;
+#endif
         if ((rc = vring_setup())) break;
         if ((rc = lin_setup())) break;
         if ((rc = setup_stream())) break;
@@ -1499,6 +1514,7 @@ int enet_hip_context_destroy(enet_hip_context* ctx) {
     (void)hipFree(ctx->d_tz);
     (void)hipFree(ctx->d_lin);
     (void)hipFree(ctx->d_rounds);
+    (void)hipFree(ctx->d_pairs);
     pipeline_release(ctx);
     (void)hipFree(ctx->d_claim);
     (void)hipFree(ctx->d_frag_desc);
@@ -1520,7 +1536,8 @@ int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgro
 
 #ifdef ENET_HIP_DIAG
 int enet_hip_diag_ablation(enet_hip_context* ctx, int mode) {
-    if (!ctx || mode < 0 || mode >= (1 << 23)) return -static_cast<int>(hipErrorInvalidValue);
+    if (!ctx || mode < 0 || mode >= (1 << 24)) return -static_cast<int>(hipErrorInvalidValue);
+    ctx->vr_pair = (mode >> 23) & 1;                         // 8388608: vring pair rounds
     ctx->join_abl = (mode >> 20) & 7;                        // 1048576 x (1..7): gather-join ablations
     ctx->vr_dynamic = (mode >> 19) & 1;                      // 524288: vring dynamic rounds
     const int prio = (mode & 1024) ? 2 : (mode >> 3) & 1;    // 8: static / 1024: progress priority

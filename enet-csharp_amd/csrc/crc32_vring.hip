@@ -559,7 +559,11 @@ struct VrIt {
 // packet: the slot's lane substitutes connectID in registers (vr_slot_fix), and the
 // packet's lane 0 writes ok[] and computed[].
 // DYN = 1: dynamic rounds (above); built for the product-shaped instances (TR != 1,
-// no ablation, nt, walks or tail-first order)
+// no ablation, nt, walks or tail-first order).  DYN = 2 (diagnostics): pair rounds --
+// workgroups k and k + H (H = G / 2, G even) share the chunks p + j H (p = k mod H):
+// the same static rounds (k + r G = p + (2 r + k / H) H), then j = 2 kStatic + c from the
+// pair's own claim word, so the two balance against each other with no word shared
+// by more than two workgroups.
 template <int LG, int TR = 0, int NT = 0, int ABL = 0, int BIN = 0, int WK = 0, int ROT = 0, int VF = 0, int DYN = 0>
 __global__ void __launch_bounds__(64 * kVrW) __attribute__((amdgpu_waves_per_eu(8, 8), amdgpu_num_vgpr(24)))
 crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, KernelTables tb, const uint32_t* basis,
@@ -605,9 +609,11 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
         if (threadIdx.x < static_cast<uint32_t>(kVrRounds)) lds_store(kVrRound + 8u * threadIdx.x, ~0u);
         // the claim word's address and generation (read where used: held across the
         // ring loop they cost SGPRs)
+        // (DYN 2: the pair's word)
+        const uint64_t* word = bl.claim + (DYN == 2 ? blockIdx.x % (gridDim.x >> 1) : 0u);
         if (threadIdx.x < 3u)
             lds_store(kVrClaimPtr + 4u * threadIdx.x,
-                      threadIdx.x < 2u ? static_cast<uint32_t>(reinterpret_cast<uint64_t>(bl.claim) >> (32u * threadIdx.x))
+                      threadIdx.x < 2u ? static_cast<uint32_t>(reinterpret_cast<uint64_t>(word) >> (32u * threadIdx.x))
                                        : bl.claim_gen);
     }
     auto lane_k = [&]() __attribute__((always_inline)) { return lane & (P - 1u); };   // block lane
@@ -686,10 +692,19 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
         if (kDyn && sl >= (kStatic - 1u) * kVrW && (sl & (kVrW - 1u)) == 0u) {
             const uint32_t r = sl / kVrW;
             if (r >= kStatic) (void)vr_round_chunk(r);
-            // (the launch's dynamic chunks: its chunks past the kStatic G static ones)
-            const uint64_t chunks = (ngroups_all + kVrW - 1u) >> 4, stat = (wt >> 4) * kStatic;
-            const uint32_t c = vr_claim_next(chunks > stat ? static_cast<uint32_t>(min<uint64_t>(chunks - stat, ~0u - 1u)) : 0u);
-            vr_round_publish(r + 1u, c == ~0u ? c : static_cast<uint32_t>(wt / kVrW) * kStatic + c);   // kStatic G + c
+            const uint64_t chunks = (ngroups_all + kVrW - 1u) >> 4, G = wt >> 4;
+            if constexpr (DYN == 2) {
+                // the pair's dynamic chunks: p + j H for j >= 2 kStatic, below the launch's chunks
+                const uint64_t H = G >> 1, pp = blockIdx.x % H;
+                const uint64_t jn = chunks > pp ? (chunks - pp + H - 1u) / H : 0u;
+                const uint32_t c = vr_claim_next(jn > 2u * kStatic ? static_cast<uint32_t>(min<uint64_t>(jn - 2u * kStatic, ~0u - 1u)) : 0u);
+                vr_round_publish(r + 1u, c == ~0u ? c : static_cast<uint32_t>(min<uint64_t>(pp + (2u * kStatic + c) * H, ~0u - 1u)));
+            } else {
+                // (the launch's dynamic chunks: its chunks past the kStatic G static ones)
+                const uint64_t stat = G * kStatic;
+                const uint32_t c = vr_claim_next(chunks > stat ? static_cast<uint32_t>(min<uint64_t>(chunks - stat, ~0u - 1u)) : 0u);
+                vr_round_publish(r + 1u, c == ~0u ? c : static_cast<uint32_t>(G) * kStatic + c);   // kStatic G + c
+            }
         }
         return sl;
     };
@@ -1125,14 +1140,20 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
 
 // the instance; dyn = its dynamic-rounds twin where one is built
 template <int LG, int TR = 0, int NT = 0, int ABL = 0, int BIN = 0, int WK = 0, int ROT = 0, int VF = 0>
-const void* vring_fn(bool dyn = false) {
-    if constexpr (TR != 1 && NT == 0 && ABL == 0 && WK == 0 && ROT == 0)
-        if (dyn) return reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT, VF, 1>);
-    return reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT, VF>);
+const void* vring_fn(int dyn = 0) {
+    if constexpr (TR != 1 && NT == 0 && ABL == 0 && WK == 0 && ROT == 0) {
+        if (dyn == 1) return reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT, VF, 1>);
+#ifdef ENET_HIP_DIAG
+        if (dyn == 2) return reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT, VF, 2>);
+#endif
+    }
+    return dyn == 0 ? reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT, VF>) : nullptr;
 }
+// the dynamic-round mode a variant selects (0: the static deal)
+int vring_dyn(const VrVariant& v) { return v.claim ? v.claim_mode : 0; }
 // receive verify (8 lanes per packet): the product instance; diagnostics: tail first, end records
 const void* vring_pick_v(bool trace, const VrVariant& v) {
-    const bool dyn = v.claim != nullptr;
+    const int dyn = vring_dyn(v);
     if (!trace && !v.nt && !v.abl && !v.walk && !v.tail_first) return vring_fn<3, 0, 0, 0, 0, 0, 0, 1>(dyn);
 #ifdef ENET_HIP_DIAG
     if (!trace && !v.nt && !v.abl && !v.walk && v.tail_first) return vring_fn<3, 0, 0, 0, 0, 0, 1, 1>();
@@ -1140,7 +1161,7 @@ const void* vring_pick_v(bool trace, const VrVariant& v) {
 #endif
     return nullptr;
 }
-const void* vring_pick_bin(int lg, bool dyn) {
+const void* vring_pick_bin(int lg, int dyn) {
     return lg == 2 ? vring_fn<2, 0, 0, 0, 1>(dyn) : vring_fn<3, 0, 0, 0, 1>(dyn);
 }
 
@@ -1153,7 +1174,7 @@ const void* vring_pick_bin(int lg, bool dyn) {
 const void* vring_pick(int lg, bool trace, const VrVariant& v) {
     if (lg != 2 && lg != 3) return nullptr;
     const bool plain = !trace && !v.nt && !v.abl && !v.walk && !v.tail_first;
-    const bool dyn = v.claim != nullptr;
+    const int dyn = vring_dyn(v);
     if (plain) return lg == 2 ? vring_fn<2>(dyn) : vring_fn<3>(dyn);
 #ifdef ENET_HIP_DIAG
     const bool nt = v.nt;
@@ -1202,7 +1223,7 @@ int vring_setup() {
     };
     static const int kAbl[] = {0, 1, 2, 3, 4, 6, 8, 19, 27, 32, 128};
     static uint64_t any_line;                                // (a non-null claim selects the DYN twins)
-    for (int d = 0; d < 2; ++d) {
+    for (int d = 0; d < 3; ++d) {
         uint64_t* const claim = d ? &any_line : nullptr;
         for (int t = 0; t < 2; ++t)
             for (int w = 0; w < 2; ++w) {
@@ -1210,12 +1231,13 @@ int vring_setup() {
                 v.tail_first = w != 0;
                 v.abl = t ? 128 : 0;
                 v.claim = claim;
+                v.claim_mode = d;
                 const int rc = set(vring_pick_v(t != 0, v), kVrLds);
                 if (rc) return rc;
             }
         for (int lg = 2; lg <= 3; ++lg) {
             int rc;
-            if ((rc = set(vring_pick_bin(lg, d != 0), kVrLdsBin))) return rc;
+            if ((rc = set(vring_pick_bin(lg, d), kVrLdsBin))) return rc;
             for (int t = 0; t < 2; ++t)
                 for (int nt = 0; nt < 2; ++nt)
                     for (int abl : kAbl)
@@ -1226,6 +1248,7 @@ int vring_setup() {
                             v.walk = (w & 1) != 0;
                             v.tail_first = (w & 2) != 0;
                             v.claim = claim;
+                            v.claim_mode = d;
                             if ((rc = set(vring_pick(lg, t != 0, v), kVrLds))) return rc;
                         }
         }
@@ -1237,8 +1260,6 @@ int vring_launch_list(int lg, int max_wgs, const VrVariant& v, hipStream_t st, c
                       const KernelTables& tb, const uint32_t* basis2, uint64_t* trace, bool bin) {
     if ((lg != 2 && lg != 3) || bl.count > static_cast<uint32_t>(kVrMaxBatches))
         return -static_cast<int>(hipErrorInvalidValue);
-    const void* fn = bin ? vring_pick_bin(lg, v.claim != nullptr) : vring_pick(lg, trace != nullptr, v);
-    if (!fn) return -static_cast<int>(hipErrorInvalidValue);   // a variant this library does not build
     // empty batches dropped: the kernel may then read any batch's packet n - 1
     VrBatches a{};
     a.claim = v.claim;
@@ -1255,8 +1276,16 @@ int vring_launch_list(int lg, int max_wgs, const VrVariant& v, hipStream_t st, c
         a.b[b].g0 = a.groups;
         a.groups += (a.b[b].n + kpk - 1u) / kpk;
     }
-    const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(
+    unsigned grid = static_cast<unsigned>(std::max<uint64_t>(
         1, std::min<uint64_t>((a.groups + kVrW - 1) / kVrW, static_cast<uint64_t>(max_wgs))));
+    VrVariant w = v;
+    if (vring_dyn(w) == 2) {                                 // pairs: an even grid of at least 2
+        if (grid < 2 || grid / 2 > static_cast<unsigned>(kVrPairWords)) w.claim = a.claim = nullptr;
+        grid &= ~1u;
+        grid = std::max(grid, 1u);
+    }
+    const void* fn = bin ? vring_pick_bin(lg, vring_dyn(w)) : vring_pick(lg, trace != nullptr, w);
+    if (!fn) return -static_cast<int>(hipErrorInvalidValue);   // a variant this library does not build
     // slots are 32-bit: a workgroup's slot count (rounds x 16) must fit
     if ((a.groups / (static_cast<uint64_t>(grid) * kVrW) + 3u) * kVrW > 0xFFFFFFF0ull)
         return -static_cast<int>(hipErrorInvalidValue);
@@ -1268,8 +1297,6 @@ int vring_launch_list(int lg, int max_wgs, const VrVariant& v, hipStream_t st, c
 int vring_launch_vlist(int max_wgs, const VrVariant& v, hipStream_t st, const VrVBatches& bl, const KernelTables& tb,
                        const uint32_t* basis2, uint64_t* trace) {
     if (bl.count > static_cast<uint32_t>(kVrMaxVBatches)) return -static_cast<int>(hipErrorInvalidValue);
-    const void* fn = vring_pick_v(trace != nullptr, v);
-    if (!fn) return -static_cast<int>(hipErrorInvalidValue);
     VrVBatches a{};                                          // empty batches dropped
     a.claim = v.claim;
     a.claim_gen = v.claim_gen;
@@ -1280,8 +1307,16 @@ int vring_launch_vlist(int max_wgs, const VrVariant& v, hipStream_t st, const Vr
         a.b[b].g0 = a.groups;
         a.groups += (a.b[b].n + 7u) / 8u;
     }
-    const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(
+    unsigned grid = static_cast<unsigned>(std::max<uint64_t>(
         1, std::min<uint64_t>((a.groups + kVrW - 1) / kVrW, static_cast<uint64_t>(max_wgs))));
+    VrVariant w = v;
+    if (vring_dyn(w) == 2) {                                 // pairs: an even grid of at least 2
+        if (grid < 2 || grid / 2 > static_cast<unsigned>(kVrPairWords)) w.claim = a.claim = nullptr;
+        grid &= ~1u;
+        grid = std::max(grid, 1u);
+    }
+    const void* fn = vring_pick_v(trace != nullptr, w);
+    if (!fn) return -static_cast<int>(hipErrorInvalidValue);
     if ((a.groups / (static_cast<uint64_t>(grid) * kVrW) + 3u) * kVrW > 0xFFFFFFF0ull)
         return -static_cast<int>(hipErrorInvalidValue);
     void* args[] = {&a, const_cast<KernelTables*>(&tb), const_cast<const uint32_t**>(&basis2), &trace};

@@ -86,8 +86,13 @@ struct VrVariant {
     // the word has seen -- or null = the static deal
     uint64_t* claim = nullptr;
     uint32_t claim_gen = 0;
+    // 1: one claim word for the launch (chip-wide rounds); 2 (diagnostics library):
+    // claim points at an array of words, one per pair of workgroups k and k + G / 2
+    // (the pair's rounds balance between its two workgroups; G made even)
+    int claim_mode = 1;
 };
 constexpr int kVrClaimWords = 16;     // 32-bit words: one 64-byte line per launch
+constexpr int kVrPairWords = 512;     // pair rounds: 64-bit words per launch (grids up to 1024)
 
 // Set the dynamic-LDS attribute of every vring kernel instance built (once per context).
 int vring_setup();

@@ -711,7 +711,8 @@ def vring_dynamic_deal(batch_groups, grid: int, rng, W: int = 16):
     return seen, per_wave, total
 
 
-def vring_dynamic_rounds_deal(batch_groups, grid: int, rng, W: int = 16, K: int = 64, S: int = 3):
+def vring_dynamic_rounds_deal(batch_groups, grid: int, rng, W: int = 16, K: int = 64, S: int = 3,
+                              pairs: bool = False):
     """Simulate one launch of the vring kernel's dynamic rounds (crc32_vring.hip DYN:
     take / vr_claim_next / vr_round_publish / vr_round_chunk), all workgroups' waves
     interleaved at random: rounds r < S (S = 3 static takes) of workgroup k are chunks
@@ -722,13 +723,19 @@ def vring_dynamic_rounds_deal(batch_groups, grid: int, rng, W: int = 16, K: int 
     and a wave stops at its first group past the end.  Checks that no wave waits
     forever and that no round entry (K of them, r % K) is rewritten while a wave that
     took a slot of its round has not read it yet; returns {global group: (batch, local
-    group)}, the groups per wave and the launch's groups."""
+    group)}, the groups per wave and the launch's groups.  pairs (DYN 2): workgroups k
+    and k + H (H = G / 2, G even) claim from the pair's own counter, chunk p + (2 S + c) H
+    (p = k mod H) -- their static rounds k + r G are the pair's chunks p + (2 r + k / H) H."""
     g0, total = [], 0
     for n in batch_groups:
         g0.append(total)
         total += n
     G = grid
+    H = G // 2
+    if pairs:
+        assert G % 2 == 0 and G >= 2
     counter = 0
+    pair_ctr = [0] * max(H, 1)
     seen, per_wave = {}, []
     wgs = [dict(ctr=S * W, pub={}, unread={}) for _ in range(G)]
     # per wave: wg, wave, slots taken, batch cursor, state, slot, groups
@@ -770,8 +777,13 @@ def vring_dynamic_rounds_deal(batch_groups, grid: int, rng, W: int = 16, K: int 
             r1 = v["sl"] // W + 1
             assert not wg["unread"].get(r1 - K), "round entry rewritten while still to be read"
             wg["pub"].pop(r1 - K, None)
-            wg["pub"][r1] = S * G + counter
-            counter += 1
+            if pairs:
+                p = v["k"] % H
+                wg["pub"][r1] = p + (2 * S + pair_ctr[p]) * H
+                pair_ctr[p] += 1
+            else:
+                wg["pub"][r1] = S * G + counter
+                counter += 1
             v["st"] = "read"
         else:                                               # read: the slot's group
             r = v["sl"] // W

@@ -853,21 +853,22 @@ def test_dynamic_rounds_claim_lines_reused_across_streams(dctx, oracle_lib):
     streams = [torch.cuda.Stream() for _ in range(3)]
     ctx = dctx
     try:
-        ctx.diag_ablation(524288)                     # the dynamic rounds
-        for lanes in (8, 4):
-            ctx.set_tuning(lanes, 0)
-            outs = []
-            for k in range(300):
-                d_p, d_o, d_l, n, exp = batches[k % len(batches)]
-                st = streams[k % 3]
-                out = torch.full((n,), -1, dtype=torch.int32, device="cuda")
-                st.wait_stream(torch.cuda.current_stream())      # (the fill first: the side streams do not wait)
-                with torch.cuda.stream(st):
-                    ctx.crc32_batch_device(d_p, d_o, d_l, n, out, stream=st.cuda_stream)
-                outs.append((out, exp, k))
-            torch.cuda.synchronize()
-            for out, exp, k in outs:
-                assert (out.cpu().numpy().view(np.uint32) == exp).all(), (lanes, k)
+        for mode in (524288, 8388608):                # the chip-wide and the pair rounds
+            ctx.diag_ablation(mode)
+            for lanes in (8, 4):
+                ctx.set_tuning(lanes, 0)
+                outs = []
+                for k in range(300):
+                    d_p, d_o, d_l, n, exp = batches[k % len(batches)]
+                    st = streams[k % 3]
+                    out = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+                    st.wait_stream(torch.cuda.current_stream())      # (the fill first: the side streams do not wait)
+                    with torch.cuda.stream(st):
+                        ctx.crc32_batch_device(d_p, d_o, d_l, n, out, stream=st.cuda_stream)
+                    outs.append((out, exp, k))
+                torch.cuda.synchronize()
+                for out, exp, k in outs:
+                    assert (out.cpu().numpy().view(np.uint32) == exp).all(), (mode, lanes, k)
     finally:
         ctx.diag_ablation(0)
         ctx.set_tuning(0, 0)
@@ -879,7 +880,7 @@ def test_dynamic_rounds_match_static_deal(dctx, oracle_lib):
     b = workloads.mixed(262144, 64, 1400, seed=0x44594E, name="cfg3")
     exp = oracle_lib.batch(b.payload, b.off, b.lens, threads=16)
     try:
-        for mode in (0, 524288):
+        for mode in (0, 524288, 8388608):         # static, chip-wide rounds, pair rounds
             dctx.diag_ablation(mode)
             dctx.set_kernel_path(0)
             got = run_batch(dctx, b.payload, b.off, b.lens)

@@ -313,7 +313,7 @@ def test_vring_dynamic_slots_cover_every_group_once(batch_groups, grid):
 @pytest.mark.parametrize("batch_groups,grid", [([512] * 5, 16), ([1], 1), ([0, 3, 0, 17], 2),
                                                ([900, 1, 70, 2, 300], 9), ([33] * 48, 7), ([4000], 3)])
 def test_vring_dynamic_rounds_cover_every_group_once(batch_groups, grid):
-    """The vring kernel's dynamic rounds (DYN): whatever the interleaving of all
+    """The vring kernel's dynamic rounds (DYN 1, and the pair rounds of DYN 2): whatever the interleaving of all
     workgroups' waves and the completion order of their round claims, every group is
     processed exactly once in its own batch, a wave's groups ascend, no wave waits
     forever and no round-table entry is rewritten while it is still to be read."""
@@ -323,12 +323,18 @@ def test_vring_dynamic_rounds_cover_every_group_once(batch_groups, grid):
     grid = max(1, min(grid, (sum(nonempty) + 15) // 16))
     for seed in range(3):
         rng = random.Random(seed * 7919 + sum(batch_groups) + grid)
-        seen, per_wave, total = vring_dynamic_rounds_deal(nonempty, grid, rng)
-        assert sorted(seen) == list(range(total))
-        g0 = [sum(nonempty[:b]) for b in range(len(nonempty))]
-        for gg, (b, local) in seen.items():
-            assert 0 <= local < nonempty[b] and g0[b] + local == gg
-        assert sum(per_wave) == total
+        for pairs in (False, True):
+            g = grid
+            if pairs:                              # (the host: an even grid of at least 2)
+                if g < 2:
+                    continue
+                g &= ~1
+            seen, per_wave, total = vring_dynamic_rounds_deal(nonempty, g, rng, pairs=pairs)
+            assert sorted(seen) == list(range(total))
+            g0 = [sum(nonempty[:b]) for b in range(len(nonempty))]
+            for gg, (b, local) in seen.items():
+                assert 0 <= local < nonempty[b] and g0[b] + local == gg
+            assert sum(per_wave) == total
 
 
 def test_gather_join_matches_oracle(oracle_lib):
