@@ -1144,7 +1144,8 @@ const void* vring_fn(int dyn = 0) {
     if constexpr (TR != 1 && NT == 0 && ABL == 0 && WK == 0 && ROT == 0) {
         if (dyn == 1) return reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT, VF, 1>);
 #ifdef ENET_HIP_DIAG
-        if (dyn == 2) return reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT, VF, 2>);
+        if constexpr (!BIN)                                  // (pair rounds: not for the records instance)
+            if (dyn == 2) return reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT, VF, 2>);
 #endif
     }
     return dyn == 0 ? reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT, VF>) : nullptr;
@@ -1279,8 +1280,8 @@ int vring_launch_list(int lg, int max_wgs, const VrVariant& v, hipStream_t st, c
     unsigned grid = static_cast<unsigned>(std::max<uint64_t>(
         1, std::min<uint64_t>((a.groups + kVrW - 1) / kVrW, static_cast<uint64_t>(max_wgs))));
     VrVariant w = v;
-    if (vring_dyn(w) == 2) {                                 // pairs: an even grid of at least 2
-        if (grid < 2 || grid / 2 > static_cast<unsigned>(kVrPairWords)) w.claim = a.claim = nullptr;
+    if (vring_dyn(w) == 2) {                                 // pairs: an even grid of at least 2 (not binned)
+        if (bin || grid < 2 || grid / 2 > static_cast<unsigned>(kVrPairWords)) w.claim = a.claim = nullptr;
         grid &= ~1u;
         grid = std::max(grid, 1u);
     }
