@@ -1352,7 +1352,11 @@ int verify_vring_list(enet_hip_context* ctx, const ENetHipVerifyBatch* batches, 
             bl.b[bl.count++] = VrVBatch{e.bytes, e.offsets, e.lengths, e.computed, static_cast<uint64_t>(e.count), 0u,
                                         e.slotOffsets, e.connectIds, e.ok};
         }
-        const int rc = vring_launch_vlist(ctx->num_cus * vring_wgs(ctx, bl.count), with_claim(ctx, v), st, bl, tb, ctx->d_basis2,
+        // two workgroups per CU by default, single batches too: one cfg2 batch 20.4-20.5 us
+        // against 22.1 at one (profiles/r04_verify_wgs/; the checksum instance is the
+        // other way round, 18.9 against 18.2-18.4)
+        const int wgs = ctx->wgs_per_cu >= 1 ? std::min(ctx->wgs_per_cu, 2) : 2;
+        const int rc = vring_launch_vlist(ctx->num_cus * wgs, with_claim(ctx, v), st, bl, tb, ctx->d_basis2,
                                           v.abl ? ctx->trace : nullptr);
         if (rc) return rc;
     }

@@ -74,7 +74,8 @@ ENET_HIP_API const char* enet_hip_error_string(int code);
  * packet (a power of two; default 8, and 4 for the length-binned entries);
  * workgroups_per_cu (0..8): resident workgroups per CU.  The VGPR-ring kernel runs
  * 1 or 2 (values above 2 mean 2 there; default 2 for a launch of several batches,
- * 1 for a single batch); the direct and gather grids use the value as given. */
+ * 1 for a single checksum batch, 2 for receive verify); the direct and gather grids
+ * use the value as given. */
 ENET_HIP_API int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgroups_per_cu);
 
 /* Kernel path for the packet batch entry points (0 = default): checksum batches

@@ -36,13 +36,14 @@ def main():
     ap.add_argument("--lanes", type=int, default=0)
     ap.add_argument("--rotate", type=int, default=5)
     ap.add_argument("--list", type=int, default=5)
+    ap.add_argument("--wgs", type=int, default=0, help="workgroups per CU (enet_hip_set_tuning; 0 = default)")
     ap.add_argument("--path", type=int, default=0, help="kernel path (13 = the lean kernel; 0 = vring at 8 lanes)")
     a = ap.parse_args()
     import torch
     import enethip
     from enethip import workloads
     import oracle as orc
-    ctx = enethip.Context(0, a.lanes, 0)
+    ctx = enethip.Context(0, a.lanes, a.wgs)
     ctx.set_kernel_path(a.path)
     st = torch.cuda.Stream()
     off = np.arange(N, dtype=np.uint64) * L
