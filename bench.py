@@ -401,8 +401,8 @@ PRODUCT_PATHS = (0, 1, 2, 13, 17)          # built in libenethip.so (the rest: l
 
 def kernel_name(args, list_launch: bool = False) -> str:
     """The dominant kernel of the measured entry point (as rocprofv3 names it:
-    crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT, VF, DYN>; DYN = 1, the dynamic
-    rounds, when the diagnostics ablation 524288 selects them)."""
+    crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT, VF, DYN>; DYN = 1 / 2, the chip-wide
+    / pair rounds, when the diagnostics ablation 524288 / 8388608 selects them)."""
     path = getattr(args, "path", 0)
     if path in (22, 23) and not args.binned:
         return f"crc32_lin_kernel<{lin_abl(args.ablate)}, {1 if path == 22 else 0}>"
@@ -413,14 +413,15 @@ def kernel_name(args, list_launch: bool = False) -> str:
     lg = {4: 2, 8: 3}.get(lanes)
     if path and path not in (17, 18, 21):
         return f"kernel path {path}"
-    dyn = 1 if (args.ablate & 524288) else 0
+    dyn = 2 if (args.ablate & 8388608) else 1 if (args.ablate & 524288) else 0   # (pair / chip-wide rounds)
     if args.binned:
+        dyn = 0 if dyn == 2 else dyn                          # (no pair rounds for the records instance)
         return (f"crc32_vring_kernel<{lg}, 0, 0, 0, 1, 0, 0, 0, {dyn}>" if path in (0, 17)
                 else f"crc32_lean_kernel<0, {lg}, 16, 2, 128>")
     if lg is None:
         return "crc32_stream_kernel / crc32_direct_kernel"
     nt, rot = (1 if path == 18 else 0), (1 if path == 21 else 0)
-    dyn = dyn if not (nt or rot or (args.ablate & ~524288)) else 0
+    dyn = dyn if not (nt or rot or (args.ablate & ~(524288 | 8388608))) else 0
     return f"crc32_vring_kernel<{lg}, 0, {nt}, 0, 0, 0, {rot}, 0, {dyn}>"
 
 
