@@ -1226,6 +1226,12 @@ bool path_built(int path) {
     return path == 0 || path == 1 || path == 2 || path == kLeanPath0 || path == kVringPath;
 #endif
 }
+// the binned gather's short-segment bound (segments of at most this many bytes are
+// folded by the join, not binned): kGatherSmall, or (diagnostics A/B) a smaller one
+uint32_t gather_small(const enet_hip_context* ctx) {
+    return ctx->gather_small >= 0 && static_cast<uint32_t>(ctx->gather_small) < kGatherSmall
+               ? static_cast<uint32_t>(ctx->gather_small) : kGatherSmall;
+}
 bool lin_path(const enet_hip_context* ctx) { return ctx->path == kLinPath || ctx->path == kLinPlainPath; }
 // the linear kernel's ablation (diagnostics: enet_hip_diag_ablation 2048 = no boundary
 // passes, + 4096 = no fold lookups either; wrong CRCs by design)
@@ -1540,9 +1546,11 @@ int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgro
 
 #ifdef ENET_HIP_DIAG
 int enet_hip_diag_ablation(enet_hip_context* ctx, int mode) {
-    if (!ctx || mode < 0 || mode >= (1 << 24)) return -static_cast<int>(hipErrorInvalidValue);
+    if (!ctx || mode < 0 || mode >= (1 << 30)) return -static_cast<int>(hipErrorInvalidValue);
     ctx->vr_pair = (mode >> 23) & 1;                         // 8388608: vring pair rounds
     ctx->join_abl = (mode >> 20) & 7;                        // 1048576 x (1..7): gather-join ablations
+    // 16777216 x (1 + b), b < 63: the binned gather's short-segment bound b bytes (0: 48)
+    ctx->gather_small = (mode >> 24) ? ((mode >> 24) & 63) - 1 : -1;
     ctx->vr_dynamic = (mode >> 19) & 1;                      // 524288: vring dynamic rounds
     const int prio = (mode & 1024) ? 2 : (mode >> 3) & 1;    // 8: static / 1024: progress priority
     ctx->vr_abl = (mode >> 11) & 255;                        // 2048 ... 262144: vring ablations / end records
@@ -1823,7 +1831,7 @@ int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* by
         const KernelTables tb = tables_of(ctx);
         const uint32_t kpk = lanes == 4 ? 16u : 8u;
         int rc;
-        if ((rc = length_bin_compact(segLengths, segOffsets, segCount, kpk, kGatherSmall, workspace, counts, st)))
+        if ((rc = length_bin_compact(segLengths, segOffsets, segCount, kpk, gather_small(ctx), workspace, counts, st)))
             return rc;
         VrBatches bl{};
         bl.count = 1;
@@ -1840,7 +1848,7 @@ int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* by
     }
     GatherArgs ga{bytes, segOffsets, segLengths, segFirst, dgramCount, out, segCount};
     const unsigned grid = grid_for(ctx, dgramCount);
-    const uint32_t small = split ? kGatherSmall : 0u;
+    const uint32_t small = split ? gather_small(ctx) : 0u;
 #ifdef ENET_HIP_DIAG
     switch (ctx->join_abl) {
         case 1: hipLaunchKernelGGL(crc32_gather_join_kernel<1>, dim3(grid), dim3(kThreads), 0, st, ga, seg_crc, tables_of(ctx), small); break;

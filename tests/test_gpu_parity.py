@@ -889,3 +889,18 @@ def test_dynamic_rounds_match_static_deal(dctx, oracle_lib):
         dctx.diag_ablation(0)
         dctx.set_tuning(0, 0)
 
+
+
+def test_gather_binned_short_segment_bounds(dctx, golden, oracle_lib):
+    """The binned gather with other short-segment bounds (diagnostics A/B: segments of
+    at most b bytes folded by the join, the rest binned), b = 0, 8, 24 and the default,
+    on test_gather_binned's lists: the split moves, the CRCs do not."""
+    cases = _gather_cases(golden, oracle_lib)
+    try:
+        for b in (0, 8, 24, 48):
+            dctx.diag_ablation(16777216 * (1 + b) if b < 48 else 0)
+            for i, (p, so, sl, f, e) in enumerate(cases):
+                got = _run_gather_binned(dctx, p, so, sl, f)
+                assert (got == e).all(), (b, i, np.nonzero(got != e)[0][:5])
+    finally:
+        dctx.diag_ablation(0)
