@@ -397,9 +397,11 @@ ENET_HIP_API int enet_hip_read_probe_device(enet_hip_context* ctx, const uint8_t
  * 2048 = no boundary passes, 2048 + 4096 = no fold lookups either (WRONG
  * checksums).  524288 (correct checksums): the vring's dynamic rounds (rounds
  * past the third claimed chip-wide from a per-launch claim line) instead of the
- * static deal.  1048576 x j, j = 1..7: the gather join without its short-segment
- * fold (bit 0 of j), its multiplies (bit 1), its short-segment loads (bit 2) --
- * WRONG checksums. */
+ * static deal; 8388608 (correct checksums): pair rounds (workgroups k and k + G/2
+ * share a claim word).  1048576 x j, j = 1..7: the gather join without its
+ * short-segment fold (bit 0 of j), its multiplies (bit 1), its short-segment loads
+ * (bit 2) -- WRONG checksums.  16777216 x (1 + b), b < 48 (correct checksums): the
+ * binned gather folds segments of at most b bytes in the join (default 48). */
 ENET_HIP_API int enet_hip_diag_ablation(enet_hip_context* ctx, int mode);
 
 /* ---- diagnostics: per-wave timeline of the lean stream kernel ----
