@@ -416,7 +416,10 @@ def kernel_name(args, list_launch: bool = False) -> str:
     dyn = 2 if (args.ablate & 8388608) else 1 if (args.ablate & 524288) else 0   # (pair / chip-wide rounds)
     if args.binned:
         dyn = 0 if dyn == 2 else dyn                          # (no pair rounds for the records instance)
-        return (f"crc32_vring_kernel<{lg}, 0, 0, 0, 1, 0, 0, 0, {dyn}>" if path in (0, 17)
+        abl = (args.ablate >> 11) & 255
+        abl = abl if abl in (2, 19) and lg == 2 else 0        # (the records instance's ablations, 4 lanes)
+        dyn = 0 if abl else dyn
+        return (f"crc32_vring_kernel<{lg}, 0, 0, {abl}, 1, 0, 0, 0, {dyn}>" if path in (0, 17)
                 else f"crc32_lean_kernel<0, {lg}, 16, 2, 128>")
     if lg is None:
         return "crc32_stream_kernel / crc32_direct_kernel"

@@ -1338,6 +1338,13 @@ VrVariant vring_variant(const enet_hip_context* ctx, bool lists) {
     return v;
 }
 
+// the records instance: plain, or (diagnostics) its no-lookup / skeleton ablations
+VrVariant bin_variant(const enet_hip_context* ctx) {
+    VrVariant v;
+    v.abl = (ctx->vr_abl == 2 || ctx->vr_abl == 19) ? ctx->vr_abl : 0;
+    return v;
+}
+
 // Receive verify on the vring kernel (8 lanes per packet, VF instance): the default
 // (path 0) and the vring paths 17 / 21; the lean kernel serves 4 lanes, the binned
 // records and path 13.
@@ -1387,7 +1394,7 @@ int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStr
     }
     if (mode == 0 && (pa.lg == 2 || pa.lg == 3) && ctx->ablation == 0 && vring_path(ctx))
         return vring_launch(pa.lg, ctx->num_cus * vring_wgs(ctx, 1),
-                            with_claim(ctx, pa.meta4 ? VrVariant{} : vring_variant(ctx, false)), st, pa, tb,
+                            with_claim(ctx, pa.meta4 ? bin_variant(ctx) : vring_variant(ctx, false)), st, pa, tb,
                             ctx->d_basis2);
     if (ctx->path != 1 && pa.lg >= 2 && pa.lg <= 4) {
         const bool lean_path = (ctx->path >= kLeanPath0 && ctx->path < kVringPath) || (ctx->path == 0 && ctx->ablation == 0);

@@ -1162,8 +1162,14 @@ const void* vring_pick_v(bool trace, const VrVariant& v) {
 #endif
     return nullptr;
 }
-const void* vring_pick_bin(int lg, int dyn) {
-    return lg == 2 ? vring_fn<2, 0, 0, 0, 1>(dyn) : vring_fn<3, 0, 0, 0, 1>(dyn);
+// (diagnostics: abl 2 = no fold lookups, 19 = no masks, lookups or end corrections, at 4 lanes)
+const void* vring_pick_bin(int lg, int dyn, int abl = 0) {
+    if (abl == 0) return lg == 2 ? vring_fn<2, 0, 0, 0, 1>(dyn) : vring_fn<3, 0, 0, 0, 1>(dyn);
+#ifdef ENET_HIP_DIAG
+    if (lg == 2 && dyn == 0 && abl == 2) return vring_fn<2, 0, 0, 2, 1>();
+    if (lg == 2 && dyn == 0 && abl == 19) return vring_fn<2, 0, 0, 19, 1>();
+#endif
+    return nullptr;
 }
 
 // The product instances: 64 VGPRs (WPE 8), one or two workgroups per CU, stages in
@@ -1238,7 +1244,8 @@ int vring_setup() {
             }
         for (int lg = 2; lg <= 3; ++lg) {
             int rc;
-            if ((rc = set(vring_pick_bin(lg, d), kVrLdsBin))) return rc;
+            for (int abl : {0, 2, 19})
+                if ((rc = set(vring_pick_bin(lg, d, abl), kVrLdsBin))) return rc;
             for (int t = 0; t < 2; ++t)
                 for (int nt = 0; nt < 2; ++nt)
                     for (int abl : kAbl)
@@ -1285,7 +1292,7 @@ int vring_launch_list(int lg, int max_wgs, const VrVariant& v, hipStream_t st, c
         grid &= ~1u;
         grid = std::max(grid, 1u);
     }
-    const void* fn = bin ? vring_pick_bin(lg, vring_dyn(w)) : vring_pick(lg, trace != nullptr, w);
+    const void* fn = bin ? vring_pick_bin(lg, vring_dyn(w), w.abl) : vring_pick(lg, trace != nullptr, w);
     if (!fn) return -static_cast<int>(hipErrorInvalidValue);   // a variant this library does not build
     // slots are 32-bit: a workgroup's slot count (rounds x 16) must fit
     if ((a.groups / (static_cast<uint64_t>(grid) * kVrW) + 3u) * kVrW > 0xFFFFFFF0ull)

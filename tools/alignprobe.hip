@@ -12,6 +12,8 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
+#include <algorithm>
 #include <vector>
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -59,7 +61,7 @@ __global__ void __launch_bounds__(256) ap_packets(const uint8_t* p, const uint64
     if (x == 0x9E3779B9u) sink[0] = x;
 }
 
-int main() {
+int main(int argc, char** argv) {
     const uint64_t bytes = 768ull << 20;
     uint8_t* d;
     uint32_t* sink;
@@ -88,8 +90,8 @@ int main() {
         timeit([&] { hipLaunchKernelGGL(ap_stride, dim3(256 * 8), dim3(256), 0, 0, d, nvec, sh, sink); },
                static_cast<double>(nvec) * 16, name);
     }
-    // cfg3-like packed packets: lengths U[64, 1400], 1 M of them (~ 766 MB)
-    const uint64_t n = 1000000;
+    // cfg3-like packed packets: lengths U[64, 1400], 1 M of them (~ 766 MB) unless argv[1] says
+    const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : 1000000;   // cfg3: 262144
     std::vector<uint32_t> len(n);
     uint64_t s = 0x4C454E53ull;
     uint64_t tot = 0;
@@ -150,6 +152,33 @@ int main() {
                static_cast<double>(tot), "shuffled packets, 4 lanes");
         timeit([&] { hipLaunchKernelGGL(ap_packets<8>, dim3(256 * 4), dim3(256), 0, 0, d, dw, dn, n, sink); },
                static_cast<double>(tot), "shuffled packets, 8 lanes");
+    }
+    // the binned records' order (crc32_lean.hip bin_tile_kernel): each tile of `tile`
+    // packets sorted by window length (32-B bins, longest first, stable inside a bin),
+    // group q of tile t placed at q * T + t (rank-interleaved) or left tile-local
+    for (uint64_t tile : {1024ull, 512ull, 256ull, 128ull}) {
+        for (int inter = 1; inter >= 0; --inter) {
+            const uint64_t kpk = 16, T = n / tile;             // full tiles; the ragged rest stays in order
+            std::vector<uint64_t> ws2(wa);
+            std::vector<uint32_t> ns2(na);
+            std::vector<uint64_t> idx(tile);
+            for (uint64_t t = 0; t < T; ++t) {
+                for (uint64_t i = 0; i < tile; ++i) idx[i] = t * tile + i;
+                std::stable_sort(idx.begin(), idx.end(), [&](uint64_t a, uint64_t b) { return na[a] > na[b]; });
+                for (uint64_t sr = 0; sr < tile; ++sr) {
+                    const uint64_t dst = inter ? ((sr / kpk) * T + t) * kpk + sr % kpk : t * tile + sr;
+                    ws2[dst] = wa[idx[sr]];
+                    ns2[dst] = na[idx[sr]];
+                }
+            }
+            hipMemcpy(dw, ws2.data(), 8 * n, hipMemcpyHostToDevice);
+            hipMemcpy(dn, ns2.data(), 4 * n, hipMemcpyHostToDevice);
+            char name[96];
+            snprintf(name, sizeof name, "binned order, 4 lanes, tile %llu, %s", static_cast<unsigned long long>(tile),
+                     inter ? "rank-interleaved" : "tile-local");
+            timeit([&] { hipLaunchKernelGGL(ap_packets<4>, dim3(256 * 4), dim3(256), 0, 0, d, dw, dn, n, sink); },
+                   static_cast<double>(tot), name);
+        }
     }
     return 0;
 }
