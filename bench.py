@@ -417,9 +417,10 @@ def kernel_name(args, list_launch: bool = False) -> str:
     if args.binned:
         dyn = 0 if dyn == 2 else dyn                          # (no pair rounds for the records instance)
         abl = (args.ablate >> 11) & 255
-        abl = abl if abl in (2, 19) and lg == 2 else 0        # (the records instance's ablations, 4 lanes)
+        abl = abl if abl in (2, 19, 64, 83) and lg == 2 else 0   # (the records instance's ablations, 4 lanes)
         dyn = 0 if abl else dyn
-        return (f"crc32_vring_kernel<{lg}, 0, 0, {abl}, 1, 0, 0, 0, {dyn}>" if path in (0, 17)
+        bin_ = 2 if getattr(args, "wgs", 0) >= 2 else 1          # (two workgroups per CU: the compact instance)
+        return (f"crc32_vring_kernel<{lg}, 0, 0, {abl}, {bin_}, 0, 0, 0, {dyn}>" if path in (0, 17)
                 else f"crc32_lean_kernel<0, {lg}, 16, 2, 128>")
     if lg is None:
         return "crc32_stream_kernel / crc32_direct_kernel"

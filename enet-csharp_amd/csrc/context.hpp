@@ -40,6 +40,7 @@ struct enet_hip_context {
     std::atomic<uint64_t> pairs_next{0};
     bool vr_pair = false;
     int join_abl = 0;            // diagnostics library: gather-join ablations
+    bool bin_identity = false;   // diagnostics library: binned records left in memory order (not sorted)
     int gather_small = -1;       // diagnostics library: the binned gather's short-segment bound (-1: default)
     // host-memory entry points (host_pipeline.hip): calls on one context serialize on mu
     std::mutex mu;

@@ -1341,7 +1341,9 @@ VrVariant vring_variant(const enet_hip_context* ctx, bool lists) {
 // the records instance: plain, or (diagnostics) its no-lookup / skeleton ablations
 VrVariant bin_variant(const enet_hip_context* ctx) {
     VrVariant v;
-    v.abl = (ctx->vr_abl == 2 || ctx->vr_abl == 19) ? ctx->vr_abl : 0;
+    const int a = ctx->vr_abl;
+    v.abl = (a == 2 || a == 19 || a == 64 || a == 83) ? a : 0;
+    v.compact = vring_wgs(ctx, 1) >= 2;                      // (two workgroups per CU: the compact instance)
     return v;
 }
 
@@ -1553,7 +1555,8 @@ int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgro
 
 #ifdef ENET_HIP_DIAG
 int enet_hip_diag_ablation(enet_hip_context* ctx, int mode) {
-    if (!ctx || mode < 0 || mode >= (1 << 30)) return -static_cast<int>(hipErrorInvalidValue);
+    if (!ctx || mode < 0) return -static_cast<int>(hipErrorInvalidValue);
+    ctx->bin_identity = (mode >> 30) & 1;                    // 2^30: binned records left in memory order
     ctx->vr_pair = (mode >> 23) & 1;                         // 8388608: vring pair rounds
     ctx->join_abl = (mode >> 20) & 7;                        // 1048576 x (1..7): gather-join ablations
     // 16777216 x (1 + b), b < 63: the binned gather's short-segment bound b bytes (0: 48)
@@ -1696,7 +1699,8 @@ int enet_hip_crc32_batch_device_binned(enet_hip_context* ctx, const uint8_t* byt
                       ((ctx->path >= kLeanPath0 && ctx->path < kVringPath) || vring_path(ctx));
     if (lean) {
         int rc;
-        if ((rc = length_bin(lengths, offsets, nullptr, nullptr, count, 64u >> pa.lg, workspace, st))) return rc;
+        if ((rc = length_bin(lengths, offsets, nullptr, nullptr, count, 64u >> pa.lg, workspace, st, ctx->bin_identity)))
+            return rc;
         pa.meta4 = static_cast<const uint32_t*>(workspace);
     }
     return launch_packets(ctx, 0, pa, st);
@@ -1845,8 +1849,13 @@ int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* by
         bl.tiles = static_cast<uint32_t>(gather_tiles(segCount));
         bl.tile_counts = counts;
         bl.b[0] = VrBatch{bytes, static_cast<const uint64_t*>(workspace), nullptr, seg_crc, 1024ull * bl.tiles, 0u};
-        if ((rc = vring_launch_list(lanes == 4 ? 2 : 3, ctx->num_cus * vring_wgs(ctx, 1), with_claim(ctx, VrVariant{}),
-                                    st, bl, tb, ctx->d_basis2, nullptr, true)))
+        // two workgroups per CU unless set: the compact records instance (cfg5 67.8-68.3 against
+        // 69.9-70.0 us at one, profiles/r04_compact/)
+        const int gw = ctx->wgs_per_cu >= 1 ? std::min(ctx->wgs_per_cu, 2) : 2;
+        VrVariant gv = bin_variant(ctx);
+        gv.compact = gw >= 2;
+        if ((rc = vring_launch_list(lanes == 4 ? 2 : 3, ctx->num_cus * gw, with_claim(ctx, gv), st, bl, tb,
+                                    ctx->d_basis2, nullptr, true)))
             return rc;
     } else if (segCount) {                                   // every segment's CRC, mixed lengths: length-binned
         const int rc = enet_hip_crc32_batch_device_binned(ctx, bytes, segOffsets, segLengths, segCount, seg_crc,

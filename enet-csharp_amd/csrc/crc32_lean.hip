@@ -754,7 +754,9 @@ __device__ __forceinline__ uint32_t bin_of(uint32_t len, uint64_t off) {
 // its kept records sorted and then empty records {0, 0, 0, pad_index} up to 1024,
 // all rank-interleaved (group q T + t, T = every tile), and count[t] = its kept
 // records.  No global atomics: the vring's records instance reads the counts.
-template <bool VERIFY, bool COMPACT = false>
+// IDENT (diagnostics): every record left at its own position (memory order), to price
+// the binned order against the records machinery.
+template <bool VERIFY, bool COMPACT = false, bool IDENT = false>
 __global__ void __launch_bounds__(kBinThreads) bin_tile_kernel(const uint32_t* len, const uint64_t* off, uint64_t n,
                                                                uint32_t kpk, const uint32_t* slot_off,
                                                                const uint32_t* connect, uint4* rec, uint32_t small,
@@ -808,8 +810,8 @@ __global__ void __launch_bounds__(kBinThreads) bin_tile_kernel(const uint32_t* l
 #pragma unroll
     for (uint32_t r = 0; r < kBinItems; ++r) {
         const uint64_t i = base + r * kBinThreads + tid;
-        const uint32_t srt = h[bin_of(L[r], o[r])] + slot[r];   // rank inside the tile
-        const uint64_t dst = interleave ? ((srt / kpk) * full + blockIdx.x) * kpk + srt % kpk : base + srt;
+        const uint32_t srt = IDENT ? r * kBinThreads + tid : h[bin_of(L[r], o[r])] + slot[r];   // rank inside the tile
+        const uint64_t dst = (interleave && !IDENT) ? ((srt / kpk) * full + blockIdx.x) * kpk + srt % kpk : base + srt;
         if (kept(r)) {
             if constexpr (VERIFY) {
                 rec[2 * dst] = make_uint4(L[r], static_cast<uint32_t>(o[r]), static_cast<uint32_t>(o[r] >> 32), slot_off[i]);
@@ -825,10 +827,18 @@ __global__ void __launch_bounds__(kBinThreads) bin_tile_kernel(const uint32_t* l
 size_t length_bin_workspace(uint64_t n, bool verify) { return (verify ? 32u : 16u) * n; }
 
 int length_bin(const uint32_t* len, const uint64_t* off, const uint32_t* slot_off, const uint32_t* connect, uint64_t n,
-               uint32_t kpk, void* workspace, hipStream_t st) {
+               uint32_t kpk, void* workspace, hipStream_t st, bool identity) {
     if (n == 0) return 0;
     if (n > 0xFFFFFFFFull || !workspace || kpk == 0 || kBinTile % kpk) return -static_cast<int>(hipErrorInvalidValue);
     const unsigned tiles = static_cast<unsigned>((n + kBinTile - 1) / kBinTile);
+#ifdef ENET_HIP_DIAG
+    if (identity && !(slot_off && connect))
+        hipLaunchKernelGGL((bin_tile_kernel<false, false, true>), dim3(tiles), dim3(kBinThreads), 0, st, len, off, n, kpk,
+                           nullptr, nullptr, static_cast<uint4*>(workspace), 0u, nullptr);
+    else
+#else
+    (void)identity;
+#endif
     if (slot_off && connect)
         hipLaunchKernelGGL(bin_tile_kernel<true>, dim3(tiles), dim3(kBinThreads), 0, st, len, off, n, kpk, slot_off,
                            connect, static_cast<uint4*>(workspace), 0u, nullptr);

@@ -78,7 +78,7 @@ int lean_launch_vlist(int lg, int num_cus, hipStream_t st, const ENetHipVerifyBa
 // Stream-ordered; n < 2^32.  Returns 0 or -hipError_t.
 size_t length_bin_workspace(uint64_t n, bool verify);
 int length_bin(const uint32_t* len, const uint64_t* off, const uint32_t* slot_off, const uint32_t* connect, uint64_t n,
-               uint32_t kpk, void* workspace, hipStream_t st);
+               uint32_t kpk, void* workspace, hipStream_t st, bool identity = false);
 // The binned gather's records: per 1024-segment tile (T = ceil(n / 1024), the
 // ragged last one included), the records {len, off_lo, off_hi, index} of the
 // segments longer than `small`, sorted longest first, then empty records {0, 0, 0,

@@ -72,6 +72,13 @@ constexpr uint32_t kVrTz7 = kVrLds;
 constexpr uint32_t kVrTileMax = kVrTz7 + kTzSmallDwords * 4;
 constexpr int kVrLdsBin = kVrTileMax + kVrW * 4;
 static_assert(kVrLdsBin <= 160 * 1024, "records instance LDS");
+// the compact records instance (BIN = 2): no x^(-8 c) tables (tz mod 8 by unsteps), the
+// tile maxima right after the plain layout -- 79 KiB, two workgroups per CU
+constexpr uint32_t kVrTileMaxC = kVrLds;
+constexpr int kVrLdsBinC = kVrTileMaxC + kVrW * 4;
+static_assert(2 * kVrLdsBinC <= 160 * 1024, "compact records instance: two workgroups per CU");
+template <int BIN>
+constexpr uint32_t vr_tile_max() { return BIN == 2 ? kVrTileMaxC : kVrTileMax; }
 // BIN's index stash (two slots of kPk dwords per wave) fits the basis staging area
 static_assert(kVrW * 2 * 16 * 4 <= kVrBasisRows * 256, "index stash over the basis staging area");
 
@@ -552,7 +559,9 @@ struct VrIt {
 // bit 4 = no end-of-packet corrections (wrong CRCs by design)
 // BIN = 1: the batch's metadata are length-binned records (VrBatch::off points at
 // them, 4 dwords per packet), read in record order; packet r's CRC goes to
-// out[record r's index] (enet_hip_crc32_batch_device_binned).  One workgroup per CU.
+// out[record r's index] (enet_hip_crc32_batch_device_binned).  One workgroup per CU;
+// BIN = 2, the compact records instance: the same without the x^(-8 c) tables (tz mod 8
+// by unsteps), two workgroups per CU.
 // ROT = 1: the tail-first stage order (below; diagnostics library); 0 = stages in
 // window order (the product).
 // VF = 1: receive verify (protocol.cs:1052-1068) over a VrVBatches list, 8 lanes per
@@ -634,12 +643,12 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
                 m = max(m, bl.tile_counts[t]);
             m = wave_max_u(m);
             if ((threadIdx.x & 63u) == 0u) *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(
-                static_cast<uintptr_t>(kVrTileMax + 4u * wave)) = m;
+                static_cast<uintptr_t>(vr_tile_max<BIN>() + 4u * wave)) = m;
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the store is in LDS
             __builtin_amdgcn_s_barrier();
             uint32_t mm = 0;
 #pragma unroll
-            for (uint32_t w = 0; w < kVrW; ++w) mm = max(mm, lds_load(kVrTileMax + 4u * w));
+            for (uint32_t w = 0; w < kVrW; ++w) mm = max(mm, lds_load(vr_tile_max<BIN>() + 4u * w));
             const uint32_t r = (mm + kPk - 1u) / kPk;
             ngroups_all = static_cast<uint64_t>(r) * bl.tiles;
             n0 = ngroups_all * kPk;
@@ -746,7 +755,7 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
              kVrStaging + 256u * wave);
     // waves 0..7: one KiB each of the zero-byte multiplier tables
     if (wave < static_cast<uint32_t>(kTzTableDwords / 256)) dma16(tb.tz + 256u * wave + 4u * lane, kVrTz + 1024u * wave);
-    if constexpr (BIN) {                                     // the small x^(-8 c) tables: 28 one-KiB chunks
+    if constexpr (BIN == 1) {                                // the small x^(-8 c) tables: 28 one-KiB chunks
 #pragma unroll
         for (uint32_t c = wave; c < static_cast<uint32_t>(kTzSmallDwords / 256); c += kVrW)
             dma16(tb.tz + kTzTableDwords + 256u * c + 4u * lane, kVrTz7 + 1024u * c);
@@ -1006,7 +1015,8 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
         clz = plz();
         ce = pe;
         const uint64_t base = group_base(pit);
-        cout = bl.b[pit.b].out ? bl.b[pit.b].out + (BIN ? 0u : base) : nullptr;
+        // (BIN with ABL & 64, diagnostics: CRCs written in record order, as an unbinned batch)
+        cout = bl.b[pit.b].out ? bl.b[pit.b].out + ((BIN && !(ABL & 64)) ? 0u : base) : nullptr;
         if constexpr (VF) {
             cok = bl.b[pit.b].ok + base;
             cps = pps;
@@ -1101,7 +1111,7 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
             // lookup and about 6 VALU each).  All unsteps (round 2) cost 96 VALU for cfg2's
             // tz = 16, run whenever any of the wave's packets had a ragged end.
             if constexpr (!(ABL & 16))
-                if (lane_k() == 0u) reg = vr_unstep_tz<BIN != 0>(reg, tz, kVrTz);
+                if (lane_k() == 0u) reg = vr_unstep_tz<BIN == 1>(reg, tz, kVrTz);
             if constexpr (VF) {
                 desired = xor_lanes<0>(LG, desired);         // the slot's bytes, from at most two lanes
                 if (lane_k() == 0u && lane_p() < crem) {
@@ -1110,7 +1120,7 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
                     if (cout) cout[lane_p()] = comp;
                 }
             } else if (lane_k() == 0u && lane_p() < crem) {
-                const uint32_t ci = BIN ? lds_load(stash_addr(cgn - 1u)) : lane_p();   // (BIN: the record's index)
+                const uint32_t ci = (BIN && !(ABL & 64)) ? lds_load(stash_addr(cgn - 1u)) : lane_p();   // (BIN: the record's index)
                 cout[ci] = finalize(reg);                                         // packet.cs:159
             }
             if (pdone) {
@@ -1162,12 +1172,17 @@ const void* vring_pick_v(bool trace, const VrVariant& v) {
 #endif
     return nullptr;
 }
-// (diagnostics: abl 2 = no fold lookups, 19 = no masks, lookups or end corrections, at 4 lanes)
-const void* vring_pick_bin(int lg, int dyn, int abl = 0) {
+// compact: BIN = 2 (two workgroups per CU).  (diagnostics: abl 2 = no fold lookups, 19 =
+// no masks, lookups or end corrections, + 64 = CRCs stored in record order, at 4 lanes)
+const void* vring_pick_bin(int lg, int dyn, int abl = 0, bool compact = false) {
+    if (abl == 0 && compact) return lg == 2 ? vring_fn<2, 0, 0, 0, 2>(dyn) : vring_fn<3, 0, 0, 0, 2>(dyn);
     if (abl == 0) return lg == 2 ? vring_fn<2, 0, 0, 0, 1>(dyn) : vring_fn<3, 0, 0, 0, 1>(dyn);
 #ifdef ENET_HIP_DIAG
-    if (lg == 2 && dyn == 0 && abl == 2) return vring_fn<2, 0, 0, 2, 1>();
-    if (lg == 2 && dyn == 0 && abl == 19) return vring_fn<2, 0, 0, 19, 1>();
+    if (lg == 2 && dyn == 0 && abl == 2) return compact ? vring_fn<2, 0, 0, 2, 2>() : vring_fn<2, 0, 0, 2, 1>();
+    if (lg == 2 && dyn == 0 && abl == 19) return compact ? vring_fn<2, 0, 0, 19, 2>() : vring_fn<2, 0, 0, 19, 1>();
+    // 64: the CRCs stored in record order (the scattered out[index] stores priced)
+    if (lg == 2 && dyn == 0 && abl == 64 && !compact) return vring_fn<2, 0, 0, 64, 1>();
+    if (lg == 2 && dyn == 0 && abl == 83 && !compact) return vring_fn<2, 0, 0, 83, 1>();
 #endif
     return nullptr;
 }
@@ -1244,8 +1259,10 @@ int vring_setup() {
             }
         for (int lg = 2; lg <= 3; ++lg) {
             int rc;
-            for (int abl : {0, 2, 19})
+            for (int abl : {0, 2, 19, 64, 83}) {
                 if ((rc = set(vring_pick_bin(lg, d, abl), kVrLdsBin))) return rc;
+                if ((rc = set(vring_pick_bin(lg, d, abl, true), kVrLdsBinC))) return rc;
+            }
             for (int t = 0; t < 2; ++t)
                 for (int nt = 0; nt < 2; ++nt)
                     for (int abl : kAbl)
@@ -1292,13 +1309,14 @@ int vring_launch_list(int lg, int max_wgs, const VrVariant& v, hipStream_t st, c
         grid &= ~1u;
         grid = std::max(grid, 1u);
     }
-    const void* fn = bin ? vring_pick_bin(lg, vring_dyn(w), w.abl) : vring_pick(lg, trace != nullptr, w);
+    const void* fn = bin ? vring_pick_bin(lg, vring_dyn(w), w.abl, w.compact) : vring_pick(lg, trace != nullptr, w);
     if (!fn) return -static_cast<int>(hipErrorInvalidValue);   // a variant this library does not build
     // slots are 32-bit: a workgroup's slot count (rounds x 16) must fit
     if ((a.groups / (static_cast<uint64_t>(grid) * kVrW) + 3u) * kVrW > 0xFFFFFFF0ull)
         return -static_cast<int>(hipErrorInvalidValue);
     void* args[] = {&a, const_cast<KernelTables*>(&tb), const_cast<const uint32_t**>(&basis2), &trace};
-    const hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(64 * kVrW), args, bin ? kVrLdsBin : kVrLds, st);
+    const int lds = bin ? (w.compact ? kVrLdsBinC : kVrLdsBin) : kVrLds;
+    const hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(64 * kVrW), args, lds, st);
     return e == hipSuccess ? 0 : -static_cast<int>(e);
 }
 

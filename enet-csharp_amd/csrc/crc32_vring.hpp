@@ -90,6 +90,8 @@ struct VrVariant {
     // claim points at an array of words, one per pair of workgroups k and k + G / 2
     // (the pair's rounds balance between its two workgroups; G made even)
     int claim_mode = 1;
+    // length-binned records: the compact instance (no x^(-8 c) tables, two workgroups per CU)
+    bool compact = false;
 };
 constexpr int kVrClaimWords = 16;     // 32-bit words: one 64-byte line per launch
 constexpr int kVrPairWords = 512;     // pair rounds: 64-bit words per launch (grids up to 1024)

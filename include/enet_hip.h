@@ -74,8 +74,9 @@ ENET_HIP_API const char* enet_hip_error_string(int code);
  * packet (a power of two; default 8, and 4 for the length-binned entries);
  * workgroups_per_cu (0..8): resident workgroups per CU.  The VGPR-ring kernel runs
  * 1 or 2 (values above 2 mean 2 there; default 2 for a launch of several batches,
- * 1 for a single checksum batch, 2 for receive verify); the direct and gather grids
- * use the value as given. */
+ * 1 for a single checksum batch, 2 for receive verify and for the binned gather's
+ * segment pass -- at 2 the length-binned records run the compact records instance);
+ * the direct and gather-join grids use the value as given. */
 ENET_HIP_API int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgroups_per_cu);
 
 /* Kernel path for the packet batch entry points (0 = default): checksum batches
@@ -401,7 +402,11 @@ ENET_HIP_API int enet_hip_read_probe_device(enet_hip_context* ctx, const uint8_t
  * share a claim word).  1048576 x j, j = 1..7: the gather join without its
  * short-segment fold (bit 0 of j), its multiplies (bit 1), its short-segment loads
  * (bit 2) -- WRONG checksums.  16777216 x (1 + b), b < 48 (correct checksums): the
- * binned gather folds segments of at most b bytes in the join (default 48). */
+ * binned gather folds segments of at most b bytes in the join (default 48).  The
+ * length-binned entry's records instance (4 lanes) takes 4096 (no lookups), 38912 (the
+ * skeleton) and 131072 (CRCs stored in record order, alone or with 38912) -- WRONG
+ * checksums; 2^30 (correct checksums): the binned entry leaves its records in memory
+ * order (no sort). */
 ENET_HIP_API int enet_hip_diag_ablation(enet_hip_context* ctx, int mode);
 
 /* ---- diagnostics: per-wave timeline of the lean stream kernel ----

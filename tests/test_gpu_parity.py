@@ -118,8 +118,8 @@ def test_cfg3_full(ctx, oracle_lib):
         assert (run_batch(ctx, b.payload, b.off, b.lens, lanes) == exp).all(), lanes
 
 
-def run_binned(ctx, payload, off, lens, lanes=0, path=0):
-    ctx.set_tuning(lanes, 0)
+def run_binned(ctx, payload, off, lens, lanes=0, path=0, wgs=0):
+    ctx.set_tuning(lanes, wgs)
     ctx.set_kernel_path(path)
     try:
         n = len(off)
@@ -133,6 +133,7 @@ def run_binned(ctx, payload, off, lens, lanes=0, path=0):
         return out.cpu().numpy().view(np.uint32)
     finally:
         ctx.set_kernel_path(0)
+        ctx.set_tuning(0, 0)
 
 
 BINNED_PATHS = (0, 17)        # 0: the default (the vring kernel's records instance), 17: the vring path itself
@@ -176,6 +177,32 @@ def test_binned_golden_and_edges(ctx, golden, oracle_lib, lanes, path):
     exp = oracle_lib.batch(payload, off, lens, threads=8)
     assert (run_binned(ctx, payload, off, lens, lanes, path) == exp).all()
     assert (run_binned(ctx, payload, off[:1], lens[:1], lanes, path) == exp[:1]).all()
+
+
+@pytest.mark.parametrize("wgs", [1, 2])
+def test_binned_records_instance_per_workgroup_count(ctx, golden, oracle_lib, wgs):
+    """The records instance at one workgroup per CU (its x^(-8 c) tables in LDS) and at
+    two (the compact instance: tz mod 8 by unsteps): cfg3 in full, the golden vectors,
+    every bin with empties and ragged ends, tiny one-stage and long many-stage groups."""
+    b = workloads.cfg3()
+    exp = oracle_lib.batch(b.payload, b.off, b.lens, threads=16)
+    payload, off, lens, exp_g = golden_batch(golden)
+    rng = np.random.default_rng(31 + wgs)
+    n = 20000
+    e_lens = rng.integers(0, 9000, size=n).astype(np.uint32)
+    e_lens[:64] = 0
+    e_lens[64:128] = np.arange(64) * 32 + 31
+    e_off = rng.integers(0, 1 << 20, size=n).astype(np.uint64)
+    e_pay = rng.integers(0, 256, size=(1 << 20) + 9000, dtype=np.uint8)
+    exp_e = oracle_lib.batch(e_pay, e_off, e_lens, threads=8)
+    tiny = workloads.mixed(300_000, 0, 40, seed=281, len_seed=282)
+    exp_t = oracle_lib.batch(tiny.payload, tiny.off, tiny.lens, threads=16)
+    for lanes in (4, 8):
+        assert (run_binned(ctx, b.payload, b.off, b.lens, lanes, 0, wgs) == exp).all(), ("cfg3", lanes)
+        assert (run_binned(ctx, payload, off, lens, lanes, 0, wgs) == exp_g).all(), ("golden", lanes)
+        assert (run_binned(ctx, e_pay, e_off, e_lens, lanes, 0, wgs) == exp_e).all(), ("edges", lanes)
+        assert (run_binned(ctx, e_pay, e_off[:1], e_lens[:1], lanes, 0, wgs) == exp_e[:1]).all(), ("one", lanes)
+        assert (run_binned(ctx, tiny.payload, tiny.off, tiny.lens, lanes, 0, wgs) == exp_t).all(), ("tiny", lanes)
 
 
 def test_binned_records_are_a_length_ordered_permutation(ctx, oracle_lib):

@@ -71,12 +71,19 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
+    // packet launches read at d + region: consecutive launches rotate over `nreg` copies
+    // of the packet span (set below), so a span smaller than the 256 MB MALL is read cold
+    uint64_t region = 0, span = bytes, nreg = 1;
     auto timeit = [&](auto fn, double B, const char* what) {
         for (int r = 0; r < 3; ++r) fn();
         hipDeviceSynchronize();
         hipEventRecord(e0);
         const int reps = 20;
-        for (int r = 0; r < reps; ++r) fn();
+        for (int r = 0; r < reps; ++r) {
+            region = (r % nreg) * span;
+            fn();
+        }
+        region = 0;
         hipEventRecord(e1);
         hipEventSynchronize(e1);
         float ms = 0;
@@ -101,6 +108,10 @@ int main(int argc, char** argv) {
         tot += len[j];
     }
     if (tot + 256 > bytes) return 1;
+    span = (tot + 256 + 4095) / 4096 * 4096;
+    nreg = bytes / span;
+    printf("%llu packets, %.1f MB, %llu rotating copies\n", static_cast<unsigned long long>(n), tot / 1e6,
+           static_cast<unsigned long long>(nreg));
     std::vector<uint64_t> wa(n), we(n);
     std::vector<uint32_t> na(n), ne(n);
     uint64_t off = 64;
@@ -120,18 +131,18 @@ int main(int argc, char** argv) {
     for (int v = 0; v < 2; ++v) {
         hipMemcpy(dw, v ? we.data() : wa.data(), 8 * n, hipMemcpyHostToDevice);
         hipMemcpy(dn, v ? ne.data() : na.data(), 4 * n, hipMemcpyHostToDevice);
-        timeit([&] { hipLaunchKernelGGL(ap_packets<4>, dim3(256 * 4), dim3(256), 0, 0, d, dw, dn, n, sink); },
+        timeit([&] { hipLaunchKernelGGL(ap_packets<4>, dim3(256 * 4), dim3(256), 0, 0, d + region, dw, dn, n, sink); },
                static_cast<double>(tot),
                v ? "packets (4 lanes, 16/wave), windows ending on packet ends" : "packets (4 lanes, 16/wave), 64-B aligned windows");
     }
     // lanes per packet, 64-B aligned windows (packets in memory order: neighbours share lines)
     hipMemcpy(dw, wa.data(), 8 * n, hipMemcpyHostToDevice);
     hipMemcpy(dn, na.data(), 4 * n, hipMemcpyHostToDevice);
-    timeit([&] { hipLaunchKernelGGL(ap_packets<1>, dim3(256 * 4), dim3(256), 0, 0, d, dw, dn, n, sink); },
+    timeit([&] { hipLaunchKernelGGL(ap_packets<1>, dim3(256 * 4), dim3(256), 0, 0, d + region, dw, dn, n, sink); },
            static_cast<double>(tot), "packets (1 lane, 64/wave), 64-B aligned windows");
-    timeit([&] { hipLaunchKernelGGL(ap_packets<2>, dim3(256 * 4), dim3(256), 0, 0, d, dw, dn, n, sink); },
+    timeit([&] { hipLaunchKernelGGL(ap_packets<2>, dim3(256 * 4), dim3(256), 0, 0, d + region, dw, dn, n, sink); },
            static_cast<double>(tot), "packets (2 lanes, 32/wave), 64-B aligned windows");
-    timeit([&] { hipLaunchKernelGGL(ap_packets<8>, dim3(256 * 4), dim3(256), 0, 0, d, dw, dn, n, sink); },
+    timeit([&] { hipLaunchKernelGGL(ap_packets<8>, dim3(256 * 4), dim3(256), 0, 0, d + region, dw, dn, n, sink); },
            static_cast<double>(tot), "packets (8 lanes, 8/wave), 64-B aligned windows");
     // the same in a shuffled packet order (binned records: neighbours in other groups)
     {
@@ -146,11 +157,11 @@ int main(int argc, char** argv) {
         }
         hipMemcpy(dw, ws2.data(), 8 * n, hipMemcpyHostToDevice);
         hipMemcpy(dn, ns2.data(), 4 * n, hipMemcpyHostToDevice);
-        timeit([&] { hipLaunchKernelGGL(ap_packets<2>, dim3(256 * 4), dim3(256), 0, 0, d, dw, dn, n, sink); },
+        timeit([&] { hipLaunchKernelGGL(ap_packets<2>, dim3(256 * 4), dim3(256), 0, 0, d + region, dw, dn, n, sink); },
                static_cast<double>(tot), "shuffled packets, 2 lanes");
-        timeit([&] { hipLaunchKernelGGL(ap_packets<4>, dim3(256 * 4), dim3(256), 0, 0, d, dw, dn, n, sink); },
+        timeit([&] { hipLaunchKernelGGL(ap_packets<4>, dim3(256 * 4), dim3(256), 0, 0, d + region, dw, dn, n, sink); },
                static_cast<double>(tot), "shuffled packets, 4 lanes");
-        timeit([&] { hipLaunchKernelGGL(ap_packets<8>, dim3(256 * 4), dim3(256), 0, 0, d, dw, dn, n, sink); },
+        timeit([&] { hipLaunchKernelGGL(ap_packets<8>, dim3(256 * 4), dim3(256), 0, 0, d + region, dw, dn, n, sink); },
                static_cast<double>(tot), "shuffled packets, 8 lanes");
     }
     // the binned records' order (crc32_lean.hip bin_tile_kernel): each tile of `tile`
@@ -176,7 +187,7 @@ int main(int argc, char** argv) {
             char name[96];
             snprintf(name, sizeof name, "binned order, 4 lanes, tile %llu, %s", static_cast<unsigned long long>(tile),
                      inter ? "rank-interleaved" : "tile-local");
-            timeit([&] { hipLaunchKernelGGL(ap_packets<4>, dim3(256 * 4), dim3(256), 0, 0, d, dw, dn, n, sink); },
+            timeit([&] { hipLaunchKernelGGL(ap_packets<4>, dim3(256 * 4), dim3(256), 0, 0, d + region, dw, dn, n, sink); },
                    static_cast<double>(tot), name);
         }
     }

@@ -69,6 +69,7 @@ def main():
     ap.add_argument("--messages", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--lanes", type=int, default=0)
+    ap.add_argument("--wgs", type=int, default=0, help="workgroups per CU (enet_hip_set_tuning; 0 = default)")
     ap.add_argument("--path", type=int, default=0, help="kernel path (enet_hip_set_kernel_path; 17 = vring records)")
     ap.add_argument("--only", choices=["gather", "gather_binned"], help="time one entry only")
     ap.add_argument("--ablate", type=int, default=0, help="diagnostics: enet_hip_diag_ablation after the oracle "
@@ -85,7 +86,7 @@ def main():
     from enethip import workloads
     import oracle as orc
     g = workloads.cfg5(a.messages)
-    ctx = enethip.Context(0, a.lanes, 0, diag=a.path not in (0, 1, 2, 13, 17) or a.ablate != 0)
+    ctx = enethip.Context(0, a.lanes, a.wgs, diag=a.path not in (0, 1, 2, 13, 17) or a.ablate != 0)
     if a.path:
         ctx.set_kernel_path(a.path)
     st = torch.cuda.Stream()
