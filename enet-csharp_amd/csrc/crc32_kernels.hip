@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -1947,16 +1948,25 @@ static int range_coder_call(enet_hip_context* ctx, bool decompress, const uint8_
     std::lock_guard<std::mutex> lk(ctx->mu);
     ENH_CHECK(hipSetDevice(ctx->device));
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-    // one lane per DGRAM, at most 4 waves per CU in flight (the models are HBM scratch)
-    const uint64_t threads = std::min<uint64_t>(count, static_cast<uint64_t>(ctx->num_cus) * 256u);
-    const size_t need = ((threads + 63) / 64) * 64 * kRangeModelBytes;
+    // one lane per DGRAM, 16 per wave, at most 16 waves per CU: 65 536 DGRAMs in flight,
+    // as many as 4 full waves per CU had, with a quarter of the stragglers per wave
+    // (1.30-1.36 against 1.05 GB/s on tools/rc_bench.py, profiles/r04_range_coder/);
+    // the models are HBM scratch, kRangeModelBytes per lane
+    uint32_t lanes = 16, waves = 16;
+#ifdef ENET_HIP_DIAG
+    if (const char* e = getenv("ENET_HIP_RC_LANES")) lanes = static_cast<uint32_t>(atoi(e));
+    if (const char* e = getenv("ENET_HIP_RC_WAVES")) waves = static_cast<uint32_t>(atoi(e));
+    if (lanes == 0 || lanes > 64 || waves == 0 || waves > 32) return -static_cast<int>(hipErrorInvalidValue);
+#endif
+    const uint64_t threads = std::min<uint64_t>(count, static_cast<uint64_t>(ctx->num_cus) * waves * lanes);
+    const size_t need = ((threads + lanes - 1) / lanes) * lanes * kRangeModelBytes;
     if (need > ctx->d_rc_scratch_cap) {
         ENH_CHECK(hipStreamSynchronize(st));
         int rc;
         if ((rc = ensure(&ctx->d_rc_scratch, &ctx->d_rc_scratch_cap, need))) return rc;
     }
     RangeArgs a{in, inOffsets, inLengths, count, out, outOffsets, outLimits, outLengths, ctx->d_rc_scratch};
-    return range_coder_launch(decompress, a, threads, st);
+    return range_coder_launch(decompress, a, threads, lanes, st);
 }
 
 int enet_hip_range_compress_device(enet_hip_context* ctx, const uint8_t* in, const uint64_t* inOffsets,

@@ -391,10 +391,14 @@ __device__ uint32_t decompress_one(Model& m, const uint8_t* in, uint32_t n, uint
     return static_cast<uint32_t>(o - out);
 }
 
+// `lanes` active lanes per wave: a wave runs its lanes' byte loops in lock step, so a
+// byte costs the wave its slowest lane's tree walk; fewer lanes per wave (more waves)
+// wait on fewer stragglers.
 template <bool DECOMPRESS>
-__global__ void __launch_bounds__(64) range_coder_kernel(RangeArgs a) {
-    const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+__global__ void __launch_bounds__(64) range_coder_kernel(RangeArgs a, uint32_t lanes) {
+    if (threadIdx.x >= lanes) return;
+    const uint64_t t = static_cast<uint64_t>(blockIdx.x) * lanes + threadIdx.x;
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * lanes;
     Model m;
     m.s = reinterpret_cast<RSym*>(a.scratch) + t * kRangeSymbols;
     m.next = 0;
@@ -408,11 +412,13 @@ __global__ void __launch_bounds__(64) range_coder_kernel(RangeArgs a) {
 
 }  // namespace
 
-int range_coder_launch(bool decompress, const RangeArgs& a, uint64_t threads, hipStream_t st) {
+int range_coder_launch(bool decompress, const RangeArgs& a, uint64_t threads, uint32_t lanes, hipStream_t st) {
     if (a.n == 0) return 0;
-    const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(1, (std::min<uint64_t>(threads, a.n) + 63) / 64));
-    if (decompress) hipLaunchKernelGGL(range_coder_kernel<true>, dim3(grid), dim3(64), 0, st, a);
-    else hipLaunchKernelGGL(range_coder_kernel<false>, dim3(grid), dim3(64), 0, st, a);
+    if (lanes == 0 || lanes > 64) return -static_cast<int>(hipErrorInvalidValue);
+    const unsigned grid =
+        static_cast<unsigned>(std::max<uint64_t>(1, (std::min<uint64_t>(threads, a.n) + lanes - 1) / lanes));
+    if (decompress) hipLaunchKernelGGL(range_coder_kernel<true>, dim3(grid), dim3(64), 0, st, a, lanes);
+    else hipLaunchKernelGGL(range_coder_kernel<false>, dim3(grid), dim3(64), 0, st, a, lanes);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : -static_cast<int>(e);
 }

@@ -21,7 +21,8 @@ struct RangeArgs {
     uint8_t* scratch;            // kRangeModelBytes per thread
 };
 
-// threads = lanes launched (each needs kRangeModelBytes of scratch)
-int range_coder_launch(bool decompress, const RangeArgs& a, uint64_t threads, hipStream_t st);
+// threads = DGRAM lanes launched (each needs kRangeModelBytes of scratch), `lanes` of
+// them per 64-wide wave (1..64: fewer active lanes per wave, less divergence)
+int range_coder_launch(bool decompress, const RangeArgs& a, uint64_t threads, uint32_t lanes, hipStream_t st);
 
 }  // namespace enethip

@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 import oracle
-from test_gpu_parity import ctx, dev  # noqa: F401  (fixture)
+from test_gpu_parity import ctx, dctx, dev  # noqa: F401  (fixtures)
 from test_range_coder import corpus, pack
 
 pytestmark = pytest.mark.gpu
@@ -57,3 +57,22 @@ def test_decompress_matches_oracle_long(ctx, oracle_lib):  # noqa: F811
     assert (glen == rlen).all() and (rlen == lens).all()
     for i in range(len(msgs)):
         assert (got[int(goff[i]):int(goff[i]) + int(glen[i])] == msgs[i]).all(), i
+
+
+@pytest.mark.parametrize("lanes,waves", [(64, 4), (16, 16), (3, 2), (1, 1)])
+def test_compress_lanes_per_wave(dctx, oracle_lib, monkeypatch, lanes, waves):  # noqa: F811
+    """Any number of active lanes per wave and waves per CU (diagnostics knobs
+    ENET_HIP_RC_LANES / _WAVES; 16 x 16 is the product's): the same bytes as the
+    oracle, including DGRAMs taken on a lane's later grid-stride turns (3 x 2 and
+    1 x 1 launch fewer lanes than the 3000 DGRAMs)."""
+    monkeypatch.setenv("ENET_HIP_RC_LANES", str(lanes))
+    monkeypatch.setenv("ENET_HIP_RC_WAVES", str(waves))
+    msgs = corpus(3000, seed=9) + [np.zeros(0, np.uint8)]
+    data, off, lens = pack(msgs)
+    limit = lens * 2 + 64
+    ref, roff, rlen = oracle.range_coder_batch(oracle_lib, False, data, off, lens, limit)
+    got, goff, glen = gpu_coder(dctx, False, data, off, lens, limit)
+    assert (glen == rlen).all()
+    for i in range(len(msgs)):
+        a, b = int(roff[i]), int(goff[i])
+        assert (got[b:b + int(glen[i])] == ref[a:a + int(rlen[i])]).all(), i

@@ -23,6 +23,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--packets", type=int, default=65536)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--sweep", default="", help="diagnostics: LANES:WAVES,... lanes per wave x waves per CU "
+                                                  "(ENET_HIP_RC_LANES / _WAVES, libenethip_diag.so); each "
+                                                  "config's compressed bytes are checked against the first's")
     a = ap.parse_args()
     import torch
     import enethip
@@ -32,7 +35,7 @@ def main():
     data, off, lens = pack(msgs)
     limit = lens * 2 + 64
     lo = np.concatenate([[0], np.cumsum(limit.astype(np.uint64))[:-1]]).astype(np.uint64)
-    ctx = enethip.Context(0)
+    ctx = enethip.Context(0, diag=bool(a.sweep))
     t = lambda x, dt: torch.from_numpy(np.ascontiguousarray(x).view(dt)).cuda()  # noqa: E731
     d_in, d_off, d_len = t(np.concatenate([data, np.zeros(16, np.uint8)]), np.uint8), t(off, np.int64), t(lens, np.int32)
     d_c = torch.zeros(int(limit.astype(np.uint64).sum()) + 16, dtype=torch.uint8, device="cuda")
@@ -54,21 +57,44 @@ def main():
             ts.append(e0.elapsed_time(e1) * 1e-3)
         return float(np.median(ts))
 
-    tc = timed(lambda: ctx.range_coder_device(False, d_in, d_off, d_len, len(off), d_c, d_lo, d_lim, d_clen,
-                                              stream=s.cuda_stream))
-    # decompress the compressed streams in place (each at its own output slot)
-    td = timed(lambda: ctx.range_coder_device(True, d_c, d_lo, d_clen, len(off), d_d, d_lo, d_lim, d_dlen,
-                                              stream=s.cuda_stream))
-    clen = d_clen.cpu().numpy().view(np.uint32)
-    dd = d_d.cpu().numpy()
-    dlen = d_dlen.cpu().numpy().view(np.uint32)
-    ok = bool((dlen == lens).all() and all((dd[int(lo[i]):int(lo[i]) + len(m)] == m).all() for i, m in enumerate(msgs)))
+    nbytes = float(lens.astype(np.uint64).sum())
+
+    def run_once():
+        tc = timed(lambda: ctx.range_coder_device(False, d_in, d_off, d_len, len(off), d_c, d_lo, d_lim, d_clen,
+                                                  stream=s.cuda_stream))
+        # decompress the compressed streams in place (each at its own output slot)
+        td = timed(lambda: ctx.range_coder_device(True, d_c, d_lo, d_clen, len(off), d_d, d_lo, d_lim, d_dlen,
+                                                  stream=s.cuda_stream))
+        clen = d_clen.cpu().numpy().view(np.uint32)
+        dd = d_d.cpu().numpy()
+        dlen = d_dlen.cpu().numpy().view(np.uint32)
+        ok = bool((dlen == lens).all() and all((dd[int(lo[i]):int(lo[i]) + len(m)] == m).all() for i, m in enumerate(msgs)))
+        return {"tc": tc, "td": td, "clen": clen, "ok": ok}
+
+    if a.sweep:
+        first = None
+        for cfg in a.sweep.split(","):
+            lanes, waves = cfg.split(":")
+            os.environ["ENET_HIP_RC_LANES"], os.environ["ENET_HIP_RC_WAVES"] = lanes, waves
+            d_c.zero_()
+            d_d.zero_()
+            r = run_once()
+            comp = (d_c.cpu().numpy().tobytes(), r["clen"].tobytes())
+            first = first or comp
+            print(json.dumps({"lanes_per_wave": int(lanes), "waves_per_cu": int(waves),
+                              "compress_us": round(r["tc"] * 1e6, 1), "decompress_us": round(r["td"] * 1e6, 1),
+                              "compress_GBps": round(nbytes / r["tc"] / 1e9, 3),
+                              "decompress_GBps": round(nbytes / r["td"] / 1e9, 3),
+                              "round_trip_ok": r["ok"], "same_bytes_as_first": comp == first}), flush=True)
+        ctx.close()
+        return
+    r = run_once()
+    tc, td, clen, ok = r["tc"], r["td"], r["clen"], r["ok"]
     lib = oracle.OracleLib()
     sub = min(len(off), 4096)
     t0 = time.perf_counter()
     oracle.range_coder_batch(lib, False, data, off[:sub], lens[:sub], limit[:sub])
     cpu = float(lens[:sub].astype(np.uint64).sum()) / (time.perf_counter() - t0)
-    nbytes = float(lens.astype(np.uint64).sum())
     print(json.dumps({"packets": len(off), "input_bytes": int(nbytes), "ratio": round(float(clen.sum()) / nbytes, 4),
                       "compress_us": round(tc * 1e6, 1), "compress_GBps": round(nbytes / tc / 1e9, 3),
                       "decompress_us": round(td * 1e6, 1), "decompress_GBps": round(nbytes / td / 1e9, 3),
