@@ -1957,6 +1957,10 @@ static int range_coder_call(enet_hip_context* ctx, bool decompress, const uint8_
     if (const char* e = getenv("ENET_HIP_RC_LANES")) lanes = static_cast<uint32_t>(atoi(e));
     if (const char* e = getenv("ENET_HIP_RC_WAVES")) waves = static_cast<uint32_t>(atoi(e));
     if (lanes == 0 || lanes > 64 || waves == 0 || waves > 32) return -static_cast<int>(hipErrorInvalidValue);
+    const char* il = getenv("ENET_HIP_RC_INTERLEAVE");
+    const uint32_t interleave = il ? static_cast<uint32_t>(atoi(il) != 0) : 0u;
+#else
+    const uint32_t interleave = 0;
 #endif
     const uint64_t threads = std::min<uint64_t>(count, static_cast<uint64_t>(ctx->num_cus) * waves * lanes);
     const size_t need = ((threads + lanes - 1) / lanes) * lanes * kRangeModelBytes;
@@ -1965,7 +1969,7 @@ static int range_coder_call(enet_hip_context* ctx, bool decompress, const uint8_
         int rc;
         if ((rc = ensure(&ctx->d_rc_scratch, &ctx->d_rc_scratch_cap, need))) return rc;
     }
-    RangeArgs a{in, inOffsets, inLengths, count, out, outOffsets, outLimits, outLengths, ctx->d_rc_scratch};
+    RangeArgs a{in, inOffsets, inLengths, count, out, outOffsets, outLimits, outLengths, ctx->d_rc_scratch, interleave};
     return range_coder_launch(decompress, a, threads, lanes, st);
 }
 

@@ -33,8 +33,10 @@ struct RSym {
 static_assert(sizeof(RSym) == 16, "ENetSymbol is 16 bytes");
 
 struct Model {
-    RSym* s;         // kRangeSymbols symbols of this lane
+    RSym* s;         // symbol 0 of this lane's kRangeSymbols
     uint32_t next;   // nextSymbol
+    uint32_t stride; // symbols between this lane's consecutive symbols (1, or the lanes of the wave)
+    __device__ __forceinline__ RSym& at(uint32_t i) const { return s[static_cast<size_t>(i) * stride]; }
 };
 
 __device__ __forceinline__ uint16_t add_symbol(Model& m, uint8_t value, uint8_t count) {
@@ -44,15 +46,15 @@ __device__ __forceinline__ uint16_t add_symbol(Model& m, uint8_t value, uint8_t 
     y.count = count;
     y.under = count;
     y.left = y.right = y.symbols = y.escapes = y.total = y.parent = 0;
-    m.s[i] = y;
+    m.at(i) = y;
     return i;
 }
 
 __device__ __forceinline__ uint16_t reset_model(Model& m) {
     m.next = 0;
     const uint16_t r = add_symbol(m, 0, 0);
-    m.s[r].escapes = kCtxEscapeMin;
-    m.s[r].total = static_cast<uint16_t>(kCtxEscapeMin + 256 * kCtxSymbolMin);
+    m.at(r).escapes = kCtxEscapeMin;
+    m.at(r).total = static_cast<uint16_t>(kCtxEscapeMin + 256 * kCtxSymbolMin);
     return r;
 }
 
@@ -63,7 +65,7 @@ __device__ uint16_t rescale_tree(Model& m, uint16_t i) {
     int sp = 0;
     uint16_t total = 0;
     for (;;) {
-        RSym& y = m.s[i];
+        RSym& y = m.at(i);
         y.count = static_cast<uint8_t>(y.count - (y.count >> 1));
         y.under = y.count;
         if (y.left && sp < 256) {                           // descend: rescale the left subtree first
@@ -75,7 +77,7 @@ __device__ uint16_t rescale_tree(Model& m, uint16_t i) {
             continue;
         }
         for (;;) {                                          // node i done: add it, go right or return
-            RSym& z = m.s[i];
+            RSym& z = m.at(i);
             total = static_cast<uint16_t>(total + z.under);
             if (z.right) {
                 i = static_cast<uint16_t>(i + z.right);
@@ -84,7 +86,7 @@ __device__ uint16_t rescale_tree(Model& m, uint16_t i) {
             if (sp == 0) return total;
             --sp;                                           // a left subtree finished: its parent's under
             const uint16_t p = st_node[sp];
-            m.s[p].under = static_cast<uint16_t>(m.s[p].under + total);
+            m.at(p).under = static_cast<uint16_t>(m.at(p).under + total);
             total = st_total[sp];
             i = p;
         }
@@ -92,9 +94,9 @@ __device__ uint16_t rescale_tree(Model& m, uint16_t i) {
 }
 
 __device__ __forceinline__ void rescale_context(Model& m, uint16_t ctx, uint32_t minimum) {
-    RSym& x = m.s[ctx];
+    RSym& x = m.at(ctx);
     const uint16_t t = x.symbols ? rescale_tree(m, static_cast<uint16_t>(ctx + x.symbols)) : 0;
-    RSym& x2 = m.s[ctx];
+    RSym& x2 = m.at(ctx);
     x2.escapes = static_cast<uint16_t>(x2.escapes - (x2.escapes >> 1));
     x2.total = static_cast<uint16_t>(t + x2.escapes + 256 * minimum);
 }
@@ -104,22 +106,22 @@ __device__ uint16_t tree_encode(Model& m, uint16_t ctx, uint8_t value, uint16_t&
                                 uint32_t delta, uint32_t minimum) {
     under = static_cast<uint16_t>(value * minimum);
     count = static_cast<uint16_t>(minimum);
-    if (!m.s[ctx].symbols) {
+    if (!m.at(ctx).symbols) {
         const uint16_t y = add_symbol(m, value, static_cast<uint8_t>(delta));
-        m.s[ctx].symbols = static_cast<uint16_t>(y - ctx);
+        m.at(ctx).symbols = static_cast<uint16_t>(y - ctx);
         return y;
     }
-    uint16_t node = static_cast<uint16_t>(ctx + m.s[ctx].symbols);
+    uint16_t node = static_cast<uint16_t>(ctx + m.at(ctx).symbols);
     for (;;) {
-        RSym n = m.s[node];
+        RSym n = m.at(node);
         if (value < n.value) {
-            m.s[node].under = static_cast<uint16_t>(n.under + delta);
+            m.at(node).under = static_cast<uint16_t>(n.under + delta);
             if (n.left) {
                 node = static_cast<uint16_t>(node + n.left);
                 continue;
             }
             const uint16_t y = add_symbol(m, value, static_cast<uint8_t>(delta));
-            m.s[node].left = static_cast<uint16_t>(y - node);
+            m.at(node).left = static_cast<uint16_t>(y - node);
             return y;
         }
         if (value > n.value) {
@@ -129,13 +131,13 @@ __device__ uint16_t tree_encode(Model& m, uint16_t ctx, uint8_t value, uint16_t&
                 continue;
             }
             const uint16_t y = add_symbol(m, value, static_cast<uint8_t>(delta));
-            m.s[node].right = static_cast<uint16_t>(y - node);
+            m.at(node).right = static_cast<uint16_t>(y - node);
             return y;
         }
         count = static_cast<uint16_t>(count + n.count);
         under = static_cast<uint16_t>(under + n.under - n.count);
-        m.s[node].under = static_cast<uint16_t>(n.under + delta);
-        m.s[node].count = static_cast<uint8_t>(n.count + delta);
+        m.at(node).under = static_cast<uint16_t>(n.under + delta);
+        m.at(node).count = static_cast<uint8_t>(n.count + delta);
         return node;
     }
 }
@@ -146,17 +148,17 @@ __device__ int tree_decode(Model& m, uint16_t ctx, uint16_t code, uint8_t& value
                            uint32_t delta, uint32_t minimum, bool create) {
     under = 0;
     count = static_cast<uint16_t>(minimum);
-    if (!m.s[ctx].symbols) {
+    if (!m.at(ctx).symbols) {
         if (!create) return -1;
         value = static_cast<uint8_t>(code / minimum);
         under = static_cast<uint16_t>(code - code % minimum);
         const uint16_t y = add_symbol(m, value, static_cast<uint8_t>(delta));
-        m.s[ctx].symbols = static_cast<uint16_t>(y - ctx);
+        m.at(ctx).symbols = static_cast<uint16_t>(y - ctx);
         return y;
     }
-    uint16_t node = static_cast<uint16_t>(ctx + m.s[ctx].symbols);
+    uint16_t node = static_cast<uint16_t>(ctx + m.at(ctx).symbols);
     for (;;) {
-        RSym n = m.s[node];
+        RSym n = m.at(node);
         const uint16_t after = static_cast<uint16_t>(under + n.under + (n.value + 1) * minimum);
         const uint16_t before = static_cast<uint16_t>(n.count + minimum);
         if (code >= after) {
@@ -169,11 +171,11 @@ __device__ int tree_decode(Model& m, uint16_t ctx, uint16_t code, uint8_t& value
             value = static_cast<uint8_t>(n.value + 1 + (code - after) / minimum);
             under = static_cast<uint16_t>(code - (code - after) % minimum);
             const uint16_t y = add_symbol(m, value, static_cast<uint8_t>(delta));
-            m.s[node].right = static_cast<uint16_t>(y - node);
+            m.at(node).right = static_cast<uint16_t>(y - node);
             return y;
         }
         if (static_cast<int>(code) < static_cast<int>(after) - static_cast<int>(before)) {
-            m.s[node].under = static_cast<uint16_t>(n.under + delta);
+            m.at(node).under = static_cast<uint16_t>(n.under + delta);
             if (n.left) {
                 node = static_cast<uint16_t>(node + n.left);
                 continue;
@@ -183,14 +185,14 @@ __device__ int tree_decode(Model& m, uint16_t ctx, uint16_t code, uint8_t& value
             value = static_cast<uint8_t>(n.value - 1 - gap / static_cast<int>(minimum));
             under = static_cast<uint16_t>(code - gap % static_cast<int>(minimum));
             const uint16_t y = add_symbol(m, value, static_cast<uint8_t>(delta));
-            m.s[node].left = static_cast<uint16_t>(y - node);
+            m.at(node).left = static_cast<uint16_t>(y - node);
             return y;
         }
         value = n.value;
         count = static_cast<uint16_t>(count + n.count);
         under = static_cast<uint16_t>(after - before);
-        m.s[node].under = static_cast<uint16_t>(n.under + delta);
-        m.s[node].count = static_cast<uint8_t>(n.count + delta);
+        m.at(node).under = static_cast<uint16_t>(n.under + delta);
+        m.at(node).count = static_cast<uint8_t>(n.count + delta);
         return node;
     }
 }
@@ -237,9 +239,9 @@ __device__ uint32_t compress_one(Model& m, const uint8_t* in, uint32_t n, uint8_
         for (uint16_t sub = predicted; sub != root;) {
             sym = tree_encode(m, sub, value, under, count, kSubSymbolDelta, 0);
             if (parent < 0) predicted = sym;
-            else m.s[parent].parent = sym;
+            else m.at(parent).parent = sym;
             parent = sym;
-            RSym& x = m.s[sub];
+            RSym& x = m.at(sub);
             total = x.total;
             if (count > 0) {
                 e.put(static_cast<uint32_t>(x.escapes) + under, count, total);
@@ -255,20 +257,20 @@ __device__ uint32_t compress_one(Model& m, const uint8_t* in, uint32_t n, uint8_
                 coded = true;
                 break;
             }
-            sub = m.s[sub].parent;
+            sub = m.at(sub).parent;
         }
         if (!coded) {
             sym = tree_encode(m, root, value, under, count, kCtxSymbolDelta, kCtxSymbolMin);
             if (parent < 0) predicted = sym;
-            else m.s[parent].parent = sym;
-            RSym& r = m.s[root];
+            else m.at(parent).parent = sym;
+            RSym& r = m.at(root);
             e.put(static_cast<uint32_t>(r.escapes) + under, count, r.total);
             if (e.fail) return 0;
             r.total = static_cast<uint16_t>(r.total + kCtxSymbolDelta);
             if (count > 0xFF - 2 * kCtxSymbolDelta + kCtxSymbolMin || r.total > kBottom - 0x100)
                 rescale_context(m, root, kCtxSymbolMin);
         }
-        if (order >= kSubOrder) predicted = m.s[predicted].parent;   // nextInput (411-443)
+        if (order >= kSubOrder) predicted = m.at(predicted).parent;   // nextInput (411-443)
         else ++order;
         if (m.next >= kRangeSymbols - kSubOrder) {
             root = reset_model(m);
@@ -323,8 +325,8 @@ __device__ uint32_t decompress_one(Model& m, const uint8_t* in, uint32_t n, uint
         int parent = -1;
         uint16_t sub = predicted;
         bool found = false;
-        for (; sub != root; sub = m.s[sub].parent) {
-            const RSym x = m.s[sub];
+        for (; sub != root; sub = m.at(sub).parent) {
+            const RSym x = m.at(sub);
             if (x.escapes <= 0) continue;
             const uint16_t total = x.total;
             if (x.escapes >= total) continue;
@@ -337,7 +339,7 @@ __device__ uint32_t decompress_one(Model& m, const uint8_t* in, uint32_t n, uint
             const int sym = tree_decode(m, sub, code, value, under, count, kSubSymbolDelta, 0, false);
             if (sym < 0) return 0;
             bottom = static_cast<uint16_t>(sym);
-            RSym& xs = m.s[sub];
+            RSym& xs = m.at(sub);
             d.update(static_cast<uint32_t>(xs.escapes) + under, count);
             xs.total = static_cast<uint16_t>(xs.total + kSubSymbolDelta);
             if (count > 0xFF - 2 * kSubSymbolDelta || xs.total > kBottom - 0x100) rescale_context(m, sub, 0);
@@ -345,7 +347,7 @@ __device__ uint32_t decompress_one(Model& m, const uint8_t* in, uint32_t n, uint
             break;
         }
         if (!found) {
-            const RSym r = m.s[root];
+            const RSym r = m.at(root);
             code = static_cast<uint16_t>((d.code - d.low) / (d.range /= r.total));
             if (code < r.escapes) {
                 d.update(0, r.escapes);
@@ -354,7 +356,7 @@ __device__ uint32_t decompress_one(Model& m, const uint8_t* in, uint32_t n, uint
             code = static_cast<uint16_t>(code - r.escapes);
             bottom = static_cast<uint16_t>(
                 tree_decode(m, root, code, value, under, count, kCtxSymbolDelta, kCtxSymbolMin, true));
-            RSym& rr = m.s[root];
+            RSym& rr = m.at(root);
             d.update(static_cast<uint32_t>(rr.escapes) + under, count);
             rr.total = static_cast<uint16_t>(rr.total + kCtxSymbolDelta);
             if (count > 0xFF - 2 * kCtxSymbolDelta + kCtxSymbolMin || rr.total > kBottom - 0x100)
@@ -362,13 +364,13 @@ __device__ uint32_t decompress_one(Model& m, const uint8_t* in, uint32_t n, uint
             sub = root;
         }
         // patchContexts (789-898): the contexts passed over learn `value`
-        for (uint16_t patch = predicted; patch != sub; patch = m.s[patch].parent) {
+        for (uint16_t patch = predicted; patch != sub; patch = m.at(patch).parent) {
             uint16_t pu, pc;
             const uint16_t y = tree_encode(m, patch, value, pu, pc, kSubSymbolDelta, 0);
             if (parent < 0) predicted = y;
-            else m.s[parent].parent = y;
+            else m.at(parent).parent = y;
             parent = y;
-            RSym& p = m.s[patch];
+            RSym& p = m.at(patch);
             if (pc <= 0) {
                 p.escapes = static_cast<uint16_t>(p.escapes + kSubEscapeDelta);
                 p.total = static_cast<uint16_t>(p.total + kSubEscapeDelta);
@@ -377,10 +379,10 @@ __device__ uint32_t decompress_one(Model& m, const uint8_t* in, uint32_t n, uint
             if (pc > 0xFF - 2 * kSubSymbolDelta || p.total > kBottom - 0x100) rescale_context(m, patch, 0);
         }
         if (parent < 0) predicted = bottom;
-        else m.s[parent].parent = bottom;
+        else m.at(parent).parent = bottom;
         if (o >= oend) return 0;
         *o++ = value;
-        if (order >= kSubOrder) predicted = m.s[predicted].parent;
+        if (order >= kSubOrder) predicted = m.at(predicted).parent;
         else ++order;
         if (m.next >= kRangeSymbols - kSubOrder) {
             root = reset_model(m);
@@ -400,7 +402,12 @@ __global__ void __launch_bounds__(64) range_coder_kernel(RangeArgs a, uint32_t l
     const uint64_t t = static_cast<uint64_t>(blockIdx.x) * lanes + threadIdx.x;
     const uint64_t stride = static_cast<uint64_t>(gridDim.x) * lanes;
     Model m;
-    m.s = reinterpret_cast<RSym*>(a.scratch) + t * kRangeSymbols;
+    // the wave's models: lane-major (each lane's symbols contiguous) or symbol-major
+    // (symbol i of the wave's lanes side by side: the lanes' recent symbols share lines)
+    RSym* const sc = reinterpret_cast<RSym*>(a.scratch);
+    m.s = a.interleave ? sc + static_cast<uint64_t>(blockIdx.x) * lanes * kRangeSymbols + threadIdx.x
+                       : sc + t * kRangeSymbols;
+    m.stride = a.interleave ? lanes : 1u;
     m.next = 0;
     for (uint64_t i = t; i < a.n; i += stride) {
         const uint8_t* in = a.in + a.in_off[i];

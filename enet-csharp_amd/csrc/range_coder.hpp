@@ -19,6 +19,7 @@ struct RangeArgs {
     const uint32_t* out_limit;
     uint32_t* out_len;           // bytes written, 0 = did not fit / corrupt input
     uint8_t* scratch;            // kRangeModelBytes per thread
+    uint32_t interleave = 0;     // 1: a wave's models symbol-major (symbol i of its lanes adjacent)
 };
 
 // threads = DGRAM lanes launched (each needs kRangeModelBytes of scratch), `lanes` of

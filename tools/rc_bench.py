@@ -23,8 +23,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--packets", type=int, default=65536)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--sweep", default="", help="diagnostics: LANES:WAVES,... lanes per wave x waves per CU "
-                                                  "(ENET_HIP_RC_LANES / _WAVES, libenethip_diag.so); each "
+    ap.add_argument("--sweep", default="", help="diagnostics: LANES:WAVES[:1],... lanes per wave x waves per CU "
+                                                  "[x symbol-major models] (ENET_HIP_RC_LANES / _WAVES / "
+                                                  "_INTERLEAVE, libenethip_diag.so); each "
                                                   "config's compressed bytes are checked against the first's")
     a = ap.parse_args()
     import torch
@@ -74,14 +75,16 @@ def main():
     if a.sweep:
         first = None
         for cfg in a.sweep.split(","):
-            lanes, waves = cfg.split(":")
+            lanes, waves, *il = cfg.split(":")
             os.environ["ENET_HIP_RC_LANES"], os.environ["ENET_HIP_RC_WAVES"] = lanes, waves
+            os.environ["ENET_HIP_RC_INTERLEAVE"] = il[0] if il else "0"
             d_c.zero_()
             d_d.zero_()
             r = run_once()
             comp = (d_c.cpu().numpy().tobytes(), r["clen"].tobytes())
             first = first or comp
             print(json.dumps({"lanes_per_wave": int(lanes), "waves_per_cu": int(waves),
+                              "symbol_major": os.environ["ENET_HIP_RC_INTERLEAVE"] != "0",
                               "compress_us": round(r["tc"] * 1e6, 1), "decompress_us": round(r["td"] * 1e6, 1),
                               "compress_GBps": round(nbytes / r["tc"] / 1e9, 3),
                               "decompress_GBps": round(nbytes / r["td"] / 1e9, 3),
