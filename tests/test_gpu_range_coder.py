@@ -59,14 +59,16 @@ def test_decompress_matches_oracle_long(ctx, oracle_lib):  # noqa: F811
         assert (got[int(goff[i]):int(goff[i]) + int(glen[i])] == msgs[i]).all(), i
 
 
-@pytest.mark.parametrize("lanes,waves", [(64, 4), (16, 16), (3, 2), (1, 1)])
-def test_compress_lanes_per_wave(dctx, oracle_lib, monkeypatch, lanes, waves):  # noqa: F811
+@pytest.mark.parametrize("lanes,waves,interleave", [(64, 4, 0), (16, 16, 0), (3, 2, 0), (1, 1, 0), (16, 16, 1),
+                                                   (5, 3, 1)])
+def test_compress_lanes_per_wave(dctx, oracle_lib, monkeypatch, lanes, waves, interleave):  # noqa: F811
     """Any number of active lanes per wave and waves per CU (diagnostics knobs
     ENET_HIP_RC_LANES / _WAVES; 16 x 16 is the product's): the same bytes as the
     oracle, including DGRAMs taken on a lane's later grid-stride turns (3 x 2 and
     1 x 1 launch fewer lanes than the 3000 DGRAMs)."""
     monkeypatch.setenv("ENET_HIP_RC_LANES", str(lanes))
     monkeypatch.setenv("ENET_HIP_RC_WAVES", str(waves))
+    monkeypatch.setenv("ENET_HIP_RC_INTERLEAVE", str(interleave))   # (1: symbol-major models)
     msgs = corpus(3000, seed=9) + [np.zeros(0, np.uint8)]
     data, off, lens = pack(msgs)
     limit = lens * 2 + 64
