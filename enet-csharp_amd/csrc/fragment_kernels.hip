@@ -246,12 +246,15 @@ __global__ void __launch_bounds__(256) frag_copy_kernel(FragArgs a) {
             pre[c + 1] = pre[c] + ((L[c] + 15u) >> 4);
             if (h && lane == c && ci != ~0ull) a.claim[ci] = ~0u;   // claim words back to ~0 for the next batch
         }
-        for (uint32_t k = lane; k < pre[kCopyCmds]; k += 64u) {
+        // chunk k's command, its byte x and its end
+        auto chunk = [&](uint32_t k, uint32_t& Lc, uint64_t& sc, uint64_t& dc, uint32_t& x) __attribute__((always_inline)) {
             uint32_t c = 0;
 #pragma unroll
             for (uint32_t q = 1; q < kCopyCmds; ++q) c += k >= pre[q] ? 1u : 0u;
-            uint32_t Lc = L[0], pc = pre[0];
-            uint64_t sc = src[0], dc = dst[0];
+            uint32_t pc = pre[0];
+            Lc = L[0];
+            sc = src[0];
+            dc = dst[0];
 #pragma unroll
             for (uint32_t q = 1; q < kCopyCmds; ++q)
                 if (c == q) {
@@ -260,8 +263,24 @@ __global__ void __launch_bounds__(256) frag_copy_kernel(FragArgs a) {
                     sc = src[q];
                     dc = dst[q];
                 }
-            const uint32_t x = (k - pc) << 4;
-            copy_span(a.bytes + sc, a.msg_bytes + dc, Lc, x);
+            x = (k - pc) << 4;
+        };
+        // two chunks per lane per turn: both whole-chunk loads issued before either store
+        const uint32_t nk = pre[kCopyCmds];
+        for (uint32_t k = lane; k < nk; k += 128u) {
+            uint32_t L0, L1, x0, x1;
+            uint64_t s0, d0, s1, d1;
+            chunk(k, L0, s0, d0, x0);
+            const bool two = k + 64u < nk;
+            chunk(two ? k + 64u : k, L1, s1, d1, x1);
+            const bool f0 = x0 + 16u <= L0, f1 = two && x1 + 16u <= L1;
+            u32x4v v0 = {0u, 0u, 0u, 0u}, v1 = {0u, 0u, 0u, 0u};
+            if (f0) __builtin_memcpy(&v0, a.bytes + s0 + x0, 16);
+            if (f1) __builtin_memcpy(&v1, a.bytes + s1 + x1, 16);
+            if (f0) __builtin_memcpy(a.msg_bytes + d0 + x0, &v0, 16);
+            else copy_span(a.bytes + s0, a.msg_bytes + d0, L0, x0);
+            if (f1) __builtin_memcpy(a.msg_bytes + d1 + x1, &v1, 16);
+            else if (two) copy_span(a.bytes + s1, a.msg_bytes + d1, L1, x1);
         }
     }
 }

@@ -1,0 +1,10 @@
+set -o pipefail
+# round 4 (as): fragment copy, two chunks per lane per turn, against the previous library, interleaved
+out=gpurun_out/r4as
+mkdir -p $out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+for rep in 1 2 3; do
+  ENET_HIP_LIBRARY=$PWD/build_ab/libenethip_base.so tools/gpu_step.sh 300 $out/frag_base_$rep.log python3 -u tools/frag_bench.py || exit 1
+  ENET_HIP_LIBRARY=$PWD/build_ab/libenethip_two.so tools/gpu_step.sh 300 $out/frag_two_$rep.log python3 -u tools/frag_bench.py || exit 1
+done
+echo done > $out/done
