@@ -193,3 +193,26 @@ def test_cfg4_shards_partition_the_million_packets():
             assert (b.payload[:32] == ref).all()
             total += b.n
         assert total == 2 * (n // k)
+
+
+def test_kernel_name_follows_the_entry_and_knobs():
+    """The dominant kernel each bench form names (rocprof's spelling of
+    crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT, VF, DYN>): product list form,
+    binned records (one workgroup per CU) and the compact records instance (two),
+    the records ablations, the dynamic-rounds twins."""
+    import argparse
+    import bench
+
+    def name(**kw):
+        a = dict(path=0, lanes=0, binned=False, ablate=0, wgs=0)
+        a.update(kw)
+        return bench.kernel_name(argparse.Namespace(**a))
+
+    assert name() == "crc32_vring_kernel<3, 0, 0, 0, 0, 0, 0, 0, 0>"
+    assert name(binned=True) == "crc32_vring_kernel<2, 0, 0, 0, 1, 0, 0, 0, 0>"
+    assert name(binned=True, wgs=2) == "crc32_vring_kernel<2, 0, 0, 0, 2, 0, 0, 0, 0>"
+    assert name(binned=True, ablate=38912) == "crc32_vring_kernel<2, 0, 0, 19, 1, 0, 0, 0, 0>"
+    assert name(binned=True, ablate=524288) == "crc32_vring_kernel<2, 0, 0, 0, 1, 0, 0, 0, 1>"
+    assert name(binned=True, ablate=8388608) == "crc32_vring_kernel<2, 0, 0, 0, 1, 0, 0, 0, 0>"
+    assert name(ablate=524288) == "crc32_vring_kernel<3, 0, 0, 0, 0, 0, 0, 0, 1>"
+    assert name(ablate=8388608) == "crc32_vring_kernel<3, 0, 0, 0, 0, 0, 0, 0, 2>"
