@@ -931,3 +931,27 @@ def test_gather_binned_short_segment_bounds(dctx, golden, oracle_lib):
                 assert (got == e).all(), (b, i, np.nonzero(got != e)[0][:5])
     finally:
         dctx.diag_ablation(0)
+
+
+def test_binned_memory_order_diagnostic(dctx, golden, oracle_lib):
+    """The binned entry with its records left in memory order (diagnostics 2^30, the
+    A/B that prices the length sort): the records instance still writes every CRC to
+    its caller index -- cfg3, the golden vectors and every bin with empties."""
+    b = workloads.cfg3()
+    exp = oracle_lib.batch(b.payload, b.off, b.lens, threads=16)
+    payload, off, lens, exp_g = golden_batch(golden)
+    rng = np.random.default_rng(41)
+    n = 20000
+    e_lens = rng.integers(0, 9000, size=n).astype(np.uint32)
+    e_lens[:64] = 0
+    e_off = rng.integers(0, 1 << 20, size=n).astype(np.uint64)
+    e_pay = rng.integers(0, 256, size=(1 << 20) + 9000, dtype=np.uint8)
+    exp_e = oracle_lib.batch(e_pay, e_off, e_lens, threads=8)
+    try:
+        dctx.diag_ablation(1 << 30)
+        for lanes in (4, 8):
+            assert (run_binned(dctx, b.payload, b.off, b.lens, lanes) == exp).all(), ("cfg3", lanes)
+            assert (run_binned(dctx, payload, off, lens, lanes) == exp_g).all(), ("golden", lanes)
+            assert (run_binned(dctx, e_pay, e_off, e_lens, lanes) == exp_e).all(), ("edges", lanes)
+    finally:
+        dctx.diag_ablation(0)
