@@ -85,3 +85,23 @@ def test_errors_without_device():
     assert lib.enet_hip_crc32_batch_device(None, None, None, None, 1, None, None) == -1
     assert lib.enet_hip_set_tuning(None, 4, 2) == -1
     assert enethip.error_string(0) == "success"
+
+
+def test_callback_every_length_and_alignment():
+    """The callback's carry-less-multiply folding (buffers of 64 bytes or more, when
+    the CPU has PCLMULQDQ) and its table tail: every length 0..320 at every 16-byte
+    misalignment, long buffers, and registers chained through enet_hip_crc32_update,
+    against zlib's CRC-32 (the same polynomial and register, packet.cs:142-160)."""
+    lib = enethip.load()
+    rng = np.random.default_rng(5)
+    blob = rng.integers(0, 256, size=80000, dtype=np.uint8).tobytes()
+    buf = ctypes.create_string_buffer(blob)
+    base = ctypes.addressof(buf)
+    for n in list(range(0, 321)) + [1023, 1024, 1025, 4095, 65536, 70001]:
+        for off in (0, 1, 7, 15):
+            reg = lib.enet_hip_crc32_update(0xFFFFFFFF, ctypes.c_void_p(base + off), n)
+            assert (~reg & 0xFFFFFFFF) == zlib.crc32(blob[off:off + n]), (n, off)
+    for cut in (0, 5, 64, 100, 777):                          # two calls chained
+        reg = lib.enet_hip_crc32_update(0xFFFFFFFF, ctypes.c_void_p(base + 3), cut)
+        reg = lib.enet_hip_crc32_update(reg, ctypes.c_void_p(base + 3 + cut), 5000 - cut)
+        assert (~reg & 0xFFFFFFFF) == zlib.crc32(blob[3:5003]), cut
