@@ -23,11 +23,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--messages", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--in-order", action="store_true",
+                    help="fragments in send order instead of shuffled (prices the scattered descriptor stores)")
     a = ap.parse_args()
     import torch
     import enethip
     from enethip import workloads
-    fb = workloads.cfg5_fragments(a.messages)
+    fb = (workloads.fragments([65536] * a.messages, shuffle=False, name=f"cfg5 receive, in order: {a.messages} x 65536 B")
+          if a.in_order else workloads.cfg5_fragments(a.messages))
     words = 2
     ctx = enethip.Context(0)
     t = lambda x, dt: torch.from_numpy(np.ascontiguousarray(x).view(dt)).cuda()  # noqa: E731
