@@ -1898,9 +1898,9 @@ int enet_hip_fragment_reassemble_device(enet_hip_context* ctx, const uint8_t* by
     std::lock_guard<std::mutex> lk(ctx->mu);
     ENH_CHECK(hipSetDevice(ctx->device));
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-    // scratch: claim words (~0 between calls, restored by frag_copy_kernel), then the
-    // per-slot winner counts and the deferred flag (0 between calls, restored by
-    // frag_copy_kernel / frag_serial_kernel)
+    // scratch: claim words (~0 between calls, restored by frag_copy_kernel or
+    // frag_copy_claims_kernel), then the per-slot winner counts and the deferred flag
+    // (0 between calls, restored by frag_copy_kernel / frag_serial_kernel)
     const size_t claims = std::max<size_t>(1, slotCount * wordsPerMsg * 32u);
     const size_t need = claims + slotCount + 1;
     // Refill on any layout change that could expose words not in the filled state.
@@ -1924,14 +1924,21 @@ int enet_hip_fragment_reassemble_device(enet_hip_context* ctx, const uint8_t* by
         ctx->d_claim_words = claims;
     }
     int rc;
-    if ((rc = ensure(&ctx->d_frag_desc, &ctx->d_frag_desc_cap, count * 28 + 64))) return rc;
+    // copy descriptors: by command (n each), and on the slots decide path also by claim
+    // word (slot-major, `claims` each; fragment_kernels.hpp frag_slots_path)
+    const size_t qn = frag_slots_path(static_cast<uint64_t>(slotCount) * wordsPerMsg * 32u, count) ? claims : 0;
+    if ((rc = ensure(&ctx->d_frag_desc, &ctx->d_frag_desc_cap, count * 28 + qn * 20 + 64))) return rc;
     uint64_t* d_src = reinterpret_cast<uint64_t*>(ctx->d_frag_desc);
     uint64_t* d_dst = d_src + count;
     uint64_t* d_cl = d_dst + count;
-    uint32_t* d_len = reinterpret_cast<uint32_t*>(d_cl + count);
+    uint64_t* q_src = d_cl + count;
+    uint64_t* q_dst = q_src + qn;
+    uint32_t* d_len = reinterpret_cast<uint32_t*>(q_dst + qn);
+    uint32_t* q_len = d_len + count;
     FragArgs a{bytes, cmdOffsets, cmdAvail, slots, count, maximumPacketSize, msgBytes, msgOffsets, msgLengths,
                msgFragCounts, fragments, wordsPerMsg, remaining, slotCount, status, ctx->d_claim,
-               ctx->d_claim + claims, ctx->d_claim + claims + slotCount, d_src, d_dst, d_len, d_cl};
+               ctx->d_claim + claims, ctx->d_claim + claims + slotCount, d_src, d_dst, d_len, d_cl,
+               qn ? q_src : nullptr, qn ? q_dst : nullptr, qn ? q_len : nullptr};
     rc = fragment_reassemble_launch(a, ctx->num_cus, st);
     // a failed launch may leave claim words set: the next call starts from fresh fills
     if (rc) ctx->d_claim_cap = 0;

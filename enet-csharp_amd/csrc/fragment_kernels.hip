@@ -30,8 +30,12 @@
 //      same slot are DEFERRED (status 2): the slot kernel checks, per slot, that
 //      the winners' ranges are disjoint and ascending in fragment-number order;
 //      the atomic kernel defers every slot with two or more winners;
-//   3. frag_copy_kernel (4 commands per wave as one flat space of 16-byte chunks):
-//      the copies of the non-deferred winners, and the claim words back to ~0;
+//   3. the copy, 4 descriptors per wave as one flat space of 16-byte chunks:
+//      frag_copy_claims_kernel on the slots path (descriptors slot-major in claim
+//      space, written coalesced by the decide kernel: on a shuffled batch the
+//      command-indexed stores cost the decide kernel 19.1 against 10.3 us,
+//      profiles/r04_frag_copy/), frag_copy_kernel (by command) on the atomic path;
+//      the non-deferred winners' copies, and the claim words back to ~0;
 //   4. frag_serial_kernel (one wave; returns at once unless something was
 //      deferred): the deferred winners in batch order, each command's stores
 //      drained before the next, so where a batch's fragments overlap the later
@@ -160,15 +164,19 @@ __global__ void __launch_bounds__(256) frag_decide_slots_kernel(FragArgs a) {
             if (lane == 32u && (m >> 32) && (f0 >> 5) + 1u < a.words) bm[(f0 >> 5) + 1u] |= static_cast<uint32_t>(m >> 32);
             removed += static_cast<uint32_t>(__builtin_popcountll(m));
             uint32_t offset = 0, end = 0;
-            if (take) {
-                const uint64_t packed = a.copy_dst[w];
-                offset = static_cast<uint32_t>(packed);
-                const uint32_t len = min(static_cast<uint32_t>(a.copy_src[w]), a.msg_len[sl] - offset);   // 625-626
-                end = offset + len;
-                a.status[w] = 1;
-                a.copy_len[w] = len;
-                a.copy_src[w] = a.cmd_off[w] + kCmdBytes;
-                a.copy_dst[w] = a.msg_off[sl] + offset;
+            const uint64_t q = sl * bits + f;             // the claim-space descriptor (coalesced)
+            if (f < bits) {
+                uint32_t len = 0;
+                if (take) {
+                    const uint64_t packed = a.copy_dst[w];
+                    offset = static_cast<uint32_t>(packed);
+                    len = min(static_cast<uint32_t>(a.copy_src[w]), a.msg_len[sl] - offset);   // 625-626
+                    end = offset + len;
+                    a.status[w] = 1;
+                    a.q_src[q] = a.cmd_off[w] + kCmdBytes;
+                    a.q_dst[q] = a.msg_off[sl] + offset;
+                }
+                a.q_len[q] = len;                          // (every number: 0 = nothing to copy)
             }
             if (m) {
                 // exclusive prefix max of the winners' ends in fragment-number (lane) order
@@ -188,8 +196,15 @@ __global__ void __launch_bounds__(256) frag_decide_slots_kernel(FragArgs a) {
         if (clash) {                                       // defer the slot's winners to the serial pass
             for (uint32_t f0 = 0; f0 < bits; f0 += 64u) {
                 const uint32_t f = f0 + lane;
-                const uint32_t w = f < bits ? a.claim[sl * bits + f] : ~0u;
-                if (w != ~0u && a.status[w] == 1) a.status[w] = 2;
+                const uint64_t q = sl * bits + f;
+                const uint32_t w = f < bits ? a.claim[q] : ~0u;
+                if (w != ~0u && a.status[w] == 1) {        // (this lane wrote q's descriptor above)
+                    a.status[w] = 2;
+                    a.copy_len[w] = a.q_len[q];            // the serial pass copies by command
+                    a.copy_src[w] = a.q_src[q];
+                    a.copy_dst[w] = a.q_dst[q];
+                    a.q_len[q] = 0u;                       // not in the claim-space copy
+                }
             }
             if (lane == 0u) *a.deferred = 1u;
         }
@@ -285,6 +300,48 @@ __global__ void __launch_bounds__(256) frag_copy_kernel(FragArgs a) {
     }
 }
 
+// The slots decide path's copy: one wave takes kCopyCmds fragment numbers of the
+// claim space at a time (a slot's fragments in number order, so the message is
+// written front to back), as one flat space of 16-byte chunks, and puts every claim
+// word back to ~0 for the next batch.
+__global__ void __launch_bounds__(256) frag_copy_claims_kernel(FragArgs a, uint64_t claims) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t waves = static_cast<uint64_t>(gridDim.x) * (blockDim.x >> 6);
+    const uint64_t w = static_cast<uint64_t>(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    for (uint64_t base = w * kCopyCmds; base < claims; base += waves * kCopyCmds) {
+        uint32_t L[kCopyCmds], pre[kCopyCmds + 1];
+        uint64_t src[kCopyCmds], dst[kCopyCmds];
+        pre[0] = 0;
+#pragma unroll
+        for (uint32_t c = 0; c < kCopyCmds; ++c) {
+            const uint64_t q = base + c;
+            const bool h = q < claims;
+            L[c] = h ? a.q_len[q] : 0u;
+            src[c] = L[c] ? a.q_src[q] : 0u;
+            dst[c] = L[c] ? a.q_dst[q] : 0u;
+            pre[c + 1] = pre[c] + ((L[c] + 15u) >> 4);
+            if (h && lane == c) a.claim[q] = ~0u;
+        }
+        const uint32_t nk = pre[kCopyCmds];
+        for (uint32_t k = lane; k < nk; k += 64u) {
+            uint32_t c = 0;
+#pragma unroll
+            for (uint32_t q = 1; q < kCopyCmds; ++q) c += k >= pre[q] ? 1u : 0u;
+            uint32_t Lc = L[0], pc = pre[0];
+            uint64_t sc = src[0], dc = dst[0];
+#pragma unroll
+            for (uint32_t q = 1; q < kCopyCmds; ++q)
+                if (c == q) {
+                    Lc = L[q];
+                    pc = pre[q];
+                    sc = src[q];
+                    dc = dst[q];
+                }
+            copy_span(a.bytes + sc, a.msg_bytes + dc, Lc, (k - pc) << 4);
+        }
+    }
+}
+
 // One wave: the deferred winners (status 2) in batch order.  A command's stores
 // are drained (vmcnt counts stores on gfx950) before the next command's begin, so
 // overlapping bytes end up with the later command's data (protocol.cs:628 copies
@@ -324,13 +381,18 @@ int fragment_reassemble_launch(const FragArgs& a, int num_cus, hipStream_t st) {
         std::max<uint64_t>(1, std::min<uint64_t>((a.n + 4 * kCopyCmds - 1) / (4 * kCopyCmds), cap)));
     hipLaunchKernelGGL(frag_claim_kernel, dim3(g_thr), dim3(256), 0, st, a);
     const uint64_t claim_space = a.slot_count * (static_cast<uint64_t>(a.words) << 5);
-    if (claim_space <= 8u * a.n + 65536u) {
+    if (frag_slots_path(claim_space, a.n)) {
+        if (!a.q_src || !a.q_dst || !a.q_len) return -static_cast<int>(hipErrorInvalidValue);
         const unsigned g_slot = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>((a.slot_count + 3) / 4, cap)));
         hipLaunchKernelGGL(frag_decide_slots_kernel, dim3(g_slot), dim3(256), 0, st, a);
+        // (slot-major descriptors: the claims' copy, message by message)
+        const unsigned g_q = static_cast<unsigned>(
+            std::max<uint64_t>(1, std::min<uint64_t>((claim_space + 4 * kCopyCmds - 1) / (4 * kCopyCmds), cap)));
+        hipLaunchKernelGGL(frag_copy_claims_kernel, dim3(g_q), dim3(256), 0, st, a, claim_space);
     } else {
         hipLaunchKernelGGL(frag_decide_kernel, dim3(g_thr), dim3(256), 0, st, a);
+        hipLaunchKernelGGL(frag_copy_kernel, dim3(g_wave), dim3(256), 0, st, a);
     }
-    hipLaunchKernelGGL(frag_copy_kernel, dim3(g_wave), dim3(256), 0, st, a);
     hipLaunchKernelGGL(frag_serial_kernel, dim3(1), dim3(64), 0, st, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : -static_cast<int>(e);

@@ -30,7 +30,17 @@ struct FragArgs {
     uint64_t* copy_dst;
     uint32_t* copy_len;
     uint64_t* copy_claim;
+    // scratch, claim space (slot_count * words * 32 each), the slots decide path only:
+    // the copy descriptor of fragment number f of slot s at s * words * 32 + f
+    // (len 0 = nothing to copy), written coalesced and copied in message order
+    uint64_t* q_src;
+    uint64_t* q_dst;
+    uint32_t* q_len;
 };
+
+// the slots decide path (claim space descriptors) serves a batch whose claim space
+// (slots x bitmap bits) is at most this many words
+inline bool frag_slots_path(uint64_t claim_space, uint64_t n) { return claim_space <= 8u * n + 65536u; }
 
 int fragment_reassemble_launch(const FragArgs& a, int num_cus, hipStream_t st);
 
