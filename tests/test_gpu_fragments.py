@@ -122,6 +122,46 @@ def test_fragments_overlapping_ranges(ctx, oracle_lib, words):  # noqa: F811
             assert (so[k] == sg[k]).all(), k
 
 
+def slots_path(claim_space, n):
+    """fragment_kernels.hpp frag_slots_path: the slot-owned decide kernel and the
+    claim-space copy descriptors when the claim space is at most 8 n + 65536 words."""
+    return claim_space <= 8 * n + 65536
+
+
+def test_fragments_slots_threshold_and_scratch_regrowth(ctx, oracle_lib):  # noqa: F811
+    """the claim-space descriptor path at its edges.  3000 slots x 1
+    bitmap word = 96 000 claim words, so a batch of n = 3808 sits exactly on 8 n + 65536
+    (slots path, q_src/q_dst/q_len sized by the claim space) and n = 3807 one step past
+    it (atomic path).  Before them a small layout; after them the same slots with 2
+    words (192 000 claim words: the claim words and the descriptor scratch both regrow
+    on a slots-path call).  Every call against the sequential oracle."""
+    rng = np.random.default_rng(61)
+    small = workloads.fragments(rng.integers(1, 3000, 200), seed=62, duplicates=0.2)
+    so, sg = state(small, 1), state(small, 1)
+    assert slots_path(200 * 32, small.n)
+    assert (run_gpu(ctx, small, sg) == run_oracle(oracle_lib, small, so)).all()
+    for k in ("msg_bytes", "fragments", "remaining"):
+        assert (so[k] == sg[k]).all(), k
+
+    big = workloads.fragments(rng.integers(1000, 9000, 3000), seed=63, duplicates=0.5)
+    assert int(big.msg_count.max()) <= 32 and big.n > 3808 + 3807
+    for words in (1, 2):
+        so, sg = state(big, words), state(big, words)
+        claims = 3000 * 32 * words
+        cuts = [0, 3808, 3808 + 3807, big.n] if words == 1 else [0, big.n]
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            if words == 1 and b - a == 3808:
+                assert slots_path(claims, b - a) and claims == 8 * (b - a) + 65536
+            if words == 1 and b - a == 3807:
+                assert not slots_path(claims, b - a)
+            if words == 2:
+                assert slots_path(claims, b - a), "the regrowth call must take the slots path"
+            sel = np.arange(a, b)
+            assert (run_gpu(ctx, big, sg, sel) == run_oracle(oracle_lib, big, so, sel)).all(), (words, a, b)
+        for k in ("msg_bytes", "fragments", "remaining"):
+            assert (so[k] == sg[k]).all(), (words, k)
+
+
 def test_fragments_scratch_layout_changes(ctx, oracle_lib):  # noqa: F811
     """The context's claim scratch (claim words, then per-slot winner counts and the
     deferred flag) across calls whose (slots, bitmap words) layouts differ -- more
