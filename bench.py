@@ -65,6 +65,9 @@ def parse(argv=None):
     ap.add_argument("--launch", default="graph", choices=["graph", "direct"],
                     help="graph = the timed steps replayed from one captured HIP graph; direct = the same "
                          "launches enqueued one by one inside the timed region")
+    ap.add_argument("--shard", default=None, metavar="R/N",
+                    help="cfg4 only, no launcher: measure rank R's shard of an N-GPU cfg4 run on this one device "
+                         "(the per-GPU point the driver's N-GPU scaling line should show)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget per CPU-baseline leg")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -506,6 +509,8 @@ def spawn_ranks(n: int, argv, engine_factory=None, cpu_factory=None) -> int:
 def main(argv=None, engine_factory=None, cpu_factory=None):
     args = parse(argv)
     ws, rank, local = dist_env()
+    if args.shard and args.gpus > 1:
+        raise SystemExit("bench.py: --shard R/N measures one shard on one device (no --gpus N)")
     if ws <= 1 and args.gpus > 1:
         # no launcher: measure N GPUs by starting the N ranks here (never print a
         # one-rank line for --gpus N)
@@ -513,8 +518,14 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
     if ws > 1 and args.gpus != ws:
         print(f"bench.py: --gpus {args.gpus} under a launcher of {ws} ranks: measuring {ws}", file=sys.stderr)
         args.gpus = ws
+    shard = None
+    if args.shard:
+        r_, n_ = (int(x) for x in args.shard.split("/"))
+        if args.config != "cfg4" or ws != 1 or not 0 <= r_ < n_:
+            raise SystemExit("bench.py: --shard R/N needs --config cfg4, one process and 0 <= R < N")
+        shard = (r_, n_)
     dist = dist_init(ws)
-    batches = make_batches(args.config, args.rotate, rank, ws)
+    batches = make_batches(args.config, args.rotate, *(shard if shard else (rank, ws)))
     diag = args.path not in PRODUCT_PATHS or args.ablate != 0
     eng = (engine_factory or GpuEngine)(local, batches, args.lanes, args.wgs, *((diag,) if diag else ()))
     if hasattr(eng, "set_streams"):
@@ -610,13 +621,16 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
             "config": {
                 "workload": {"cfg2": "cfg2: 65536 packets x 1200 B packed",
                              "cfg3": "cfg3: 262144 packets x U[64,1400] B packed",
-                             "cfg4": f"cfg4: 1048576 packets x 1200 B, shard {rank} of {ws} (contiguous packets)",
+                             "cfg4": (f"cfg4: 1048576 packets x 1200 B, shard {shard[0]} of {shard[1]} (contiguous "
+                                      f"packets) measured alone on one device" if shard else
+                                      f"cfg4: 1048576 packets x 1200 B, shard {rank} of {ws} (contiguous packets)"),
                              "small": "small: 2048 packets x 1200 B (harness tests)"}[args.config] +
                             f", {len(batches)} rotating resident batches per GPU",
                 "packets_per_gpu": batches[0].n,
                 "payload_bytes_per_step": int(batches[0].payload_bytes),
                 "steps_per_launch": per_launch_steps,
-                "parallelism": f"{ws} independent shards (no collective)",
+                "parallelism": (f"shard {shard[0]}/{shard[1]} alone (the per-GPU point of {shard[1]} independent "
+                                f"shards)" if shard else f"{ws} independent shards (no collective)"),
                 "lanes_per_packet": args.lanes or "default",
                 "streams": args.streams,
                 "entry": ("enet_hip_crc32_batch_device_binned" if args.binned else

@@ -218,6 +218,16 @@ namespace enet
             uint dstAddr, ushort dstPort, nuint* sent);
 
         [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_udp_receive_decompress_verify(IntPtr ctx, int fd, byte* arena,
+            nuint stride, nuint maxDgrams, uint* peerConnectIds, nuint peerCount, int timeoutMs, uint* lengths,
+            byte* ok, nuint* received);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_udp_compress_stamp_send(IntPtr ctx, int fd, byte* bytes, nuint byteCount,
+            ulong* segOffsets, uint* segLengths, nuint segCount, uint* segFirst, uint* slotOffsets, nuint dgramCount,
+            uint dstAddr, ushort dstPort, nuint* sent);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
         public static extern int enet_hip_read_probe_device(IntPtr ctx, byte* bytes, nuint byteCount, uint* sink,
             void* stream);
 

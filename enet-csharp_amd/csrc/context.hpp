@@ -98,8 +98,18 @@ inline int ensure_pinned(uint8_t** p, size_t* cap, size_t need) {
     return 0;
 }
 
+// The batched range coder (crc32_kernels.hip) for a caller that holds ctx->mu.
+int range_coder_locked(enet_hip_context* ctx, bool decompress, const uint8_t* in, const uint64_t* inOffsets,
+                       const uint32_t* inLengths, size_t count, uint8_t* out, const uint64_t* outOffsets,
+                       const uint32_t* outLimits, uint32_t* outLengths, hipStream_t st);
+
 // The host-memory pipeline's streams and events (created on first use).
 int pipeline_init(enet_hip_context* ctx);
 void pipeline_release(enet_hip_context* ctx);
 
 }  // namespace enethip
+
+// sendmmsg of gather lists given as segment pointers (host_io.cpp; the compressing
+// send pipeline mixes the caller's arena with its compressed bytes)
+int enethip_udp_send_ptrs(int fd, const uint8_t* const* segPtrs, const uint32_t* segLengths, const uint32_t* segFirst,
+                          size_t dgramCount, uint32_t dstAddr, uint16_t dstPort, size_t* sent);

@@ -129,6 +129,12 @@ __device__ __forceinline__ u32x4 zero_prefix(u32x4 v, uint32_t n) {
     return u32x4{v.x & k0, v.y & k1, v.z & k2, v.w & k3};
 }
 
+// 64-bit unsigned min / max.  HIP's device min<uint64_t> / max<uint64_t> templates go
+// through double (v_cvt_f64_u32 ... v_max_f64 ... v_cvt_u32_f64: about 12 VALU, and
+// inexact above 2^53); these are a compare and two selects, or scalar ops on uniform values.
+__host__ __device__ __forceinline__ constexpr uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+__host__ __device__ __forceinline__ constexpr uint64_t umax64(uint64_t a, uint64_t b) { return a < b ? b : a; }
+
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }

@@ -37,14 +37,12 @@
 #include "context.hpp"
 #include "enet_hip.h"
 #include "fragment_kernels.hpp"
+#include "gather_join.hpp"
 #include "range_coder.hpp"
 
 namespace enethip {
 
 constexpr int kThreads = 512;                     // direct / gather kernels: 8 waves
-// Gather segments of at most this many bytes are folded byte by byte by the join
-// (crc32_gather_join_kernel), not by the binned checksum pass
-constexpr uint32_t kGatherSmall = 48;
 
 template <int NT>
 __device__ __forceinline__ void fill_table(uint8_t* lds, const uint32_t* image) {
@@ -807,15 +805,6 @@ __global__ void __launch_bounds__(kThreads) crc32_direct_kernel(PacketArgs pa, K
     }
 }
 
-struct GatherArgs {
-    const uint8_t* bytes;
-    const uint64_t* seg_off;
-    const uint32_t* seg_len;
-    const uint32_t* seg_first;
-    uint64_t n;
-    uint32_t* out;
-    uint64_t segs;      // segments with a CRC in seg_crc (the join's bound; the host's segCount)
-};
 
 // One lane per DGRAM; segments folded in order and joined by the carry-combine.
 __global__ void __launch_bounds__(kThreads) crc32_gather_kernel(GatherArgs ga, KernelTables tb) {
@@ -859,44 +848,7 @@ __global__ void __launch_bounds__(kThreads) crc32_gather_kernel(GatherArgs ga, K
 // segment's last byte), the long ones' CRCs and x^(8 len) -- before folding any.  A
 // short segment's 4-byte steps are slicing-by-4 on the dword v_alignbyte cuts at its
 // offset, its last L mod 4 bytes Sarwate steps (T_3 .. T_0 = columns 6, 4, 2, 0 of
-// the P = 1 image, 4 KiB in LDS).  Restated in tests/kernel_model.py (fold_small).
-constexpr int kSmallDwords = (3 + static_cast<int>(kGatherSmall) + 3) / 4;
-static_assert(15 + kGatherSmall <= 16 * ((kSmallDwords + 1 + 3) / 4), "a short segment's aligned lines fit the join's loads");
-
-
-// p[i] as a GLOBAL load (a generic pointer makes hipcc emit a flat load)
-template <class T>
-__device__ __forceinline__ T gload(const T* p, uint64_t i) {
-    return *reinterpret_cast<__attribute__((address_space(1))) const T*>(reinterpret_cast<uintptr_t>(p + i));
-}
-
-__device__ __forceinline__ void load_small(const uint8_t* a, uint32_t L, uint32_t (&d)[kSmallDwords + 1]) {
-    const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a)) & 3u;
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(a) & ~static_cast<uintptr_t>(3));
-    const uint32_t nd = (sh + L + 3u) >> 2;
-    // global loads (through a generic pointer hipcc emits flat loads, counted in lgkmcnt
-    // too: round 3's form, within noise of this one -- DESIGN.md 4.4)
-#pragma unroll
-    for (int k = 0; k < kSmallDwords; ++k) d[k] = static_cast<uint32_t>(k) < nd ? gload(w, k) : 0u;
-    d[kSmallDwords] = 0u;
-}
-
-__device__ __forceinline__ uint32_t fold_small(uint32_t reg, uint32_t sh, uint32_t L,
-                                               const uint32_t (&d)[kSmallDwords + 1], const uint32_t (*t4)[256]) {
-    const uint32_t nf = L >> 2;
-    uint32_t tail = 0;
-#pragma unroll
-    for (int i = 0; i < kSmallDwords - 1; ++i) {
-        const uint32_t v = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
-        if (static_cast<uint32_t>(i) < nf) {
-            const uint32_t x = reg ^ v;
-            reg = t4[3][x & 0xFFu] ^ t4[2][(x >> 8) & 0xFFu] ^ t4[1][(x >> 16) & 0xFFu] ^ t4[0][x >> 24];
-        }
-        tail = static_cast<uint32_t>(i) == nf ? v : tail;
-    }
-    for (uint32_t j = 0; j < (L & 3u); ++j) reg = t4[0][(reg ^ (tail >> (8u * j))) & 0xFFu] ^ (reg >> 8);
-    return reg;
-}
+// the P = 1 image, 4 KiB in LDS).  (fold_small, gather_join.hpp.)
 
 // JV (diagnostics, wrong CRCs by design): bit 0 = no short-segment fold (its dwords
 // XORed in), bit 1 = no multiply (XOR), bit 2 = no short-segment loads
@@ -914,7 +866,7 @@ __global__ void __launch_bounds__(kThreads) crc32_gather_join_kernel(GatherArgs 
         // segFirst lives in device memory, so the host cannot check segFirst[n] ==
         // segCount: clamp to the segments the binned pass filled (a short segCount
         // then gives wrong CRCs for the DGRAMs past it, never a read past seg_crc)
-        const uint32_t s1 = static_cast<uint32_t>(min<uint64_t>(ga.seg_first[d + 1], ga.segs));
+        const uint32_t s1 = static_cast<uint32_t>(umin64(ga.seg_first[d + 1], ga.segs));
         const uint32_t s0 = min(ga.seg_first[d], s1);
         uint32_t reg = 0xFFFFFFFFu;
         for (uint32_t q0 = s0; q0 < s1; q0 += kQ) {
@@ -960,6 +912,27 @@ __global__ void __launch_bounds__(kThreads) crc32_gather_join_kernel(GatherArgs 
 }
 
 
+// The post-join of the split join (gather_join.hpp): one thread per segment, after
+// the records pass.  A long segment q of DGRAM d = info[q].x adds
+// bswap(R_q x^(8 after_q)) to out[d] (R_q = ~bswap(seg_crc[q])), ~seg_crc[q] when
+// nothing follows it.  Only segFirst[0] <= q < segFirst[n] (clamped to the binned
+// segments) belong to a DGRAM; d < n bounds the atomic whatever the arrays hold.
+__global__ void __launch_bounds__(256) crc32_gather_post_kernel(const uint32_t* seg_len, const uint32_t* seg_crc,
+                                                                const uint2* info, const uint32_t* seg_first,
+                                                                uint64_t n, uint64_t segs, uint32_t small,
+                                                                uint32_t* out) {
+    const uint64_t hi = umin64(seg_first[n], segs), lo = seg_first[0];
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256u;
+    for (uint64_t q = lo + static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x; q < hi; q += stride) {
+        const uint32_t L = seg_len[q];
+        const uint2 in = info[q];
+        const uint32_t c = seg_crc[q];
+        if (L <= small || in.x >= n) continue;
+        const uint32_t add = in.y == kOneReflected ? ~c : bswap32(mulmod(~bswap32(c), in.y));
+        atomicXor(out + in.x, add);
+    }
+}
+
 // Read-roofline probe: every byte loaded once by 16-byte coalesced loads,
 // 4 loads in flight per lane, XOR-folded so nothing is dead code.
 __global__ void __launch_bounds__(kThreads) read_probe_kernel(const uint8_t* bytes, uint64_t nvec, uint32_t* sink) {
@@ -1003,7 +976,9 @@ struct HostTables {
         : image(static_cast<size_t>(kImages) * kImageDwords), xn(2 * kXnEntries), init(64),
           basis(static_cast<size_t>(kImages) * kBasisDwords), basis2(static_cast<size_t>(kImages) * kVrBasisDwords),
           tz(kTzTableDwords + kTzSmallDwords), lin(kImageDwords) {
-        if (lin_image(lin.data())) basis_ok = false;
+#ifdef ENET_HIP_DIAG
+        if (lin_image(lin.data())) basis_ok = false;   // (the linear-stream kernel: diagnostics only)
+#endif
         init[0] = 0xFFFFFFFFu;
         for (int r = 1; r < 64; ++r) init[r] = unstep_zero(init[r - 1]);
         std::vector<uint32_t> cinv(kCinvEntries);
@@ -1310,9 +1285,19 @@ bool vring_path(const enet_hip_context* ctx) {
 // on at most a few streams at once), with a generation one larger, so the kernel
 // needs no reset of it (crc32_vring.hip vr_claim_next).  After 2^32 - 2 uses of a
 // line (2^40 launches) the context falls back to the static deal.
+// Contract of the dynamic modes (diagnostics A/B only; the product never sets them):
+// a launch must have ended before 255 later launches of the context have started
+// (kVrClaimLines - 1; a launch held back behind an event while 256 others run would
+// find its line at a newer generation and skip its dynamic chunks), and a launch
+// being captured into a graph takes the static deal -- a replay would reuse the
+// captured {line, generation} and find the word already counted up.
 constexpr uint32_t kVrClaimLines = 256;
 constexpr uint32_t kVrPairLines = 64;
-VrVariant with_claim(enet_hip_context* ctx, VrVariant v) {
+VrVariant with_claim(enet_hip_context* ctx, VrVariant v, hipStream_t st) {
+    if (ctx->vr_pair || ctx->vr_dynamic) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return v;
+    }
     if (!v.walk && ctx->vr_pair && ctx->d_pairs) {           // pair rounds (diagnostics)
         const uint64_t seq = ctx->pairs_next.fetch_add(1u);
         const uint64_t gen = seq / kVrPairLines + 1u;
@@ -1372,7 +1357,7 @@ int verify_vring_list(enet_hip_context* ctx, const ENetHipVerifyBatch* batches, 
         // against 22.1 at one (profiles/r04_verify_wgs/; the checksum instance is the
         // other way round, 18.9 against 18.2-18.4)
         const int wgs = ctx->wgs_per_cu >= 1 ? std::min(ctx->wgs_per_cu, 2) : 2;
-        const int rc = vring_launch_vlist(ctx->num_cus * wgs, with_claim(ctx, v), st, bl, tb, ctx->d_basis2,
+        const int rc = vring_launch_vlist(ctx->num_cus * wgs, with_claim(ctx, v, st), st, bl, tb, ctx->d_basis2,
                                           v.abl ? ctx->trace : nullptr);
         if (rc) return rc;
     }
@@ -1397,7 +1382,7 @@ int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStr
     }
     if (mode == 0 && (pa.lg == 2 || pa.lg == 3) && ctx->ablation == 0 && vring_path(ctx))
         return vring_launch(pa.lg, ctx->num_cus * vring_wgs(ctx, 1),
-                            with_claim(ctx, pa.meta4 ? bin_variant(ctx) : vring_variant(ctx, false)), st, pa, tb,
+                            with_claim(ctx, pa.meta4 ? bin_variant(ctx) : vring_variant(ctx, false), st), st, pa, tb,
                             ctx->d_basis2);
     if (ctx->path != 1 && pa.lg >= 2 && pa.lg <= 4) {
         const bool lean_path = (ctx->path >= kLeanPath0 && ctx->path < kVringPath) || (ctx->path == 0 && ctx->ablation == 0);
@@ -1489,18 +1474,22 @@ int enet_hip_context_create(int device, enet_hip_context** out) {
         if ((rc = herr(hipMemcpy(ctx->d_tz, ht.tz.data(), ht.tz.size() * 4, hipMemcpyHostToDevice)))) break;
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_basis2), ht.basis2.size() * 4)))) break;
         if ((rc = herr(hipMemcpy(ctx->d_basis2, ht.basis2.data(), ht.basis2.size() * 4, hipMemcpyHostToDevice)))) break;
+#ifdef ENET_HIP_DIAG
+        // the linear-stream image and the dynamic-round claim words: diagnostics paths
+        // only (the product library builds neither kernel -- ADVICE r4)
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_lin), ht.lin.size() * 4)))) break;
         if ((rc = herr(hipMemcpy(ctx->d_lin, ht.lin.data(), ht.lin.size() * 4, hipMemcpyHostToDevice)))) break;
         const size_t claim_bytes = static_cast<size_t>(kVrClaimLines) * kVrClaimWords * 4;
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_rounds), claim_bytes)))) break;
         if ((rc = herr(hipMemset(ctx->d_rounds, 0, claim_bytes)))) break;
-#ifdef ENET_HIP_DIAG
         const size_t pair_bytes = static_cast<size_t>(kVrPairLines) * kVrPairWords * 8;
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_pairs), pair_bytes)))) break;
         if ((rc = herr(hipMemset(ctx->d_pairs, 0, pair_bytes)))) break;
 #endif
         if ((rc = vring_setup())) break;
+#ifdef ENET_HIP_DIAG
         if ((rc = lin_setup())) break;
+#endif
         if ((rc = setup_stream())) break;
 #ifdef ENET_HIP_DIAG
         if ((rc = setup_vstream())) break;
@@ -1559,7 +1548,7 @@ int enet_hip_diag_ablation(enet_hip_context* ctx, int mode) {
     if (!ctx || mode < 0) return -static_cast<int>(hipErrorInvalidValue);
     ctx->bin_identity = (mode >> 30) & 1;                    // 2^30: binned records left in memory order
     ctx->vr_pair = (mode >> 23) & 1;                         // 8388608: vring pair rounds
-    ctx->join_abl = (mode >> 20) & 7;                        // 1048576 x (1..7): gather-join ablations
+    ctx->join_abl = (mode >> 20) & 7;                        // 1048576 x (1..7): the one-pass gather join after the records (4: unablated; others: its ablations)
     // 16777216 x (1 + b), b < 63: the binned gather's short-segment bound b bytes (0: 48)
     ctx->gather_small = (mode >> 24) ? ((mode >> 24) & 63) - 1 : -1;
     ctx->vr_dynamic = (mode >> 19) & 1;                      // 524288: vring dynamic rounds
@@ -1656,7 +1645,7 @@ int enet_hip_crc32_batch_list_device(enet_hip_context* ctx, const ENetHipBatch* 
                 bl.b[bl.count++] = VrBatch{batches[b].bytes, batches[b].offsets, batches[b].lengths, batches[b].out,
                                            static_cast<uint64_t>(batches[b].count), 0u};
             const int rc = vring_launch_list(lg, ctx->num_cus * vring_wgs(ctx, bl.count),
-                                             with_claim(ctx, vring_variant(ctx, true)), st, bl, tb, ctx->d_basis2,
+                                             with_claim(ctx, vring_variant(ctx, true), st), st, bl, tb, ctx->d_basis2,
                                              ctx->trace);
             if (rc) return rc;
         }
@@ -1814,8 +1803,12 @@ int enet_hip_crc32_gather_device(enet_hip_context* ctx, const uint8_t* bytes, co
     return herr(hipGetLastError());
 }
 
+// records | seg_crc | tile counts | the split join's info[] (8 B per segment)
+static size_t gather_counts_bytes(size_t segCount) { return (4u * gather_tiles(segCount) + 15u) & ~static_cast<size_t>(15u); }
+
 size_t enet_hip_gather_binned_workspace_size(size_t segCount) {
-    return gather_records_bytes(segCount) + gather_crc_bytes(segCount) + 4u * gather_tiles(segCount) + 16u;
+    return gather_records_bytes(segCount) + gather_crc_bytes(segCount) + gather_counts_bytes(segCount) +
+           8u * segCount + 16u;
 }
 
 int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* bytes, const uint64_t* segOffsets,
@@ -1839,6 +1832,39 @@ int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* by
     // counts on the device: VrBatches::tile_counts) and checksummed by the vring's
     // records instance.  Other paths: every segment through the binned entry.
     const bool split = vring_path(ctx) && ctx->ablation == 0 && (lanes == 4 || lanes == 8);
+    GatherArgs ga{bytes, segOffsets, segLengths, segFirst, dgramCount, out, segCount};
+#ifdef ENET_HIP_DIAG
+    const bool old_join = ctx->join_abl != 0;                // (diagnostics: the one-pass join after the records)
+#else
+    constexpr bool old_join = false;
+#endif
+    if (split && !old_join) {
+        // the split join (gather_join.hpp): pre-join beside the binning tiles, records,
+        // post-join per segment -- no pass waits on a DGRAM's metadata chain after the records
+        const KernelTables tb = tables_of(ctx);
+        const uint32_t kpk = lanes == 4 ? 16u : 8u;
+        uint2* info = reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(counts) + gather_counts_bytes(segCount));
+        const uint32_t small = gather_small(ctx);
+        const unsigned pj = static_cast<unsigned>(std::min<uint64_t>((dgramCount + 255u) / 256u, 8u * ctx->num_cus));
+        int rc;
+        if ((rc = gather_bin_prejoin(ga, info, tb, small, kpk, workspace, counts, pj, st))) return rc;
+        if (!segCount) return 0;
+        VrBatches bl{};
+        bl.count = 1;
+        bl.tiles = static_cast<uint32_t>(gather_tiles(segCount));
+        bl.tile_counts = counts;
+        bl.b[0] = VrBatch{bytes, static_cast<const uint64_t*>(workspace), nullptr, seg_crc, 1024ull * bl.tiles, 0u};
+        const int gw = ctx->wgs_per_cu >= 1 ? std::min(ctx->wgs_per_cu, 2) : 2;
+        VrVariant gv = bin_variant(ctx);
+        gv.compact = gw >= 2;
+        if ((rc = vring_launch_list(lanes == 4 ? 2 : 3, ctx->num_cus * gw, with_claim(ctx, gv, st), st, bl, tb,
+                                    ctx->d_basis2, nullptr, true)))
+            return rc;
+        const unsigned pg = static_cast<unsigned>(std::min<uint64_t>((segCount + 255u) / 256u, 8u * ctx->num_cus));
+        hipLaunchKernelGGL(crc32_gather_post_kernel, dim3(pg), dim3(256), 0, st, segLengths, seg_crc, info, segFirst,
+                           static_cast<uint64_t>(dgramCount), static_cast<uint64_t>(segCount), small, out);
+        return herr(hipGetLastError());
+    }
     if (segCount && split) {
         const KernelTables tb = tables_of(ctx);
         const uint32_t kpk = lanes == 4 ? 16u : 8u;
@@ -1855,7 +1881,7 @@ int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* by
         const int gw = ctx->wgs_per_cu >= 1 ? std::min(ctx->wgs_per_cu, 2) : 2;
         VrVariant gv = bin_variant(ctx);
         gv.compact = gw >= 2;
-        if ((rc = vring_launch_list(lanes == 4 ? 2 : 3, ctx->num_cus * gw, with_claim(ctx, gv), st, bl, tb,
+        if ((rc = vring_launch_list(lanes == 4 ? 2 : 3, ctx->num_cus * gw, with_claim(ctx, gv, st), st, bl, tb,
                                     ctx->d_basis2, nullptr, true)))
             return rc;
     } else if (segCount) {                                   // every segment's CRC, mixed lengths: length-binned
@@ -1863,7 +1889,6 @@ int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* by
                                                           workspace, bws, st);
         if (rc) return rc;
     }
-    GatherArgs ga{bytes, segOffsets, segLengths, segFirst, dgramCount, out, segCount};
     const unsigned grid = grid_for(ctx, dgramCount);
     const uint32_t small = split ? gather_small(ctx) : 0u;
 #ifdef ENET_HIP_DIAG
@@ -1945,16 +1970,16 @@ int enet_hip_fragment_reassemble_device(enet_hip_context* ctx, const uint8_t* by
     return rc;
 }
 
-static int range_coder_call(enet_hip_context* ctx, bool decompress, const uint8_t* in, const uint64_t* inOffsets,
-                            const uint32_t* inLengths, size_t count, uint8_t* out, const uint64_t* outOffsets,
-                            const uint32_t* outLimits, uint32_t* outLengths, void* stream) {
-    if (!ctx) return -static_cast<int>(hipErrorInvalidValue);
+}  // extern "C"
+
+// The batched range coder with the context's lock already held (the public entries
+// below, and the UDP pipelines of host_pipeline.hip that decompress / compress inside
+// their own locked call).
+int enethip::range_coder_locked(enet_hip_context* ctx, bool decompress, const uint8_t* in, const uint64_t* inOffsets,
+                                const uint32_t* inLengths, size_t count, uint8_t* out, const uint64_t* outOffsets,
+                                const uint32_t* outLimits, uint32_t* outLengths, hipStream_t st) {
     if (count == 0) return 0;
-    if (!in || !inOffsets || !inLengths || !out || !outOffsets || !outLimits || !outLengths)
-        return -static_cast<int>(hipErrorInvalidValue);
-    std::lock_guard<std::mutex> lk(ctx->mu);
     ENH_CHECK(hipSetDevice(ctx->device));
-    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     // one lane per DGRAM, 16 per wave, at most 16 waves per CU: 65 536 DGRAMs in flight,
     // as many as 4 full waves per CU had, with a quarter of the stragglers per wave
     // (1.30-1.36 against 1.05 GB/s on tools/rc_bench.py, profiles/r04_range_coder/);
@@ -1978,6 +2003,20 @@ static int range_coder_call(enet_hip_context* ctx, bool decompress, const uint8_
     }
     RangeArgs a{in, inOffsets, inLengths, count, out, outOffsets, outLimits, outLengths, ctx->d_rc_scratch, interleave};
     return range_coder_launch(decompress, a, threads, lanes, st);
+}
+
+extern "C" {
+
+static int range_coder_call(enet_hip_context* ctx, bool decompress, const uint8_t* in, const uint64_t* inOffsets,
+                            const uint32_t* inLengths, size_t count, uint8_t* out, const uint64_t* outOffsets,
+                            const uint32_t* outLimits, uint32_t* outLengths, void* stream) {
+    if (!ctx) return -static_cast<int>(hipErrorInvalidValue);
+    if (count == 0) return 0;
+    if (!in || !inOffsets || !inLengths || !out || !outOffsets || !outLimits || !outLengths)
+        return -static_cast<int>(hipErrorInvalidValue);
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    return range_coder_locked(ctx, decompress, in, inOffsets, inLengths, count, out, outOffsets, outLimits, outLengths,
+                              stream ? static_cast<hipStream_t>(stream) : ctx->stream);
 }
 
 int enet_hip_range_compress_device(enet_hip_context* ctx, const uint8_t* in, const uint64_t* inOffsets,

@@ -37,6 +37,7 @@
 #include <algorithm>
 
 #include "crc32_lean.hpp"
+#include "gather_join.hpp"
 
 namespace enethip {
 
@@ -757,15 +758,14 @@ __device__ __forceinline__ uint32_t bin_of(uint32_t len, uint64_t off) {
 // IDENT (diagnostics): every record left at its own position (memory order), to price
 // the binned order against the records machinery.
 template <bool VERIFY, bool COMPACT = false, bool IDENT = false>
-__global__ void __launch_bounds__(kBinThreads) bin_tile_kernel(const uint32_t* len, const uint64_t* off, uint64_t n,
-                                                               uint32_t kpk, const uint32_t* slot_off,
-                                                               const uint32_t* connect, uint4* rec, uint32_t small,
-                                                               uint32_t* count) {
+__device__ __forceinline__ void bin_tile_body(uint32_t blk, uint32_t ntiles, const uint32_t* len, const uint64_t* off,
+                                              uint64_t n, uint32_t kpk, const uint32_t* slot_off,
+                                              const uint32_t* connect, uint4* rec, uint32_t small, uint32_t* count) {
     __shared__ uint32_t h[kBins], wsum[kBinThreads / 64];
     const uint32_t tid = threadIdx.x;
     h[tid] = 0;
     __syncthreads();
-    const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kBinTile;
+    const uint64_t base = static_cast<uint64_t>(blk) * kBinTile;
     uint32_t L[kBinItems], slot[kBinItems];
     uint64_t o[kBinItems];
 #pragma unroll
@@ -800,18 +800,18 @@ __global__ void __launch_bounds__(kBinThreads) bin_tile_kernel(const uint32_t* l
     }
     h[tid] = pre + incl - mine;                              // first slot of bin tid in the tile
     __syncthreads();
-    const uint64_t full = COMPACT ? gridDim.x : n / kBinTile;    // T
-    const bool interleave = COMPACT || blockIdx.x < full;
+    const uint64_t full = COMPACT ? ntiles : n / kBinTile;    // T
+    const bool interleave = COMPACT || blk < full;
     if constexpr (COMPACT) {
-        if (tid == 0) count[blockIdx.x] = kept_n;
+        if (tid == 0) count[blk] = kept_n;
         for (uint32_t srt = kept_n + tid; srt < kBinTile; srt += kBinThreads)        // the padding
-            rec[((srt / kpk) * full + blockIdx.x) * kpk + srt % kpk] = make_uint4(0u, 0u, 0u, static_cast<uint32_t>(n));
+            rec[((srt / kpk) * full + blk) * kpk + srt % kpk] = make_uint4(0u, 0u, 0u, static_cast<uint32_t>(n));
     }
 #pragma unroll
     for (uint32_t r = 0; r < kBinItems; ++r) {
         const uint64_t i = base + r * kBinThreads + tid;
         const uint32_t srt = IDENT ? r * kBinThreads + tid : h[bin_of(L[r], o[r])] + slot[r];   // rank inside the tile
-        const uint64_t dst = (interleave && !IDENT) ? ((srt / kpk) * full + blockIdx.x) * kpk + srt % kpk : base + srt;
+        const uint64_t dst = (interleave && !IDENT) ? ((srt / kpk) * full + blk) * kpk + srt % kpk : base + srt;
         if (kept(r)) {
             if constexpr (VERIFY) {
                 rec[2 * dst] = make_uint4(L[r], static_cast<uint32_t>(o[r]), static_cast<uint32_t>(o[r] >> 32), slot_off[i]);
@@ -822,6 +822,35 @@ __global__ void __launch_bounds__(kBinThreads) bin_tile_kernel(const uint32_t* l
             }
         }
     }
+}
+
+template <bool VERIFY, bool COMPACT = false, bool IDENT = false>
+__global__ void __launch_bounds__(kBinThreads) bin_tile_kernel(const uint32_t* len, const uint64_t* off, uint64_t n,
+                                                               uint32_t kpk, const uint32_t* slot_off,
+                                                               const uint32_t* connect, uint4* rec, uint32_t small,
+                                                               uint32_t* count) {
+    bin_tile_body<VERIFY, COMPACT, IDENT>(blockIdx.x, gridDim.x, len, off, n, kpk, slot_off, connect, rec, small, count);
+}
+
+// The binned gather's first launch: blocks [0, pj) run the split join's pre-join
+// (gather_join.hpp, one thread per DGRAM: short segments folded, out[d] = finalize(A),
+// info[q] for the long ones), blocks [pj, pj + tiles) the compact length-binning
+// tiles of the segments.  The two need nothing from each other, so one launch
+// overlaps the pre-join's dependent loads (segFirst, then lengths and offsets, then
+// bytes) with the binning instead of running them after the records pass.
+__global__ void __launch_bounds__(kBinThreads) gather_bin_prejoin_kernel(GatherArgs ga, uint2* info, KernelTables tb,
+                                                                         uint32_t small, uint32_t pj, uint32_t kpk,
+                                                                         uint4* rec, uint32_t* count) {
+    if (blockIdx.x >= pj) {
+        bin_tile_body<false, true>(blockIdx.x - pj, gridDim.x - pj, ga.seg_len, ga.seg_off, ga.segs, kpk, nullptr,
+                                   nullptr, rec, small, count);
+        return;
+    }
+    __shared__ uint32_t t4[4][256];
+    fill_t4<kBinThreads>(t4, tb.image);
+    for (uint64_t d = static_cast<uint64_t>(blockIdx.x) * kBinThreads + threadIdx.x; d < ga.n;
+         d += static_cast<uint64_t>(pj) * kBinThreads)
+        gather_prejoin_dgram(ga, info, tb, small, d, t4);
 }
 
 size_t length_bin_workspace(uint64_t n, bool verify) { return (verify ? 32u : 16u) * n; }
@@ -857,6 +886,18 @@ int length_bin_compact(const uint32_t* len, const uint64_t* off, uint64_t n, uin
     const unsigned tiles = static_cast<unsigned>((n + kBinTile - 1) / kBinTile);
     hipLaunchKernelGGL((bin_tile_kernel<false, true>), dim3(tiles), dim3(kBinThreads), 0, st, len, off, n, kpk, nullptr,
                        nullptr, static_cast<uint4*>(records), small, counts);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : -static_cast<int>(e);
+}
+
+int gather_bin_prejoin(const GatherArgs& ga, uint2* info, const KernelTables& tb, uint32_t small, uint32_t kpk,
+                       void* records, uint32_t* counts, unsigned prejoin_blocks, hipStream_t st) {
+    if (ga.segs > 0xFFFFFFFFull || (ga.segs && (!records || !counts)) || kpk == 0 || kBinTile % kpk ||
+        prejoin_blocks == 0)
+        return -static_cast<int>(hipErrorInvalidValue);
+    const unsigned tiles = static_cast<unsigned>((ga.segs + kBinTile - 1) / kBinTile);
+    hipLaunchKernelGGL(gather_bin_prejoin_kernel, dim3(prejoin_blocks + tiles), dim3(kBinThreads), 0, st, ga, info, tb,
+                       small, prejoin_blocks, kpk, static_cast<uint4*>(records), counts);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : -static_cast<int>(e);
 }

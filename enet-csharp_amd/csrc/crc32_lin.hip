@@ -286,10 +286,10 @@ __global__ void __launch_bounds__(64 * kLnW) crc32_lin_kernel(VrBatches bl, cons
         const VrBatch B = batch(b);
         const uint64_t p0 = (u - B.g0) * kLnPk, pl = B.n - 1u;
         const uint64_t oa = reinterpret_cast<uint64_t>(B.off), la = reinterpret_cast<uint64_t>(B.len);
-        const uint64_t q0 = min<uint64_t>(p0 + (lane >> 1), pl), q1 = min<uint64_t>(p0 + 32u + (lane >> 1), pl);
+        const uint64_t q0 = umin64(p0 + (lane >> 1), pl), q1 = umin64(p0 + 32u + (lane >> 1), pl);
         ln_dma4(oa + 8u * q0 + 4u * (lane & 1u), mb);
         ln_dma4(oa + 8u * q1 + 4u * (lane & 1u), mb + 256u);
-        ln_dma4(la + 4u * min<uint64_t>(p0 + lane, pl), mb + 512u);
+        ln_dma4(la + 4u * umin64(p0 + lane, pl), mb + 512u);
     };
     // the unit from its landed metadata: span, tiles, fast or not, lane values
     auto describe = [&](uint32_t b, uint64_t u, uint32_t mb, Unit& un, uint32_t& sr, uint32_t& er,
@@ -297,7 +297,7 @@ __global__ void __launch_bounds__(64 * kLnW) crc32_lin_kernel(VrBatches bl, cons
         const VrBatch B = batch(b);
         un.b = b;
         un.p0 = (u - B.g0) * kLnPk;
-        un.np = static_cast<uint32_t>(min<uint64_t>(kLnPk, B.n - un.p0));
+        un.np = static_cast<uint32_t>(umin64(kLnPk, B.n - un.p0));
         const uint32_t np = un.np;
         const uint32_t li = min(lane, np - 1u);
         const uint64_t off = static_cast<uint64_t>(lds_load(mb + 8u * li)) |

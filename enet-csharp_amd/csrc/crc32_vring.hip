@@ -382,6 +382,65 @@ __device__ __forceinline__ constexpr uint32_t vr_col_const() {
     [d0] "=&v"(d[0]), [d1] "=&v"(d[1]), [d2] "=&v"(d[2]), [d3] "=&v"(d[3]), [d4] "=&v"(d[4]),    \
         [d5] "=&v"(d[5]), [d6] "=&v"(d[6]), [d7] "=&v"(d[7]), [t0] "=&v"(t0), [t1] "=&v"(t1)
 
+// The same preparation IN PLACE on a landed slot (round 5): the register XORed into
+// the slot's dword 0 or 4 (hs), then the two swap rounds as v_swap_b32 under EXEC
+// masks -- lanes with bit 2 of l5 swap dwords q <-> q ^ 1, lanes with bit 3 swap
+// q <-> q ^ 2 -- so the fold reads the slot registers themselves (vr_slot_values):
+// 1 + 2 VALU + 8 swaps against vr_shuffle_slot's 25 VALU with 8 result copies.  The
+// masks are the lane patterns of those bits (0xF0 and 0xFF00 repeated); EXEC is
+// restored before the block ends (the fold runs on whole waves).  Only a landed slot
+// may be written (tools/isa_inflight_check.py checks every path).
+#define VR_ROTATE_ASM(S0, S1, S2, S3, S4, S5, S6, S7)                                             \
+    "v_bfe_i32 %[t0], %[lane], 4, 1\n\t"                      /* hs */                                \
+    "v_bitop3_b32 " S0 ", " S0 ", %[reg], %[t0] bitop3:0xb4\n\t" /* A.x ^= reg & ~hs */             \
+    "v_bitop3_b32 " S4 ", " S4 ", %[reg], %[t0] bitop3:0x78\n\t" /* B.x ^= reg & hs */              \
+    "s_mov_b64 %[sv], exec\n\t"                                                                        \
+    "s_and_b32 exec_lo, exec_lo, 0xf0f0f0f0\n\t"              /* m1 lanes */                          \
+    "s_and_b32 exec_hi, exec_hi, 0xf0f0f0f0\n\t"                                                       \
+    "v_swap_b32 " S0 ", " S1 "\n\t"                                                                    \
+    "v_swap_b32 " S2 ", " S3 "\n\t"                                                                    \
+    "v_swap_b32 " S4 ", " S5 "\n\t"                                                                    \
+    "v_swap_b32 " S6 ", " S7 "\n\t"                                                                    \
+    "s_mov_b64 exec, %[sv]\n\t"                                                                        \
+    "s_and_b32 exec_lo, exec_lo, 0xff00ff00\n\t"              /* m2 lanes */                          \
+    "s_and_b32 exec_hi, exec_hi, 0xff00ff00\n\t"                                                       \
+    "v_swap_b32 " S0 ", " S2 "\n\t"                                                                    \
+    "v_swap_b32 " S1 ", " S3 "\n\t"                                                                    \
+    "v_swap_b32 " S4 ", " S6 "\n\t"                                                                    \
+    "v_swap_b32 " S5 ", " S7 "\n\t"                                                                    \
+    "s_mov_b64 exec, %[sv]"
+template <int SLOT>
+__device__ __forceinline__ void vr_rotate_slot(uint32_t reg, uint32_t lane, uint32_t (&d)[8]) {
+    uint32_t t0;
+    uint64_t sv;
+    if constexpr (SLOT == 0) {
+        asm volatile(VR_ROTATE_ASM("v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55")
+                     : [t0] "=&v"(t0), [sv] "=&s"(sv) : [reg] "v"(reg), [lane] "v"(lane)
+                     : "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "memory");
+        asm volatile("" : "={v48}"(d[0]), "={v49}"(d[1]), "={v50}"(d[2]), "={v51}"(d[3]), "={v52}"(d[4]),
+                          "={v53}"(d[5]), "={v54}"(d[6]), "={v55}"(d[7]));
+    } else {
+        asm volatile(VR_ROTATE_ASM("v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63")
+                     : [t0] "=&v"(t0), [sv] "=&s"(sv) : [reg] "v"(reg), [lane] "v"(lane)
+                     : "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "memory");
+        asm volatile("" : "={v56}"(d[0]), "={v57}"(d[1]), "={v58}"(d[2]), "={v59}"(d[3]), "={v60}"(d[4]),
+                          "={v61}"(d[5]), "={v62}"(d[6]), "={v63}"(d[7]));
+    }
+}
+
+template <int SLOT>
+__device__ __forceinline__ void vr_shuffle_slot(uint32_t reg, uint32_t lane, uint32_t (&d)[8]);
+// true: the fold reads the slot registers rotated in place (vr_rotate_slot); false: the
+// round-2 copies (vr_shuffle_slot)
+constexpr bool kVrRotateInPlace = true;
+// (IP = false: the records instance's record-order diagnostics (ABL 64), which spill
+// 8 bytes with the in-place form)
+template <int SLOT, bool IP = true>
+__device__ __forceinline__ void vr_prepare(uint32_t reg, uint32_t lane, uint32_t (&d)[8]) {
+    if constexpr (kVrRotateInPlace && IP) vr_rotate_slot<SLOT>(reg, lane, d);
+    else vr_shuffle_slot<SLOT>(reg, lane, d);
+}
+
 template <int SLOT>
 __device__ __forceinline__ void vr_shuffle_slot(uint32_t reg, uint32_t lane, uint32_t (&d)[8]) {
     uint32_t t0, t1;
@@ -429,6 +488,66 @@ __device__ __forceinline__ uint32_t vr_lookups(const uint32_t (&d)[8], const VrS
     });
     __builtin_amdgcn_sched_barrier(0);
     reduce(7);
+    return acc;
+}
+
+// The fused fold of a landed slot (round 5, the product instances): vr_rotate_slot's
+// in-place preparation, then vr_lookups' 32 lookups reading the slot registers
+// themselves, in ONE asm block -- with the fold in C++ the compiler copied the 8
+// rotated slot registers out first (its operands must be registers it allocates).
+// Same schedule as vr_lookups: group g's four lookups issued, then group g-1's four
+// reduced after a counted lgkmcnt(4) (LDS returns in order), at most 8 in flight.
+#define VR_LK(S, C, T0, T1, T2, T3)                                                               \
+    "v_perm_b32 " T0 ", " S ", " C ", %[s0]\n\t"                                                  \
+    "v_perm_b32 " T1 ", " S ", " C ", %[s1]\n\t"                                                  \
+    "v_perm_b32 " T2 ", " S ", " C ", %[s2]\n\t"                                                  \
+    "v_perm_b32 " T3 ", " S ", " C ", %[s3]\n\t"                                                  \
+    "ds_read_b32 " T0 ", " T0 "\n\t"                                                             \
+    "ds_read_b32 " T1 ", " T1 "\n\t"                                                             \
+    "ds_read_b32 " T2 ", " T2 "\n\t"                                                             \
+    "ds_read_b32 " T3 ", " T3 "\n\t"
+#define VR_RED(T0, T1, T2, T3)                                                                    \
+    "v_bitop3_b32 %[acc], %[acc], " T0 ", " T1 " bitop3:0x96\n\t"                                 \
+    "v_bitop3_b32 %[acc], %[acc], " T2 ", " T3 " bitop3:0x96\n\t"
+#define VR_LKX(...) VR_LK(__VA_ARGS__)
+#define VR_REDX(...) VR_RED(__VA_ARGS__)
+#define VR_TA "%[a0]", "%[a1]", "%[a2]", "%[a3]"
+#define VR_TB "%[b0]", "%[b1]", "%[b2]", "%[b3]"
+#define VR_FOLD_ASM(S0, S1, S2, S3, S4, S5, S6, S7)                                               \
+    VR_ROTATE_ASM(S0, S1, S2, S3, S4, S5, S6, S7) "\n\t"                                          \
+    VR_LKX(S0, "%[c0]", VR_TA)                                                                      \
+    VR_LKX(S1, "%[c1]", VR_TB)                                                                      \
+    "s_waitcnt lgkmcnt(4)\n\t"                                                                     \
+    "v_bitop3_b32 %[acc], %[a0], %[a1], %[a2] bitop3:0x96\n\t"                                     \
+    "v_xor_b32 %[acc], %[acc], %[a3]\n\t"                                                          \
+    VR_LKX(S2, "%[c2]", VR_TA) "s_waitcnt lgkmcnt(4)\n\t" VR_REDX(VR_TB)                             \
+    VR_LKX(S3, "%[c3]", VR_TB) "s_waitcnt lgkmcnt(4)\n\t" VR_REDX(VR_TA)                             \
+    VR_LKX(S4, "%[c4]", VR_TA) "s_waitcnt lgkmcnt(4)\n\t" VR_REDX(VR_TB)                             \
+    VR_LKX(S5, "%[c5]", VR_TB) "s_waitcnt lgkmcnt(4)\n\t" VR_REDX(VR_TA)                             \
+    VR_LKX(S6, "%[c6]", VR_TA) "s_waitcnt lgkmcnt(4)\n\t" VR_REDX(VR_TB)                             \
+    VR_LKX(S7, "%[c7]", VR_TB) "s_waitcnt lgkmcnt(4)\n\t" VR_REDX(VR_TA)                             \
+    "s_waitcnt lgkmcnt(0)\n\t" VR_REDX(VR_TB)
+template <int SLOT>
+__device__ __forceinline__ uint32_t vr_fold_slot(uint32_t reg, uint32_t lane, const VrSched& s) {
+    uint32_t acc, t0, a0, a1, a2, a3, b0, b1, b2, b3;
+    uint64_t sv;
+    const uint32_t c0 = vr_col_const<0>() ^ s.cl, c1 = vr_col_const<1>() ^ s.cl, c2 = vr_col_const<2>() ^ s.cl,
+                   c3 = vr_col_const<3>() ^ s.cl, c4 = vr_col_const<4>() ^ s.cl, c5 = vr_col_const<5>() ^ s.cl,
+                   c6 = vr_col_const<6>() ^ s.cl, c7 = vr_col_const<7>() ^ s.cl;
+    const uint32_t s0 = s.sel0, s1 = s.sel0 ^ 0x101u, s2 = s.sel0 ^ 0x202u, s3 = s.sel0 ^ 0x303u;
+#define VR_FOLD_OPERANDS                                                                                 \
+    : [acc] "=&v"(acc), [t0] "=&v"(t0), [sv] "=&s"(sv), [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2),   \
+      [a3] "=&v"(a3), [b0] "=&v"(b0), [b1] "=&v"(b1), [b2] "=&v"(b2), [b3] "=&v"(b3)                     \
+    : [reg] "v"(reg), [lane] "v"(lane), [c0] "v"(c0), [c1] "v"(c1), [c2] "v"(c2), [c3] "v"(c3),           \
+      [c4] "v"(c4), [c5] "v"(c5), [c6] "v"(c6), [c7] "v"(c7), [s0] "v"(s0), [s1] "v"(s1), [s2] "v"(s2),   \
+      [s3] "v"(s3)
+    if constexpr (SLOT == 0)
+        asm volatile(VR_FOLD_ASM("v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55") VR_FOLD_OPERANDS
+                     : "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "memory");
+    else
+        asm volatile(VR_FOLD_ASM("v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63") VR_FOLD_OPERANDS
+                     : "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "memory");
+#undef VR_FOLD_OPERANDS
     return acc;
 }
 
@@ -519,8 +638,12 @@ __device__ __forceinline__ uint32_t vr_round_chunk(uint32_t r) {
                      "ds_read_b64 %0, %1\n\t"
                      "s_waitcnt lgkmcnt(0)"
                      : "=&v"(tc), "=&v"(a) : "s"(e) : "memory");
-        if (__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(tc)) == r)
-            return __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(tc >> 32));
+        const uint32_t tag = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(tc));
+        if (tag == r) return __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(tc >> 32));
+        // a tag past r means round r's entry was overwritten (64 rounds later) before
+        // this wave read it: the interleaving the host-side model excludes.  Fail loudly
+        // instead of polling forever (~0u = the unpublished sentinel)
+        if (tag != ~0u && tag - r - 1u < 0x7FFFFFFFu) __builtin_trap();
         __builtin_amdgcn_s_sleep(1);
     }
 }
@@ -649,7 +772,7 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
             uint32_t mm = 0;
 #pragma unroll
             for (uint32_t w = 0; w < kVrW; ++w) mm = max(mm, lds_load(vr_tile_max<BIN>() + 4u * w));
-            const uint32_t r = (mm + kPk - 1u) / kPk;
+            const uint32_t r = __builtin_amdgcn_readfirstlane((mm + kPk - 1u) / kPk);   // (uniform: SGPRs)
             ngroups_all = static_cast<uint64_t>(r) * bl.tiles;
             n0 = ngroups_all * kPk;
         }
@@ -706,12 +829,12 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
                 // the pair's dynamic chunks: p + j H for j >= 2 kStatic, below the launch's chunks
                 const uint64_t H = G >> 1, pp = blockIdx.x % H;
                 const uint64_t jn = chunks > pp ? (chunks - pp + H - 1u) / H : 0u;
-                const uint32_t c = vr_claim_next(jn > 2u * kStatic ? static_cast<uint32_t>(min<uint64_t>(jn - 2u * kStatic, ~0u - 1u)) : 0u);
-                vr_round_publish(r + 1u, c == ~0u ? c : static_cast<uint32_t>(min<uint64_t>(pp + (2u * kStatic + c) * H, ~0u - 1u)));
+                const uint32_t c = vr_claim_next(jn > 2u * kStatic ? static_cast<uint32_t>(umin64(jn - 2u * kStatic, ~0u - 1u)) : 0u);
+                vr_round_publish(r + 1u, c == ~0u ? c : static_cast<uint32_t>(umin64(pp + (2u * kStatic + c) * H, ~0u - 1u)));
             } else {
                 // (the launch's dynamic chunks: its chunks past the kStatic G static ones)
                 const uint64_t stat = G * kStatic;
-                const uint32_t c = vr_claim_next(chunks > stat ? static_cast<uint32_t>(min<uint64_t>(chunks - stat, ~0u - 1u)) : 0u);
+                const uint32_t c = vr_claim_next(chunks > stat ? static_cast<uint32_t>(umin64(chunks - stat, ~0u - 1u)) : 0u);
                 vr_round_publish(r + 1u, c == ~0u ? c : static_cast<uint32_t>(G) * kStatic + c);   // kStatic G + c
             }
         }
@@ -770,8 +893,8 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
         // lane l loads field f = l / kPk of packet l % kPk (lanes past the fields: field
         // 0), the packet clamped to the batch's last (always a valid address; the
         // prologue of a wave with no group at all loads batch 0's last packet)
-        const uint64_t bn = max<uint64_t>(batch_n(it.b), 1u);   // (no kept record at all: record 0, unused)
-        const uint64_t base = min<uint64_t>(group_base(it), bn - 1u);
+        const uint64_t bn = umax64(batch_n(it.b), 1u);   // (no kept record at all: record 0, unused)
+        const uint64_t base = umin64(group_base(it), bn - 1u);
         const uint64_t left = bn - 1u - base;                // (uniform: scalar select, no VALU)
         const uint32_t l = vr_lane();                       // (recomputed: not a register held across the loop)
         uint32_t f = l / kPk;
@@ -896,8 +1019,21 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
         const uint32_t a1 = (ABL & 8) ? a0 + 16u * P : q0 + 16u - hs16;
         const uint32_t lz = plz();
         const uint64_t ws = pws();
-        const uint64_t s0 = (a0 < pe && a0 + 16u > lz) ? ws + a0 : zero;
-        const uint64_t s1 = (a1 < pe && a1 + 16u > lz) ? ws + a1 : zero;
+        // An interior stage -- window stage >= 1 (past every head piece: lz < 64 <= 32 P)
+        // and ending at or before the packet's end in every lane -- has no piece outside
+        // [lz, pe): its addresses skip the zero-line selects (wave-uniform branch; about
+        // 18 of the stage's VALU, round 5)
+        const uint32_t wst = stage_of(pst, pstages);
+        constexpr bool kFast = !(ABL & (8 | 64));           // (not the line-shaped / record-order diagnostics)
+        const bool inner = !pdone && wst >= 1u && 32u * P * (wst + 1u) <= pe;
+        uint64_t s0, s1;
+        if (kFast && __builtin_amdgcn_ballot_w64(!inner) == 0u) {
+            s0 = ws + a0;
+            s1 = ws + a1;
+        } else {
+            s0 = (a0 < pe && a0 + 16u > lz) ? ws + a0 : zero;
+            s1 = (a1 < pe && a1 + 16u > lz) ? ws + a1 : zero;
+        }
         const bool meta = (pst == 0u) & qlive & !pdone;     // (one branch, no short-circuit flow blocks)
         if (meta) {
             load_meta(qit);
@@ -1049,7 +1185,22 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
         const uint32_t cst = stage_of(cs, cstages);          // the window stage this step folds
         const bool tail_first = kRot && cs == 0u && cstages > 1u;   // (wave-uniform)
         const uint32_t rin = tail_first ? 0u : reg;
-        uint32_t d[8];
+        // the fold of the landed slot S: the fused asm (product instances), or the
+        // rotation then the C++ lookups (diagnostics ablations), or -- receive verify's
+        // edge stages, whose slot fix-up works on copies -- the copies' fold
+        // (not in the verify diagnostics -- tail first, pair rounds, trace -- which then spill)
+        constexpr bool kFused = kVrRotateInPlace && !(ABL & (2 | 64)) && !(VF && (kRot || DYN == 2 || TR));
+        auto fold = [&]() __attribute__((always_inline)) -> uint32_t {
+            if constexpr (kFused) {
+                return vr_fold_slot<S>(rin, lane, make_vr_sched(lane));
+            } else {
+                uint32_t d[8];
+                vr_prepare<S, !(ABL & 64)>(rin, lane, d);
+                if constexpr (ABL & 2) return xor3(xor3(d[0], d[1], d[2]), xor3(d[3], d[4], d[5]), d[6] ^ d[7]);
+                else return vr_lookups(d, make_vr_sched(lane));
+            }
+        };
+        uint32_t nr;
         if (cs == nedge) {                                   // head / tail pieces: keep [clz, ce) only
             const uint32_t q0 = 32u * (lane_k() + P * cst);              // windows < 2 GiB: differences fit int32
             if constexpr (VF) {                              // masked in place, then the slot fix-up on copies
@@ -1059,21 +1210,19 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
                 vr_read_stage<S>(A, B);
                 if (cps != ~0u) vr_slot_fix(A, B, make_vr_sched(lane).hs, static_cast<int32_t>(cps - q0), cconn, desired);
                 nedge = next_edge_m(cs + 1u);
+                uint32_t d[8];
                 vr_shuffle(rin, lane, A, B, d);
+                if constexpr (ABL & 2) nr = xor3(xor3(d[0], d[1], d[2]), xor3(d[3], d[4], d[5]), d[6] ^ d[7]);
+                else nr = vr_lookups(d, make_vr_sched(lane));
             } else {                                         // masked in place, then folded as any stage
                 if constexpr (!(ABL & 1))
                     vr_edge_mask_slot<S>(lane & 16u, static_cast<int32_t>(clz - q0), static_cast<int32_t>(ce - q0));
                 nedge = next_edge_m(cs + 1u);
-                vr_shuffle_slot<S>(rin, lane, d);
+                nr = fold();
             }
         } else {
-            vr_shuffle_slot<S>(rin, lane, d);
+            nr = fold();
         }
-        uint32_t nr;
-        if constexpr (ABL & 2)
-            nr = xor3(xor3(d[0], d[1], d[2]), xor3(d[3], d[4], d[5]), d[6] ^ d[7]);
-        else
-            nr = vr_lookups(d, make_vr_sched(lane));
         const bool inw = 32u * (lane_k() + P * cst) < ce;           // the lane's block k + P cst is in the window
         if (tail_first) rt = inw ? nr : 0u;
         else reg = inw ? nr : reg;
@@ -1151,13 +1300,15 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
 // the instance; dyn = its dynamic-rounds twin where one is built
 template <int LG, int TR = 0, int NT = 0, int ABL = 0, int BIN = 0, int WK = 0, int ROT = 0, int VF = 0>
 const void* vring_fn(int dyn = 0) {
+    // (the dynamic-round twins are diagnostics: the product library's contexts never set
+    // vr_dynamic, so it builds none -- ADVICE r4)
+#ifdef ENET_HIP_DIAG
     if constexpr (TR != 1 && NT == 0 && ABL == 0 && WK == 0 && ROT == 0) {
         if (dyn == 1) return reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT, VF, 1>);
-#ifdef ENET_HIP_DIAG
         if constexpr (!BIN)                                  // (pair rounds: not for the records instance)
             if (dyn == 2) return reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT, VF, 2>);
-#endif
     }
+#endif
     return dyn == 0 ? reinterpret_cast<const void*>(crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT, VF>) : nullptr;
 }
 // the dynamic-round mode a variant selects (0: the static deal)

@@ -42,9 +42,65 @@ constexpr uint32_t kMaximumPeerId = 0xFFF;    // ENET_PROTOCOL_MAXIMUM_PEER_ID
 int neg_errno() { return -(ENET_HIP_ERRNO_BASE + (errno ? errno : EIO)); }
 constexpr int kBadArg = -1;                   // -hipErrorInvalidValue, as every entry point
 
+// sendmmsg over DGRAM gather lists: DGRAM d = segments segFirst[d] .. segFirst[d+1]-1,
+// segment s at seg(s) (a pointer), segLengths[s] bytes; 256 DGRAMs per call.
+template <class Seg>
+int send_lists(int fd, Seg seg, const uint32_t* segLengths, const uint32_t* segFirst, size_t dgramCount,
+               uint32_t dstAddr, uint16_t dstPort, size_t* sent) {
+    sockaddr_in to{};
+    to.sin_family = AF_INET;
+    to.sin_addr.s_addr = htonl(dstAddr);
+    to.sin_port = htons(dstPort);
+    std::vector<mmsghdr> msgs(kMmsgBatch);
+    std::vector<iovec> iov(kMmsgBatch * kMaxSegments);
+    size_t done = 0;
+    while (done < dgramCount) {
+        const size_t want = std::min(kMmsgBatch, dgramCount - done);
+        for (size_t i = 0; i < want; ++i) {
+            const size_t d = done + i;
+            const uint32_t s0 = segFirst[d], s1 = segFirst[d + 1];
+            if (s1 < s0 || s1 - s0 > kMaxSegments) return kBadArg;
+            iovec* v = &iov[i * kMaxSegments];
+            for (uint32_t s = s0; s < s1; ++s) {
+                v[s - s0].iov_base = const_cast<uint8_t*>(seg(s));
+                v[s - s0].iov_len = segLengths[s];
+            }
+            memset(&msgs[i].msg_hdr, 0, sizeof(msghdr));
+            msgs[i].msg_hdr.msg_iov = v;
+            msgs[i].msg_hdr.msg_iovlen = s1 - s0;
+            msgs[i].msg_hdr.msg_name = &to;
+            msgs[i].msg_hdr.msg_namelen = sizeof(to);
+        }
+        const int r = sendmmsg(fd, msgs.data(), static_cast<unsigned>(want), 0);
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            if (errno == EAGAIN || errno == EWOULDBLOCK || errno == ENOBUFS) break;   // socket buffer full
+            *sent = done;
+            return neg_errno();
+        }
+        done += static_cast<size_t>(r);
+        if (r == 0) break;
+    }
+    *sent = done;
+    return 0;
+}
+
 }  // namespace
 
+// (host_io.hpp) the same with every segment given as a pointer: the compressing send
+// pipeline (host_pipeline.hip) mixes the caller's arena and its compressed bytes
+int enethip_udp_send_ptrs(int fd, const uint8_t* const* segPtrs, const uint32_t* segLengths, const uint32_t* segFirst,
+                          size_t dgramCount, uint32_t dstAddr, uint16_t dstPort, size_t* sent) {
+    if (!sent) return kBadArg;
+    *sent = 0;
+    if (dgramCount == 0) return 0;
+    if (fd < 0 || !segFirst || (segFirst[dgramCount] > segFirst[0] && (!segPtrs || !segLengths))) return kBadArg;
+    return send_lists(fd, [&](uint32_t s) { return segPtrs[s]; }, segLengths, segFirst, dgramCount, dstAddr, dstPort,
+                      sent);
+}
+
 extern "C" {
+
 
 int enet_hip_udp_receive(int fd, uint8_t* arena, size_t stride, size_t maxDgrams, uint32_t* lengths,
                          uint32_t* srcAddr, uint16_t* srcPort, int timeoutMs, size_t* received) {
@@ -132,42 +188,8 @@ int enet_hip_udp_send(int fd, const uint8_t* bytes, const uint64_t* segOffsets, 
     if (dgramCount == 0) return 0;
     if (fd < 0 || !bytes || !segFirst || (segFirst[dgramCount] > segFirst[0] && (!segOffsets || !segLengths)))
         return kBadArg;
-    sockaddr_in to{};
-    to.sin_family = AF_INET;
-    to.sin_addr.s_addr = htonl(dstAddr);
-    to.sin_port = htons(dstPort);
-    std::vector<mmsghdr> msgs(kMmsgBatch);
-    std::vector<iovec> iov(kMmsgBatch * kMaxSegments);
-    size_t done = 0;
-    while (done < dgramCount) {
-        const size_t want = std::min(kMmsgBatch, dgramCount - done);
-        for (size_t i = 0; i < want; ++i) {
-            const size_t d = done + i;
-            const uint32_t s0 = segFirst[d], s1 = segFirst[d + 1];
-            if (s1 < s0 || s1 - s0 > kMaxSegments) return kBadArg;
-            iovec* v = &iov[i * kMaxSegments];
-            for (uint32_t s = s0; s < s1; ++s) {
-                v[s - s0].iov_base = const_cast<uint8_t*>(bytes + segOffsets[s]);
-                v[s - s0].iov_len = segLengths[s];
-            }
-            memset(&msgs[i].msg_hdr, 0, sizeof(msghdr));
-            msgs[i].msg_hdr.msg_iov = v;
-            msgs[i].msg_hdr.msg_iovlen = s1 - s0;
-            msgs[i].msg_hdr.msg_name = &to;
-            msgs[i].msg_hdr.msg_namelen = sizeof(to);
-        }
-        const int r = sendmmsg(fd, msgs.data(), static_cast<unsigned>(want), 0);
-        if (r < 0) {
-            if (errno == EINTR) continue;
-            if (errno == EAGAIN || errno == EWOULDBLOCK || errno == ENOBUFS) break;   // socket buffer full
-            *sent = done;
-            return neg_errno();
-        }
-        done += static_cast<size_t>(r);
-        if (r == 0) break;
-    }
-    *sent = done;
-    return 0;
+    return send_lists(fd, [&](uint32_t s) { return bytes + segOffsets[s]; }, segLengths, segFirst, dgramCount,
+                      dstAddr, dstPort, sent);
 }
 
 int enet_hip_stamp_callback(uint8_t* bytes, const uint64_t* segOffsets, const uint32_t* segLengths,

@@ -99,6 +99,26 @@ std::vector<Chunk> plan_chunks(const uint64_t* off, const uint32_t* len, size_t 
     return ch;
 }
 
+constexpr uint32_t kHeaderFlagCompressed = 1u << 14, kHeaderFlagSentTime = 1u << 15;   // include/protocol.cs
+constexpr uint32_t kRecvBuffer = 4096;                     // ENet's receive buffer (protocol.cs:1038-1044)
+
+// Compressed DGRAM j of a receive batch (arena row rows[j], hsz[j] = header + slot
+// bytes): the header copied in front of its decompressed body in plain row j, and row
+// rows[j]'s offset / length in the verify batch -- length 0 (no slot: ok = 0) when the
+// decompression failed or needed more than 4096 - hsz bytes (protocol.cs:1042-1043).
+__global__ void rc_fix_kernel(uint8_t* d, const uint32_t* rows, const uint32_t* hsz, uint32_t k, uint64_t pitch,
+                              uint64_t plain, const uint32_t* outLen, uint64_t* off, uint32_t* len) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= k) return;
+    const uint32_t i = rows[j], h = hsz[j];
+    const uint8_t* src = d + pitch * i;
+    uint8_t* dst = d + plain + static_cast<uint64_t>(kRecvBuffer) * j;
+    for (uint32_t b = 0; b < h; ++b) dst[b] = src[b];      // protocol.cs:1045 memcpy(packetData[1], header, headerSize)
+    const uint32_t L = outLen[j];
+    off[i] = plain + static_cast<uint64_t>(kRecvBuffer) * j;
+    len[i] = (L > 0u && L <= kRecvBuffer - h) ? h + L : 0u;
+}
+
 }  // namespace
 }  // namespace enethip
 
@@ -315,6 +335,227 @@ int enet_hip_udp_receive_verify(enet_hip_context* ctx, int fd, uint8_t* arena, s
     for (size_t i = 0; i < n; ++i)
         if (h_verdict[i] != ENET_HIP_DGRAM_CHECKSUM) ok[i] = 0;
     return 0;
+}
+
+int enet_hip_udp_receive_decompress_verify(enet_hip_context* ctx, int fd, uint8_t* arena, size_t stride,
+                                           size_t maxDgrams, const uint32_t* peerConnectIds, size_t peerCount,
+                                           int timeoutMs, uint32_t* lengths, uint8_t* ok, size_t* received) {
+    if (!ctx || !received) return -static_cast<int>(hipErrorInvalidValue);
+    *received = 0;
+    if (!arena || !lengths || !ok || (peerCount && !peerConnectIds) || stride < kRecvBuffer)
+        return -static_cast<int>(hipErrorInvalidValue);
+    size_t n = 0;
+    int rc = enet_hip_udp_receive(fd, arena, stride, maxDgrams, lengths, nullptr, nullptr, timeoutMs, &n);
+    if (rc) return rc;                                   // -errno
+    *received = n;
+    if (n == 0) return 0;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ENH_CHECK(hipSetDevice(ctx->device));
+    if ((rc = pipeline_init(ctx))) return rc;
+    // pinned staging: off u64 | len | slot | connect | verdict, then the compressed
+    // DGRAMs' rows | hsz | inOff u64 | inLen | outOff u64 | outLim | outLen, then their
+    // decompressed rows (D2H)
+    const size_t ho = align16(8 * n), hl = align16(4 * n), hv = align16(n);
+    const size_t base = ho + 3 * hl + hv, cmeta = 2 * ho + 5 * hl;
+    if ((rc = ensure_pinned(&ctx->h_pipe[0], &ctx->h_pipe_cap[0], base + cmeta + n * kRecvBuffer))) return rc;
+    uint8_t* hp = ctx->h_pipe[0];
+    uint64_t* h_off = reinterpret_cast<uint64_t*>(hp);
+    uint32_t* h_len = reinterpret_cast<uint32_t*>(hp + ho);
+    uint32_t* h_slot = reinterpret_cast<uint32_t*>(hp + ho + hl);
+    uint32_t* h_conn = reinterpret_cast<uint32_t*>(hp + ho + 2 * hl);
+    uint8_t* h_verdict = hp + ho + 3 * hl;
+    uint32_t* h_rows = reinterpret_cast<uint32_t*>(hp + base);
+    uint32_t* h_hsz = reinterpret_cast<uint32_t*>(hp + base + hl);
+    uint64_t* h_inoff = reinterpret_cast<uint64_t*>(hp + base + 2 * hl);
+    uint32_t* h_inlen = reinterpret_cast<uint32_t*>(hp + base + 2 * hl + ho);
+    uint64_t* h_outoff = reinterpret_cast<uint64_t*>(hp + base + 3 * hl + ho);
+    uint32_t* h_outlim = reinterpret_cast<uint32_t*>(hp + base + 3 * hl + 2 * ho);
+    uint32_t* h_outlen = reinterpret_cast<uint32_t*>(hp + base + 4 * hl + 2 * ho);
+    uint8_t* h_plain = hp + base + cmeta;
+    if ((rc = enet_hip_parse_headers(arena, stride, lengths, n, peerConnectIds, peerCount, h_slot, h_conn, h_verdict)))
+        return rc;
+    // the header stage's compressed DGRAMs go to the decompressor (protocol.cs:1033-1050)
+    uint32_t k = 0;
+    size_t maxLen = 16;
+    for (size_t i = 0; i < n; ++i) {
+        if (h_verdict[i] == ENET_HIP_DROP_COMPRESSED) {
+            const uint8_t* dg = arena + i * stride;
+            const uint32_t word = (static_cast<uint32_t>(dg[0]) << 8) | dg[1];
+            const uint32_t peer = word & 0x0FFFu;
+            const uint32_t hs = (word & kHeaderFlagSentTime) ? 4u : 2u;
+            if (lengths[i] < hs + 4u) {                  // no room for the slot before the body
+                h_verdict[i] = ENET_HIP_DROP_SHORT;
+                continue;
+            }
+            h_slot[i] = hs;
+            h_conn[i] = peer == 0x0FFFu ? 0u : peerConnectIds[peer];   // (peer < peerCount: checked before)
+            h_rows[k] = static_cast<uint32_t>(i);
+            h_hsz[k] = hs + 4u;
+            ++k;
+            maxLen = std::max<size_t>(maxLen, lengths[i]);
+        } else if (h_verdict[i] == ENET_HIP_DGRAM_CHECKSUM) {
+            maxLen = std::max<size_t>(maxLen, lengths[i]);
+        }
+    }
+    const size_t pitch = align16(maxLen);
+    for (size_t i = 0; i < n; ++i) {
+        h_off[i] = i * pitch;
+        h_len[i] = h_verdict[i] == ENET_HIP_DGRAM_CHECKSUM ? lengths[i] : 0u;   // compressed: set on the device
+    }
+    const uint64_t plain = align16(n * pitch + 16);        // decompressed rows after the received ones
+    for (uint32_t j = 0; j < k; ++j) {
+        h_inoff[j] = h_rows[j] * pitch + h_hsz[j];
+        h_inlen[j] = lengths[h_rows[j]] - h_hsz[j];
+        h_outoff[j] = plain + static_cast<uint64_t>(kRecvBuffer) * j + h_hsz[j];
+        h_outlim[j] = kRecvBuffer - h_hsz[j];
+    }
+    // device: [DGRAMs at `pitch` | decompressed rows | off | len | slot | connect | ok | compressed metadata]
+    const size_t db = plain + align16(static_cast<size_t>(k) * kRecvBuffer + 16);
+    if ((rc = ensure_device(&ctx->d_pipe[0], &ctx->d_pipe_cap[0], db + base + cmeta))) return rc;
+    uint8_t* d = ctx->d_pipe[0];
+    uint64_t* d_off = reinterpret_cast<uint64_t*>(d + db);
+    uint32_t* d_len = reinterpret_cast<uint32_t*>(d + db + ho);
+    uint32_t* d_slot = reinterpret_cast<uint32_t*>(d + db + ho + hl);
+    uint32_t* d_conn = reinterpret_cast<uint32_t*>(d + db + ho + 2 * hl);
+    uint8_t* d_ok = d + db + ho + 3 * hl;
+    uint8_t* dc = d + db + base;
+    uint32_t* d_rows = reinterpret_cast<uint32_t*>(dc);
+    uint32_t* d_hsz = reinterpret_cast<uint32_t*>(dc + hl);
+    uint64_t* d_inoff = reinterpret_cast<uint64_t*>(dc + 2 * hl);
+    uint32_t* d_inlen = reinterpret_cast<uint32_t*>(dc + 2 * hl + ho);
+    uint64_t* d_outoff = reinterpret_cast<uint64_t*>(dc + 3 * hl + ho);
+    uint32_t* d_outlim = reinterpret_cast<uint32_t*>(dc + 3 * hl + 2 * ho);
+    uint32_t* d_outlen = reinterpret_cast<uint32_t*>(dc + 4 * hl + 2 * ho);
+    hipStream_t st = ctx->pipe[0];
+    ENH_CHECK(hipMemcpy2DAsync(d, pitch, arena, stride, maxLen, n, hipMemcpyHostToDevice, st));
+    ENH_CHECK(hipMemcpyAsync(d_off, h_off, ho + 3 * hl, hipMemcpyHostToDevice, st));   // off | len | slot | connect
+    if (k) {
+        ENH_CHECK(hipMemcpyAsync(dc, hp + base, cmeta - hl, hipMemcpyHostToDevice, st));   // (all but outLen)
+        if ((rc = range_coder_locked(ctx, true, d, d_inoff, d_inlen, k, d, d_outoff, d_outlim, d_outlen, st))) return rc;
+        hipLaunchKernelGGL(rc_fix_kernel, dim3((k + 255) / 256), dim3(256), 0, st, d, d_rows, d_hsz, k,
+                           static_cast<uint64_t>(pitch), plain, d_outlen, d_off, d_len);
+        ENH_CHECK(hipGetLastError());
+    }
+    if ((rc = enet_hip_verify_batch_device(ctx, d, d_off, d_len, d_slot, d_conn, n, d_ok, nullptr, st))) return rc;
+    ENH_CHECK(hipMemcpyAsync(ok, d_ok, n, hipMemcpyDeviceToHost, st));
+    if (k) {
+        ENH_CHECK(hipMemcpyAsync(h_outlen, d_outlen, 4 * k, hipMemcpyDeviceToHost, st));
+        ENH_CHECK(hipMemcpyAsync(h_plain, d + plain, static_cast<size_t>(k) * kRecvBuffer, hipMemcpyDeviceToHost, st));
+    }
+    ENH_CHECK(hipStreamSynchronize(st));
+    for (uint32_t j = 0; j < k; ++j) {                    // receivedData := the decompressed DGRAM
+        const uint32_t L = h_outlen[j], h = h_hsz[j], i = h_rows[j];
+        if (L == 0u || L > kRecvBuffer - h) continue;
+        memcpy(arena + static_cast<size_t>(i) * stride, h_plain + static_cast<size_t>(j) * kRecvBuffer, h + L);
+        lengths[i] = h + L;
+        h_verdict[i] = ENET_HIP_DGRAM_CHECKSUM;
+    }
+    for (size_t i = 0; i < n; ++i)
+        if (h_verdict[i] != ENET_HIP_DGRAM_CHECKSUM) ok[i] = 0;
+    return 0;
+}
+
+int enet_hip_udp_compress_stamp_send(enet_hip_context* ctx, int fd, uint8_t* bytes, size_t byteCount,
+                                     const uint64_t* segOffsets, const uint32_t* segLengths, size_t segCount,
+                                     const uint32_t* segFirst, const uint32_t* slotOffsets, size_t dgramCount,
+                                     uint32_t dstAddr, uint16_t dstPort, size_t* sent) {
+    if (!sent) return -static_cast<int>(hipErrorInvalidValue);
+    *sent = 0;
+    if (!ctx) return -static_cast<int>(hipErrorInvalidValue);
+    if (dgramCount == 0) return 0;
+    if (!bytes || !segOffsets || !segLengths || !segFirst || !slotOffsets) return -static_cast<int>(hipErrorInvalidValue);
+    for (size_t d = 0; d < dgramCount; ++d) {             // header + slot in the first buffer, at most 65 buffers
+        const uint32_t s0 = segFirst[d];
+        if (segFirst[d + 1] <= s0 || segFirst[d + 1] > segCount || segFirst[d + 1] - s0 > 65u ||
+            static_cast<uint64_t>(slotOffsets[d]) + 4u > segLengths[s0] || segLengths[s0] < 2u)
+            return -static_cast<int>(hipErrorInvalidValue);
+    }
+    for (size_t s = segFirst[0]; s < segFirst[dgramCount]; ++s)
+        if (segOffsets[s] > byteCount || segLengths[s] > byteCount - segOffsets[s])
+            return -static_cast<int>(hipErrorInvalidValue);
+    const size_t n = dgramCount;
+    // the commands of DGRAM d (its buffers after the first), concatenated: in[d]
+    std::vector<uint64_t> in_off(n);
+    std::vector<uint32_t> in_len(n), out_len(n);
+    uint64_t total = 0;
+    for (size_t d = 0; d < n; ++d) {
+        uint64_t L = 0;
+        for (uint32_t s = segFirst[d] + 1u; s < segFirst[d + 1]; ++s) L += segLengths[s];
+        if (L > 0xFFFFFFFFull) return -static_cast<int>(hipErrorInvalidValue);
+        in_off[d] = total;
+        in_len[d] = static_cast<uint32_t>(L);
+        total += L;
+    }
+    std::vector<uint8_t> comp(total + 16);
+    int rc;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        ENH_CHECK(hipSetDevice(ctx->device));
+        if ((rc = pipeline_init(ctx))) return rc;
+        const size_t ab = align16(total + 16), ho = align16(8 * n), hl = align16(4 * n);
+        // pinned: commands | in_off | in_len | out_len, then the compressed bytes (D2H)
+        if ((rc = ensure_pinned(&ctx->h_pipe[0], &ctx->h_pipe_cap[0], 2 * ab + ho + 2 * hl))) return rc;
+        uint8_t* hp = ctx->h_pipe[0];
+        for (size_t d = 0; d < n; ++d) {
+            uint64_t o = in_off[d];
+            for (uint32_t s = segFirst[d] + 1u; s < segFirst[d + 1]; ++s) {
+                memcpy(hp + o, bytes + segOffsets[s], segLengths[s]);
+                o += segLengths[s];
+            }
+        }
+        memcpy(hp + ab, in_off.data(), 8 * n);
+        memcpy(hp + ab + ho, in_len.data(), 4 * n);
+        // device: commands | compressed | in_off | in_len | out_len (the output offsets and
+        // limits are the input's: the reference's limit is the commands' own length)
+        if ((rc = ensure_device(&ctx->d_pipe[0], &ctx->d_pipe_cap[0], 2 * ab + ho + 2 * hl))) return rc;
+        uint8_t* d = ctx->d_pipe[0];
+        uint64_t* d_off = reinterpret_cast<uint64_t*>(d + 2 * ab);
+        uint32_t* d_len = reinterpret_cast<uint32_t*>(d + 2 * ab + ho);
+        uint32_t* d_out = reinterpret_cast<uint32_t*>(d + 2 * ab + ho + hl);
+        hipStream_t st = ctx->pipe[0];
+        ENH_CHECK(hipMemcpyAsync(d, hp, total, hipMemcpyHostToDevice, st));
+        ENH_CHECK(hipMemcpyAsync(d_off, hp + ab, ho + hl, hipMemcpyHostToDevice, st));
+        if ((rc = range_coder_locked(ctx, false, d, d_off, d_len, n, d + ab, d_off, d_len, d_out, st))) return rc;
+        ENH_CHECK(hipMemcpyAsync(hp + ab + ho + hl, d_out, 4 * n, hipMemcpyDeviceToHost, st));
+        ENH_CHECK(hipMemcpyAsync(hp + ab + ho + 2 * hl, d + ab, total, hipMemcpyDeviceToHost, st));
+        ENH_CHECK(hipStreamSynchronize(st));
+        memcpy(out_len.data(), hp + ab + ho + hl, 4 * n);
+        memcpy(comp.data(), hp + ab + ho + 2 * hl, total);
+    }
+    // protocol.cs:1670-1676: keep the compressed form only when it is shorter; the flag
+    // goes into the header before the CRC (it is part of the checksummed bytes)
+    std::vector<uint8_t> keep(n);
+    for (size_t d = 0; d < n; ++d) {
+        keep[d] = out_len[d] > 0u && out_len[d] < in_len[d];
+        if (keep[d]) bytes[segOffsets[segFirst[d]]] |= static_cast<uint8_t>(kHeaderFlagCompressed >> 8);
+    }
+    std::vector<uint32_t> crc(n);
+    if ((rc = enet_hip_crc32_gather_binned_host(ctx, bytes, byteCount, segOffsets, segLengths, segCount, segFirst, n,
+                                                crc.data())))
+        return rc;
+    for (size_t d = 0; d < n; ++d)                        // protocol.cs:1697: the slot := the CRC
+        memcpy(bytes + segOffsets[segFirst[d]] + slotOffsets[d], &crc[d], 4);
+    // protocol.cs:1700-1705: the wire form -- the first buffer, then the compressed
+    // bytes in place of the commands
+    std::vector<const uint8_t*> ptrs;
+    std::vector<uint32_t> lens, first(n + 1);
+    for (size_t d = 0; d < n; ++d) {
+        first[d] = static_cast<uint32_t>(ptrs.size());
+        const uint32_t s0 = segFirst[d];
+        ptrs.push_back(bytes + segOffsets[s0]);
+        lens.push_back(segLengths[s0]);
+        if (keep[d]) {
+            ptrs.push_back(comp.data() + in_off[d]);
+            lens.push_back(out_len[d]);
+        } else {
+            for (uint32_t s = s0 + 1u; s < segFirst[d + 1]; ++s) {
+                ptrs.push_back(bytes + segOffsets[s]);
+                lens.push_back(segLengths[s]);
+            }
+        }
+    }
+    first[n] = static_cast<uint32_t>(ptrs.size());
+    return enethip_udp_send_ptrs(fd, ptrs.data(), lens.data(), first.data(), n, dstAddr, dstPort, sent);
 }
 
 int enet_hip_udp_stamp_send(enet_hip_context* ctx, int fd, uint8_t* bytes, size_t byteCount,

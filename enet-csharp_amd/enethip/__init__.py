@@ -45,6 +45,7 @@ EXPORTED_SYMBOLS = (
     "enet_hip_range_compress_device", "enet_hip_range_decompress_device",
     "enet_hip_crc32_gather_binned_host", "enet_hip_udp_receive", "enet_hip_parse_headers", "enet_hip_udp_send",
     "enet_hip_stamp_callback", "enet_hip_verify_callback", "enet_hip_udp_receive_verify", "enet_hip_udp_stamp_send",
+    "enet_hip_udp_receive_decompress_verify", "enet_hip_udp_compress_stamp_send",
 )
 
 # include/enet_hip.h socket-harness constants
@@ -175,6 +176,11 @@ def load(path: str | None = None, diag: bool = False) -> ctypes.CDLL:
     L.enet_hip_udp_receive_verify.argtypes = [vp, i32, vp, sz, sz, vp, sz, i32, vp, vp, szp]
     L.enet_hip_udp_stamp_send.restype = i32
     L.enet_hip_udp_stamp_send.argtypes = [vp, i32, vp, sz, vp, vp, sz, vp, vp, sz, u32, ctypes.c_uint16, szp]
+    L.enet_hip_udp_receive_decompress_verify.restype = i32
+    L.enet_hip_udp_receive_decompress_verify.argtypes = [vp, i32, vp, sz, sz, vp, sz, i32, vp, vp, szp]
+    L.enet_hip_udp_compress_stamp_send.restype = i32
+    L.enet_hip_udp_compress_stamp_send.argtypes = [vp, i32, vp, sz, vp, vp, sz, vp, vp, sz, u32, ctypes.c_uint16,
+                                                   szp]
     L.enet_hip_is_diagnostics_build.restype = i32
     L.enet_hip_is_diagnostics_build.argtypes = []
     L.enet_hip_fragment_reassemble_device.restype = i32
@@ -399,6 +405,34 @@ class Context:
                                                  _u(seg_first, np.uint32), _u(slot_off, np.uint32))
         sent = ctypes.c_size_t(0)
         _check("enet_hip_udp_stamp_send", self.lib.enet_hip_udp_stamp_send(
+            self.handle, int(fd), _ptr(payload), int(payload.nbytes), _ptr(seg_off), _ptr(seg_len), len(seg_off),
+            _ptr(seg_first), _ptr(slot_off), len(seg_first) - 1, int(addr), int(port), ctypes.byref(sent)))
+        return sent.value
+
+    def udp_receive_decompress_verify(self, fd: int, arena, stride: int, max_dgrams: int, peer_connect_ids,
+                                      timeout_ms: int = 0):
+        """-> (count, lengths[count], ok[count]): as udp_receive_verify, compressed DGRAMs
+        decompressed on the GPU first (range coder) and left decompressed in their arena
+        slots with their new lengths (c/protocol.cs:1033-1068)."""
+        peers = _u(peer_connect_ids, np.uint32)
+        lens = np.zeros(max(1, max_dgrams), np.uint32)
+        ok = np.zeros(max(1, max_dgrams), np.uint8)
+        got = ctypes.c_size_t(0)
+        _check("enet_hip_udp_receive_decompress_verify", self.lib.enet_hip_udp_receive_decompress_verify(
+            self.handle, int(fd), _ptr(arena), int(stride), int(max_dgrams), _ptr(peers) if len(peers) else None,
+            len(peers), int(timeout_ms), _ptr(lens), _ptr(ok), ctypes.byref(got)))
+        n = got.value
+        return n, lens[:n], ok[:n]
+
+    def udp_compress_stamp_send(self, fd: int, payload, seg_off, seg_len, seg_first, slot_off, addr: int,
+                                port: int) -> int:
+        """GPU range compress of each DGRAM's commands, header flag where shorter, GPU
+        stamp over the uncompressed lists (payload modified in place), then sendmmsg of
+        the wire form (c/protocol.cs:1665-1705)."""
+        seg_off, seg_len, seg_first, slot_off = (_u(seg_off, np.uint64), _u(seg_len, np.uint32),
+                                                 _u(seg_first, np.uint32), _u(slot_off, np.uint32))
+        sent = ctypes.c_size_t(0)
+        _check("enet_hip_udp_compress_stamp_send", self.lib.enet_hip_udp_compress_stamp_send(
             self.handle, int(fd), _ptr(payload), int(payload.nbytes), _ptr(seg_off), _ptr(seg_len), len(seg_off),
             _ptr(seg_first), _ptr(slot_off), len(seg_first) - 1, int(addr), int(port), ctypes.byref(sent)))
         return sent.value

@@ -211,12 +211,15 @@ ENET_HIP_API int enet_hip_crc32_gather_device(enet_hip_context* ctx, const uint8
                                               void* stream);
 
 /* Same results as enet_hip_crc32_gather_device, with the segment count known on
- * the host (segCount = segFirst[dgramCount]).  Three passes on `stream`: segments
- * over 48 B (MTU payloads) sorted per tile of 1024 by length bin, their CRCs from
- * the vring kernel's records instance, then one thread per DGRAM folds the short
- * ones (headers, commands) itself and joins the long ones' CRCs with one GF(2)
- * multiply by x^(8 len) each.  `workspace`: caller-owned device memory of at
- * least enet_hip_gather_binned_workspace_size(segCount) bytes, 16-byte aligned, not
+ * the host (segCount = segFirst[dgramCount]; segFirst non-decreasing, so each
+ * segment belongs to at most one DGRAM).  Three passes on `stream`: (1) segments
+ * over 48 B (MTU payloads) sorted per tile of 1024 by length bin and, in the same
+ * launch, one thread per DGRAM folding the short ones (headers, commands) with the
+ * long ones' own registers taken as zero; (2) the long segments' CRCs from the vring
+ * kernel's records instance; (3) one thread per long segment adding its CRC, times
+ * x^(8 bytes after it), into its DGRAM's result (the CRC is affine in it).
+ * `workspace`: caller-owned device memory of at least
+ * enet_hip_gather_binned_workspace_size(segCount) bytes, 16-byte aligned, not
  * shared with a call in flight; segCount < 2^32.  Async; graph-capturable. */
 ENET_HIP_API size_t enet_hip_gather_binned_workspace_size(size_t segCount);
 ENET_HIP_API int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* bytes,
@@ -362,6 +365,36 @@ ENET_HIP_API int enet_hip_udp_stamp_send(enet_hip_context* ctx, int fd, uint8_t*
                                          const uint64_t* segOffsets, const uint32_t* segLengths, size_t segCount,
                                          const uint32_t* segFirst, const uint32_t* slotOffsets, size_t dgramCount,
                                          uint32_t dstAddr, uint16_t dstPort, size_t* sent);
+
+/* The same two pipelines for hosts that set ENet's range coder as their compressor
+ * (enet_host_compress_with_range_coder, c/compress.cs:69-943) beside the checksum.
+ *
+ * Receive (c/protocol.cs:1033-1068): a DGRAM whose header carries
+ * ENET_PROTOCOL_HEADER_FLAG_COMPRESSED is decompressed on the GPU
+ * (enet_hip_range_decompress_device) -- the body after the header and checksum slot,
+ * to at most 4096 - headerSize bytes; a result of 0 or over that limit drops the
+ * DGRAM -- the header copied in front, and the CRC verified over the DGRAM so
+ * decompressed, as the reference does on packetData[1].  Each decompressed DGRAM
+ * replaces the received one in its arena slot (stride >= 4096) and lengths[i] becomes
+ * its length (receivedData / receivedDataLength).  Uncompressed DGRAMs go as in
+ * enet_hip_udp_receive_verify.
+ *
+ * Send (c/protocol.cs:1665-1705): each DGRAM's commands (the segments after its first,
+ * which holds the header and the slot) are compressed on the GPU
+ * (enet_hip_range_compress_device, limit = their length); where the result is
+ * shorter, the header's peerID word gets ENET_PROTOCOL_HEADER_FLAG_COMPRESSED (in
+ * `bytes`), the CRC is taken over the UNCOMPRESSED gather list on the GPU and
+ * written into the slot, and the DGRAM goes out as its first segment followed by
+ * the compressed bytes.  Synchronous, both. */
+ENET_HIP_API int enet_hip_udp_receive_decompress_verify(enet_hip_context* ctx, int fd, uint8_t* arena, size_t stride,
+                                                        size_t maxDgrams, const uint32_t* peerConnectIds,
+                                                        size_t peerCount, int timeoutMs, uint32_t* lengths, uint8_t* ok,
+                                                        size_t* received);
+ENET_HIP_API int enet_hip_udp_compress_stamp_send(enet_hip_context* ctx, int fd, uint8_t* bytes, size_t byteCount,
+                                                  const uint64_t* segOffsets, const uint32_t* segLengths,
+                                                  size_t segCount, const uint32_t* segFirst,
+                                                  const uint32_t* slotOffsets, size_t dgramCount, uint32_t dstAddr,
+                                                  uint16_t dstPort, size_t* sent);
 
 /* ---- multi-GPU: independent contiguous shards, no collective ----
  * Packets [i*count/k, (i+1)*count/k) go to contexts[i], each through the pipelined

@@ -822,6 +822,36 @@ def gather_join(seg_crcs, seg_lens) -> int:
     return finalize(reg)
 
 
+
+def gather_split_join(arena: bytes, segs, small: int = 48) -> int:
+    """The split join (gather_join.hpp): the pre-join walks the DGRAM with every long
+    segment's own register R_q taken as 0 -- short segments folded (fold_small), long
+    ones reg' = (reg ^ ~0) x^(8 L) -- and records x^(8 after_q) for each long q; the
+    post-join XORs bswap(R_q x^(8 after_q)) into finalize(A) (~crc_q when after_q = 0).
+    segs = [(offset, length)] into arena."""
+    total = sum(L for _, L in segs)
+    reg, pos, pend = 0xFFFFFFFF, 0, []
+    for a, L in segs:
+        if L == 0:
+            continue
+        pos += L
+        if L <= small:
+            reg = fold_small(reg, arena, a, L)
+        else:
+            reg = 0 if reg == 0xFFFFFFFF else mulmod(reg ^ 0xFFFFFFFF, x8n(L))
+            after = total - pos
+            pend.append((a, L, x8n(after) if after else ONE))
+    out = finalize(reg)
+    for a, L, m in pend:                                     # the post-join, one segment each
+        r = 0xFFFFFFFF
+        for b in arena[a:a + L]:
+            r = t0((r ^ b) & 0xFF) ^ (r >> 8)
+        c = finalize(r)                                      # the records pass's seg_crc
+        r = ~int.from_bytes(c.to_bytes(4, "little"), "big") & 0xFFFFFFFF
+        add = (~c & 0xFFFFFFFF) if m == ONE else int.from_bytes(mulmod(r, m).to_bytes(4, "little"), "big")
+        out ^= add
+    return out
+
 def fold_small(reg: int, arena: bytes, a: int, L: int) -> int:
     """crc32_kernels.hip fold_small (the join's short segments, <= 64 B): the aligned
     dwords covering [a, a + L) loaded first, each 4 bytes one slicing-by-4 step on the

@@ -216,3 +216,27 @@ def test_kernel_name_follows_the_entry_and_knobs():
     assert name(binned=True, ablate=8388608) == "crc32_vring_kernel<2, 0, 0, 0, 1, 0, 0, 0, 0>"
     assert name(ablate=524288) == "crc32_vring_kernel<3, 0, 0, 0, 0, 0, 0, 0, 1>"
     assert name(ablate=8388608) == "crc32_vring_kernel<3, 0, 0, 0, 0, 0, 0, 0, 2>"
+
+
+def test_shard_option_measures_one_cfg4_shard(monkeypatch):
+    """`bench.py --config cfg4 --shard R/N`: rank R's contiguous shard
+    of an N-GPU cfg4 run, measured alone on one device, so the driver's N-GPU curve
+    has a per-GPU point to be read against; invalid with --gpus N or another config."""
+    import io
+    import contextlib
+    import bench
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE"):
+        monkeypatch.delenv(k, raising=False)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        bench.main(["--config", "cfg4", "--shard", "7/8", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"],
+                   engine_factory=FakeEngine, cpu_factory=fake_cpu)
+    d = json.loads([l for l in buf.getvalue().splitlines() if l.startswith("{")][0])
+    assert d["n_gpus"] == 1 and d["scaling"] == "strong"
+    assert d["config"]["packets_per_gpu"] == (1 << 20) // 8
+    assert "shard 7 of 8" in d["config"]["workload"] and d["config"]["parallelism"].startswith("shard 7/8 alone")
+    for bad in (["--config", "cfg2", "--shard", "0/2"], ["--config", "cfg4", "--shard", "2/2"],
+                ["--config", "cfg4", "--shard", "0/2", "--gpus", "2"]):
+        with pytest.raises(SystemExit):
+            bench.main(bad + ["--steps", "2", "--warmup", "1", "--no-cpu-baseline"], engine_factory=FakeEngine,
+                       cpu_factory=fake_cpu)

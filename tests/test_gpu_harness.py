@@ -162,3 +162,146 @@ def test_gpu_stamp_send_and_receive_verify(ctx, oracle_lib, corrupt):  # noqa: F
         free_pinned(p)
         rx.close()
         tx.close()
+
+
+def compressible(sb, rng, frac=0.6):
+    """Make the bodies of a fraction of the DGRAMs low-entropy (ENet command streams
+    of repeated fields): those compress, the random ones do not (sent as they are)."""
+    g = sb.gather
+    for d in np.nonzero(rng.random(sb.n) < frac)[0]:
+        s = int(g.seg_first[d]) + 2                          # the body segment
+        o, L = int(g.seg_off[s]), int(g.seg_len[s])
+        pat = rng.integers(0, 6, size=max(1, L // 16)).astype(np.uint8)
+        g.payload[o:o + L] = np.resize(pat, L)
+
+
+def expected_wire(oracle_lib, sb):
+    """protocol.cs:1665-1705 restated: range-compress each DGRAM's commands (limit =
+    their length), keep the compressed form only when shorter (header flag 0x4000),
+    stamp the CRC over the UNCOMPRESSED gather list, wire = first buffer + (compressed
+    or original commands).  Returns (wire DGRAMs, expected payload after the call)."""
+    import oracle
+    g = sb.gather
+    pay = g.payload.copy()
+    cmds, offs, lens = [], [], []
+    pos = 0
+    for d in range(sb.n):
+        segs = range(int(g.seg_first[d]) + 1, int(g.seg_first[d + 1]))
+        c = b"".join(bytes(pay[int(g.seg_off[s]):int(g.seg_off[s]) + int(g.seg_len[s])]) for s in segs)
+        cmds.append(c)
+        offs.append(pos)
+        lens.append(len(c))
+        pos += len(c)
+    data = np.frombuffer(b"".join(cmds) + b"\0" * 16, np.uint8)
+    out, oo, ol = oracle.range_coder_batch(oracle_lib, False, data, np.array(offs, np.uint64),
+                                           np.array(lens, np.uint32), np.array(lens, np.uint32))
+    keep = (ol > 0) & (ol < np.array(lens, np.uint32))
+    for d in np.nonzero(keep)[0]:
+        pay[int(g.seg_off[int(g.seg_first[d])])] |= 0x40
+    crc = oracle_lib.gather(pay, g.seg_off, g.seg_len, g.seg_first)
+    wire = []
+    for d in range(sb.n):
+        s0 = int(g.seg_first[d])
+        o = int(g.seg_off[s0])
+        so = o + int(sb.slot_off[d])
+        pay[so:so + 4] = np.frombuffer(np.uint32(crc[d]).tobytes(), np.uint8)
+        first = bytes(pay[o:o + int(g.seg_len[s0])])
+        body = bytes(out[int(oo[d]):int(oo[d]) + int(ol[d])]) if keep[d] else cmds[d]
+        wire.append(first + body)
+    return wire, pay, keep
+
+
+def expected_receive(oracle_lib, dgrams, peers):
+    """protocol.cs:1001-1068 restated for range-coded hosts: header stage, the
+    decompression of flagged DGRAMs (limit 4096 - headerSize, 0 = drop), then the
+    checksum verify over the (decompressed) DGRAM.  -> (keep, DGRAM as kept)."""
+    import oracle
+    keep, outs = [], []
+    for dg in dgrams:
+        k, res = 0, dg
+        if len(dg) >= 2:
+            word = (dg[0] << 8) | dg[1]
+            peer, hs = word & 0x0FFF, (4 if word & 0x8000 else 2)
+            if peer == 0xFFF or peer < len(peers):
+                ok_size = len(dg) >= hs + 4
+                if ok_size and word & 0x4000:
+                    body = np.frombuffer(dg[hs + 4:] + b"\0" * 16, np.uint8)
+                    out, oo, ol = oracle.range_coder_batch(oracle_lib, True, body, np.array([0], np.uint64),
+                                                           np.array([len(dg) - hs - 4], np.uint32),
+                                                           np.array([4096 - hs - 4], np.uint32))
+                    ok_size = ol[0] > 0
+                    if ok_size:
+                        res = dg[:hs + 4] + bytes(out[:int(ol[0])])
+                if ok_size:
+                    conn = 0 if peer == 0xFFF else int(peers[peer])
+                    desired = int.from_bytes(res[hs:hs + 4], "little")
+                    k = int(oracle_lib.crc32(res[:hs] + np.uint32(conn).tobytes() + res[hs + 4:]) == desired)
+        keep.append(k)
+        outs.append(res)
+    return np.array(keep, np.uint8), outs
+
+
+@pytest.mark.parametrize("corrupt", [0, 40])
+def test_gpu_compress_stamp_send_and_decompress_verify(ctx, oracle_lib, corrupt):  # noqa: F811
+    """the GPU pipelines with ENet's range coder beside the checksum.
+    enet_hip_udp_compress_stamp_send puts on the wire exactly the DGRAMs the
+    reference would (compress where shorter, flag, CRC over the uncompressed list);
+    enet_hip_udp_receive_decompress_verify keeps exactly the DGRAMs the reference
+    keeps and leaves them decompressed in their slots with their new lengths --
+    corrupted compressed bodies (decoder failures or CRC mismatches) included."""
+    rng = np.random.default_rng(90 + corrupt)
+    sb = workloads.send_batch(1200, seed=91 + corrupt)
+    compressible(sb, rng)
+    g = sb.gather
+    wire, exp_pay, keep = expected_wire(oracle_lib, sb)
+    assert 0 < keep.sum() < sb.n                               # both forms on the wire
+    rx, tx, port = sockets()
+    arena, p = pinned(STRIDE * 512)
+    try:
+        got = []
+        for a in range(0, sb.n, 300):
+            b = min(sb.n, a + 300)
+            sent = ctx.udp_compress_stamp_send(tx.fileno(), g.payload, g.seg_off, g.seg_len, g.seg_first[a:b + 1],
+                                               sb.slot_off[a:b], LOOPBACK, port)
+            assert sent == b - a
+            while len(got) < b:
+                n, lens, _, _ = enethip.udp_receive(rx.fileno(), arena, STRIDE, 512, timeout_ms=2000)
+                assert n > 0
+                got.extend(bytes(arena[i * STRIDE:i * STRIDE + int(lens[i])]) for i in range(n))
+        assert (g.payload == exp_pay).all()                    # header flags and slots as the reference's
+        assert got == wire
+        # the wire form back through the GPU receive pipeline (some bodies corrupted)
+        dgrams = list(wire)
+        for d in rng.choice(sb.n, corrupt, replace=False) if corrupt else []:
+            b = bytearray(dgrams[d])
+            hs = 4 if b[0] & 0x80 else 2
+            if len(b) > hs + 5:
+                b[int(rng.integers(hs + 4, len(b)))] ^= 0x10
+            dgrams[d] = bytes(b)
+        exp_keep, exp_out = expected_receive(oracle_lib, dgrams, sb.peers)
+        oks, outs, lens_all = [], [], []
+        for a in range(0, sb.n, 300):
+            b = min(sb.n, a + 300)
+            for dg in dgrams[a:b]:
+                tx.sendto(dg, ("127.0.0.1", port))
+            k = 0
+            while k < b - a:
+                n, lens, ok = ctx.udp_receive_decompress_verify(rx.fileno(), arena, STRIDE, 512, sb.peers,
+                                                                timeout_ms=2000)
+                assert n > 0
+                oks.append(ok.copy())
+                lens_all.append(lens.copy())
+                outs.extend(bytes(arena[i * STRIDE:i * STRIDE + int(lens[i])]) for i in range(n))
+                k += n
+        ok = np.concatenate(oks)
+        assert (ok == exp_keep).all(), np.nonzero(ok != exp_keep)[0][:10]
+        if corrupt:
+            assert 0 < int((ok == 0).sum()) <= corrupt
+        else:
+            assert ok.all()
+        for i in np.nonzero(exp_keep)[0]:
+            assert outs[i] == exp_out[i], i                    # decompressed in place, new length
+    finally:
+        free_pinned(p)
+        rx.close()
+        tx.close()

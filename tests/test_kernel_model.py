@@ -350,6 +350,21 @@ def test_gather_join_matches_oracle(oracle_lib):
         assert km.gather_join(crcs, [len(s) for s in segs]) == oracle_lib.crc32(b"".join(segs))
 
 
+
+def test_gather_split_join_matches_oracle(oracle_lib):
+    """The split join of the binned gather (gather_join.hpp: pre-join with the long
+    segments' registers taken as 0 and x^(8 after) recorded, post-join XOR of each long
+    segment's CRC times it) over lists of 0-9 segments mixing short (<= 48 B, folded)
+    and long ones in any order, empty ones among them, at every offset mod 4, against
+    the oracle's CRC of the concatenation."""
+    rng = random.Random(99)
+    arena = bytes(rng.getrandbits(8) for _ in range(8192))
+    for _ in range(300):
+        segs = [(rng.randrange(0, 6000), rng.choice([0, 1, 3, 8, 24, 47, 48, 49, 60, 200, 1360]))
+                for _ in range(rng.randint(0, 9))]
+        exp = oracle_lib.crc32(b"".join(arena[a:a + L] for a, L in segs))
+        assert km.gather_split_join(arena, segs) == exp, segs
+
 def test_unstep_column_is_cinv():
     """The vring kernel's tz correction: tz unsteps through the U column equal the multiply
     by CINV[tz] = x^(-8 tz) for every tz < 32 (random registers), U is a permutation-derived
