@@ -1412,7 +1412,7 @@ int ensure(uint8_t** p, size_t* cap, size_t need) { return ensure_device(p, cap,
 
 // The binned gather's workspace: records (1024 per tile of segments, length_bin_compact's
 // layout; the binned entry's records fit too) | seg_crc[segCount + 1] (the last: the
-// padding records' CRCs, never read) | tile counts
+// padding records' CRCs, never read) | tile counts | info[segCount] (the split join)
 size_t gather_tiles(size_t segCount) { return (segCount + 1023u) / 1024u; }
 size_t gather_records_bytes(size_t segCount) { return 16u * 1024u * gather_tiles(segCount); }
 size_t gather_crc_bytes(size_t segCount) { return (4u * (segCount + 1u) + 15u) & ~static_cast<size_t>(15u); }

@@ -176,11 +176,13 @@ def load(path: str | None = None, diag: bool = False) -> ctypes.CDLL:
     L.enet_hip_udp_receive_verify.argtypes = [vp, i32, vp, sz, sz, vp, sz, i32, vp, vp, szp]
     L.enet_hip_udp_stamp_send.restype = i32
     L.enet_hip_udp_stamp_send.argtypes = [vp, i32, vp, sz, vp, vp, sz, vp, vp, sz, u32, ctypes.c_uint16, szp]
-    L.enet_hip_udp_receive_decompress_verify.restype = i32
-    L.enet_hip_udp_receive_decompress_verify.argtypes = [vp, i32, vp, sz, sz, vp, sz, i32, vp, vp, szp]
-    L.enet_hip_udp_compress_stamp_send.restype = i32
-    L.enet_hip_udp_compress_stamp_send.argtypes = [vp, i32, vp, sz, vp, vp, sz, vp, vp, sz, u32, ctypes.c_uint16,
-                                                   szp]
+    # (an ENET_HIP_LIBRARY build from before round 5 lacks these two: measurement A/B only)
+    if p in (os.path.join(PKG_ROOT, "libenethip.so"), DIAG_LIB_PATH) or hasattr(L, "enet_hip_udp_compress_stamp_send"):
+        L.enet_hip_udp_receive_decompress_verify.restype = i32
+        L.enet_hip_udp_receive_decompress_verify.argtypes = [vp, i32, vp, sz, sz, vp, sz, i32, vp, vp, szp]
+        L.enet_hip_udp_compress_stamp_send.restype = i32
+        L.enet_hip_udp_compress_stamp_send.argtypes = [vp, i32, vp, sz, vp, vp, sz, vp, vp, sz, u32, ctypes.c_uint16,
+                                                       szp]
     L.enet_hip_is_diagnostics_build.restype = i32
     L.enet_hip_is_diagnostics_build.argtypes = []
     L.enet_hip_fragment_reassemble_device.restype = i32

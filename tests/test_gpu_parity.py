@@ -901,6 +901,41 @@ def test_dynamic_rounds_claim_lines_reused_across_streams(dctx, oracle_lib):
         ctx.set_tuning(0, 0)
 
 
+def test_dynamic_rounds_graph_capture_replays(dctx, oracle_lib):
+    """a dynamic-rounds launch captured in a graph would replay its
+    one {claim line, generation} and skip chunks on the second replay.  Under capture
+    the entry takes the static deal (crc32_kernels.hip with_claim): the captured
+    launches, replayed three times, stay exact in both dynamic modes and lane counts."""
+    rng = np.random.default_rng(0xD2)
+    n = 20000
+    lens = rng.integers(0, 1500, n).astype(np.uint32)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    payload = np.frombuffer(rng.bytes(int(lens.sum()) + 64), np.uint8).copy()
+    exp = oracle_lib.batch(payload, off, lens, threads=16)
+    d_p, d_o, d_l = dev(payload), dev(off), dev(lens)
+    st = torch.cuda.Stream()
+    try:
+        for mode in (524288, 8388608):
+            dctx.diag_ablation(mode)
+            for lanes in (8, 4):
+                dctx.set_tuning(lanes, 0)
+                out = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+                torch.cuda.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=st):
+                    dctx.crc32_batch_device(d_p, d_o, d_l, n, out, stream=st.cuda_stream)
+                for rep in range(3):
+                    out.fill_(-1)
+                    g.replay()
+                    torch.cuda.synchronize()
+                    assert (out.cpu().numpy().view(np.uint32) == exp).all(), (mode, lanes, rep)
+                del g
+    finally:
+        dctx.diag_ablation(0)
+        dctx.set_tuning(0, 0)
+
+
 def test_dynamic_rounds_match_static_deal(dctx, oracle_lib):
     """The dynamic rounds (diagnostics ablation 524288: CRCs still exact) and the static
     deal give the same CRCs on cfg3's mixed lengths, single batches and lists."""

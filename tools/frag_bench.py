@@ -7,6 +7,8 @@ The bitmaps / remaining counters are reset between calls (untimed); HIP events
 bracket each call on its stream.  Result checked against the original messages.
 
     python tools/frag_bench.py [--messages 4096] [--reps 20]
+    python tools/frag_bench.py --messages 1024 --words 2 --first 1   (one fragment
+        against a 65 536-word claim space -- the slots path; --messages 1025: the atomic path)
 """
 import argparse
 import json
@@ -25,13 +27,17 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--in-order", action="store_true",
                     help="fragments in send order instead of shuffled (prices the scattered descriptor stores)")
+    ap.add_argument("--words", type=int, default=2, help="bitmap words per message slot")
+    ap.add_argument("--first", type=int, default=0,
+                    help="pass only the first N fragments (tiny batch against the whole slot table)")
     a = ap.parse_args()
     import torch
     import enethip
     from enethip import workloads
     fb = (workloads.fragments([65536] * a.messages, shuffle=False, name=f"cfg5 receive, in order: {a.messages} x 65536 B")
           if a.in_order else workloads.cfg5_fragments(a.messages))
-    words = 2
+    words = a.words
+    nf = a.first if a.first else fb.n
     ctx = enethip.Context(0)
     t = lambda x, dt: torch.from_numpy(np.ascontiguousarray(x).view(dt)).cuda()  # noqa: E731
     d_payload = t(fb.payload, np.uint8)
@@ -52,18 +58,23 @@ def main():
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         with torch.cuda.stream(s):
             e0.record(s)
-            ctx.fragment_reassemble_device(d_payload, d_off, d_avail, d_slots, fb.n, 32 << 20, d_msg, d_moff, d_mlen,
+            ctx.fragment_reassemble_device(d_payload, d_off, d_avail, d_slots, nf, 32 << 20, d_msg, d_moff, d_mlen,
                                            d_mcnt, d_frag, words, d_rem, len(fb.msg_len), d_status,
                                            stream=s.cuda_stream)
             e1.record(s)
         torch.cuda.synchronize()
         if r >= 2:
             times.append(e0.elapsed_time(e1) * 1e-3)
-    ok = bool((d_status.cpu().numpy() == 1).all() and (d_rem.cpu().numpy() == 0).all() and
-              (d_msg.cpu().numpy() == np.concatenate(fb.messages)).all())
+    if a.first:                                   # a partial batch: every fragment new, nothing else
+        ok = bool((d_status.cpu().numpy()[:nf] == 1).all())
+    else:
+        ok = bool((d_status.cpu().numpy() == 1).all() and (d_rem.cpu().numpy() == 0).all() and
+                  (d_msg.cpu().numpy() == np.concatenate(fb.messages)).all())
     dt = float(np.median(times))
-    moved = 2.0 * fb.data_bytes
-    print(json.dumps({"workload": fb.name, "fragments": fb.n, "data_bytes": fb.data_bytes,
+    moved = 2.0 * (float(fb.cmd_avail[:nf].astype(np.uint64).sum()) if a.first else fb.data_bytes)
+    claims = len(fb.msg_len) * words * 32
+    print(json.dumps({"workload": fb.name, "fragments": nf, "claim_space": claims,
+                      "slots_path": claims <= 8 * nf + 65536, "data_bytes": fb.data_bytes,
                       "us_per_call": round(dt * 1e6, 2), "GBps_moved": round(moved / dt / 1e9, 1),
                       "hbm_frac": round(moved / dt / 8e12, 4), "ok": ok}), flush=True)
     ctx.close()
