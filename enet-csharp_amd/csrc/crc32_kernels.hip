@@ -912,6 +912,7 @@ __global__ void __launch_bounds__(kThreads) crc32_gather_join_kernel(GatherArgs 
 }
 
 
+#ifdef ENET_HIP_DIAG
 // The post-join of the split join (gather_join.hpp): one thread per segment, after
 // the records pass.  A long segment q of DGRAM d = info[q].x adds
 // bswap(R_q x^(8 after_q)) to out[d] (R_q = ~bswap(seg_crc[q])), ~seg_crc[q] when
@@ -921,17 +922,29 @@ __global__ void __launch_bounds__(256) crc32_gather_post_kernel(const uint32_t* 
                                                                 const uint2* info, const uint32_t* seg_first,
                                                                 uint64_t n, uint64_t segs, uint32_t small,
                                                                 uint32_t* out) {
+    constexpr uint32_t kPer = 2;                             // segments per thread, loads issued together
     const uint64_t hi = umin64(seg_first[n], segs), lo = seg_first[0];
-    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256u;
-    for (uint64_t q = lo + static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x; q < hi; q += stride) {
-        const uint32_t L = seg_len[q];
-        const uint2 in = info[q];
-        const uint32_t c = seg_crc[q];
-        if (L <= small || in.x >= n) continue;
-        const uint32_t add = in.y == kOneReflected ? ~c : bswap32(mulmod(~bswap32(c), in.y));
-        atomicXor(out + in.x, add);
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256u * kPer;
+    for (uint64_t c = lo + static_cast<uint64_t>(blockIdx.x) * 256u * kPer + threadIdx.x; c < hi; c += stride) {
+        uint32_t L[kPer], C[kPer];
+        uint2 in[kPer];
+#pragma unroll
+        for (uint32_t i = 0; i < kPer; ++i) {
+            const uint64_t q = c + 256u * i;
+            const bool h = q < hi;
+            L[i] = h ? seg_len[q] : 0u;
+            in[i] = h ? info[q] : make_uint2(~0u, 0u);
+            C[i] = h ? seg_crc[q] : 0u;
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < kPer; ++i) {
+            if (L[i] <= small || in[i].x >= n) continue;
+            const uint32_t add = in[i].y == kOneReflected ? ~C[i] : bswap32(mulmod(~bswap32(C[i]), in[i].y));
+            atomicXor(out + in[i].x, add);
+        }
     }
 }
+#endif  // ENET_HIP_DIAG
 
 // Read-roofline probe: every byte loaded once by 16-byte coalesced loads,
 // 4 loads in flight per lane, XOR-folded so nothing is dead code.
@@ -1548,7 +1561,7 @@ int enet_hip_diag_ablation(enet_hip_context* ctx, int mode) {
     if (!ctx || mode < 0) return -static_cast<int>(hipErrorInvalidValue);
     ctx->bin_identity = (mode >> 30) & 1;                    // 2^30: binned records left in memory order
     ctx->vr_pair = (mode >> 23) & 1;                         // 8388608: vring pair rounds
-    ctx->join_abl = (mode >> 20) & 7;                        // 1048576 x (1..7): the one-pass gather join after the records (4: unablated; others: its ablations)
+    ctx->join_abl = (mode >> 20) & 7;                        // 1048576 x (1, 2, 3, 5, 7): gather-join ablations; 4194304: the split join
     // 16777216 x (1 + b), b < 63: the binned gather's short-segment bound b bytes (0: 48)
     ctx->gather_small = (mode >> 24) ? ((mode >> 24) & 63) - 1 : -1;
     ctx->vr_dynamic = (mode >> 19) & 1;                      // 524288: vring dynamic rounds
@@ -1803,12 +1816,16 @@ int enet_hip_crc32_gather_device(enet_hip_context* ctx, const uint8_t* bytes, co
     return herr(hipGetLastError());
 }
 
-// records | seg_crc | tile counts | the split join's info[] (8 B per segment)
+// records | seg_crc | tile counts (| diagnostics: the split join's info[], 8 B per segment)
 static size_t gather_counts_bytes(size_t segCount) { return (4u * gather_tiles(segCount) + 15u) & ~static_cast<size_t>(15u); }
 
 size_t enet_hip_gather_binned_workspace_size(size_t segCount) {
+#ifdef ENET_HIP_DIAG
     return gather_records_bytes(segCount) + gather_crc_bytes(segCount) + gather_counts_bytes(segCount) +
            8u * segCount + 16u;
+#else
+    return gather_records_bytes(segCount) + gather_crc_bytes(segCount) + gather_counts_bytes(segCount) + 16u;
+#endif
 }
 
 int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* bytes, const uint64_t* segOffsets,
@@ -1834,13 +1851,11 @@ int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* by
     const bool split = vring_path(ctx) && ctx->ablation == 0 && (lanes == 4 || lanes == 8);
     GatherArgs ga{bytes, segOffsets, segLengths, segFirst, dgramCount, out, segCount};
 #ifdef ENET_HIP_DIAG
-    const bool old_join = ctx->join_abl != 0;                // (diagnostics: the one-pass join after the records)
-#else
-    constexpr bool old_join = false;
-#endif
-    if (split && !old_join) {
-        // the split join (gather_join.hpp): pre-join beside the binning tiles, records,
-        // post-join per segment -- no pass waits on a DGRAM's metadata chain after the records
+    if (split && ctx->join_abl == 4) {
+        // (diagnostics 4194304) the split join (gather_join.hpp): pre-join beside the
+        // binning tiles, records, post-join per segment.  Bit-exact, and slower than the
+        // one-pass join below: 70.3-72.4 against 68.3-70.4 us on cfg5 (DESIGN 4.4,
+        // profiles/r05_split_join/)
         const KernelTables tb = tables_of(ctx);
         const uint32_t kpk = lanes == 4 ? 16u : 8u;
         uint2* info = reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(counts) + gather_counts_bytes(segCount));
@@ -1860,11 +1875,12 @@ int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* by
         if ((rc = vring_launch_list(lanes == 4 ? 2 : 3, ctx->num_cus * gw, with_claim(ctx, gv, st), st, bl, tb,
                                     ctx->d_basis2, nullptr, true)))
             return rc;
-        const unsigned pg = static_cast<unsigned>(std::min<uint64_t>((segCount + 255u) / 256u, 8u * ctx->num_cus));
+        const unsigned pg = static_cast<unsigned>(std::min<uint64_t>((segCount + 511u) / 512u, 8u * ctx->num_cus));
         hipLaunchKernelGGL(crc32_gather_post_kernel, dim3(pg), dim3(256), 0, st, segLengths, seg_crc, info, segFirst,
                            static_cast<uint64_t>(dgramCount), static_cast<uint64_t>(segCount), small, out);
         return herr(hipGetLastError());
     }
+#endif
     if (segCount && split) {
         const KernelTables tb = tables_of(ctx);
         const uint32_t kpk = lanes == 4 ? 16u : 8u;

@@ -832,26 +832,30 @@ __global__ void __launch_bounds__(kBinThreads) bin_tile_kernel(const uint32_t* l
     bin_tile_body<VERIFY, COMPACT, IDENT>(blockIdx.x, gridDim.x, len, off, n, kpk, slot_off, connect, rec, small, count);
 }
 
-// The binned gather's first launch: blocks [0, pj) run the split join's pre-join
+#ifdef ENET_HIP_DIAG
+// The binned gather's first launch: blocks [0, tiles) are the compact length-binning
+// tiles of the segments, blocks [tiles, tiles + pj) the split join's pre-join
 // (gather_join.hpp, one thread per DGRAM: short segments folded, out[d] = finalize(A),
-// info[q] for the long ones), blocks [pj, pj + tiles) the compact length-binning
-// tiles of the segments.  The two need nothing from each other, so one launch
+// info[q] for the long ones).  78 VGPRs (6 waves per SIMD): cfg5's 588 + 784 blocks are
+// resident at once.  The two need nothing from each other, so one launch
 // overlaps the pre-join's dependent loads (segFirst, then lengths and offsets, then
 // bytes) with the binning instead of running them after the records pass.
-__global__ void __launch_bounds__(kBinThreads) gather_bin_prejoin_kernel(GatherArgs ga, uint2* info, KernelTables tb,
+__global__ void __launch_bounds__(kBinThreads) __attribute__((amdgpu_waves_per_eu(6))) gather_bin_prejoin_kernel(GatherArgs ga, uint2* info, KernelTables tb,
                                                                          uint32_t small, uint32_t pj, uint32_t kpk,
                                                                          uint4* rec, uint32_t* count) {
-    if (blockIdx.x >= pj) {
-        bin_tile_body<false, true>(blockIdx.x - pj, gridDim.x - pj, ga.seg_len, ga.seg_off, ga.segs, kpk, nullptr,
-                                   nullptr, rec, small, count);
+    const uint32_t tiles = gridDim.x - pj;
+    if (blockIdx.x < tiles) {
+        bin_tile_body<false, true>(blockIdx.x, tiles, ga.seg_len, ga.seg_off, ga.segs, kpk, nullptr, nullptr, rec,
+                                   small, count);
         return;
     }
     __shared__ uint32_t t4[4][256];
     fill_t4<kBinThreads>(t4, tb.image);
-    for (uint64_t d = static_cast<uint64_t>(blockIdx.x) * kBinThreads + threadIdx.x; d < ga.n;
+    for (uint64_t d = static_cast<uint64_t>(blockIdx.x - tiles) * kBinThreads + threadIdx.x; d < ga.n;
          d += static_cast<uint64_t>(pj) * kBinThreads)
         gather_prejoin_dgram(ga, info, tb, small, d, t4);
 }
+#endif  // ENET_HIP_DIAG
 
 size_t length_bin_workspace(uint64_t n, bool verify) { return (verify ? 32u : 16u) * n; }
 
@@ -890,6 +894,7 @@ int length_bin_compact(const uint32_t* len, const uint64_t* off, uint64_t n, uin
     return e == hipSuccess ? 0 : -static_cast<int>(e);
 }
 
+#ifdef ENET_HIP_DIAG
 int gather_bin_prejoin(const GatherArgs& ga, uint2* info, const KernelTables& tb, uint32_t small, uint32_t kpk,
                        void* records, uint32_t* counts, unsigned prejoin_blocks, hipStream_t st) {
     if (ga.segs > 0xFFFFFFFFull || (ga.segs && (!records || !counts)) || kpk == 0 || kBinTile % kpk ||
@@ -901,5 +906,6 @@ int gather_bin_prejoin(const GatherArgs& ga, uint2* info, const KernelTables& tb
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : -static_cast<int>(e);
 }
+#endif  // ENET_HIP_DIAG
 
 }  // namespace enethip

@@ -88,7 +88,7 @@ int length_bin(const uint32_t* len, const uint64_t* off, const uint32_t* slot_of
 // records: 16 x 1024 T bytes; counts: 4 T bytes.  No global atomics.
 int length_bin_compact(const uint32_t* len, const uint64_t* off, uint64_t n, uint32_t kpk, uint32_t small,
                        void* records, uint32_t* counts, hipStream_t st);
-// length_bin_compact over ga's segments (ga.segs of them) and, in the same launch
+// (diagnostics) length_bin_compact over ga's segments (ga.segs of them) and, in the same launch
 // (prejoin_blocks more workgroups), the split join's pre-join over ga's DGRAMs
 // (gather_join.hpp): out[d] = finalize(A_d), info[q] for the long segments.
 int gather_bin_prejoin(const GatherArgs& ga, uint2* info, const KernelTables& tb, uint32_t small, uint32_t kpk,

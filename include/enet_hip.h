@@ -211,14 +211,11 @@ ENET_HIP_API int enet_hip_crc32_gather_device(enet_hip_context* ctx, const uint8
                                               void* stream);
 
 /* Same results as enet_hip_crc32_gather_device, with the segment count known on
- * the host (segCount = segFirst[dgramCount]; segFirst non-decreasing, so each
- * segment belongs to at most one DGRAM).  Three passes on `stream`: (1) segments
- * over 48 B (MTU payloads) sorted per tile of 1024 by length bin and, in the same
- * launch, one thread per DGRAM folding the short ones (headers, commands) with the
- * long ones' own registers taken as zero; (2) the long segments' CRCs from the vring
- * kernel's records instance; (3) one thread per long segment adding its CRC, times
- * x^(8 bytes after it), into its DGRAM's result (the CRC is affine in it).
- * `workspace`: caller-owned device memory of at least
+ * the host (segCount = segFirst[dgramCount]).  Three passes on `stream`: segments
+ * over 48 B (MTU payloads) sorted per tile of 1024 by length bin, their CRCs from
+ * the vring kernel's records instance, then one thread per DGRAM folds the short
+ * ones (headers, commands) itself and joins the long ones' CRCs with one GF(2)
+ * multiply by x^(8 len) each.  `workspace`: caller-owned device memory of at least
  * enet_hip_gather_binned_workspace_size(segCount) bytes, 16-byte aligned, not
  * shared with a call in flight; segCount < 2^32.  Async; graph-capturable. */
 ENET_HIP_API size_t enet_hip_gather_binned_workspace_size(size_t segCount);

@@ -591,6 +591,24 @@ def test_gather_binned(ctx, golden, oracle_lib):
         ctx.set_tuning(0, 0)
 
 
+def test_gather_split_join_diagnostics(dctx, golden, oracle_lib):
+    """The split join (diagnostics 4194304, gather_join.hpp: the short segments folded
+    beside the binning tiles, each long segment's CRC XORed in afterwards with
+    x^(8 bytes after it)) -- measured slower than the one-pass join and kept out of the
+    product -- on every test_gather_binned list at 4 and 8 lanes, against the oracle."""
+    cases = _gather_cases(golden, oracle_lib)
+    try:
+        dctx.diag_ablation(4194304)
+        for lanes in (0, 4):
+            dctx.set_tuning(lanes, 0)
+            for i, (p, so, sl, f, e) in enumerate(cases):
+                got = _run_gather_binned(dctx, p, so, sl, f)
+                assert (got == e).all(), (lanes, i, np.nonzero(got != e)[0][:5])
+    finally:
+        dctx.diag_ablation(0)
+        dctx.set_tuning(0, 0)
+
+
 def test_gather_binned_back_to_back_and_graph(ctx, oracle_lib):
     """The binned gather's three passes (bin, records checksum, join) over workspaces that
     calls reuse: 12 calls back to back on one non-default stream without a sync, three
