@@ -399,7 +399,8 @@ def make_batches(cfg: str, rotate: int, rank: int, world: int = 1):
     return out
 
 
-PRODUCT_PATHS = (0, 1, 2, 13, 17)          # built in libenethip.so (the rest: libenethip_diag.so)
+PRODUCT_PATHS = (0, 13, 17)                # built in libenethip.so (the rest: libenethip_diag.so)
+PRODUCT_LANES = (0, 4, 8)                  # lanes per packet libenethip.so takes (the rest: diagnostics)
 
 
 def kernel_name(args, list_launch: bool = False) -> str:
@@ -526,7 +527,7 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
         shard = (r_, n_)
     dist = dist_init(ws)
     batches = make_batches(args.config, args.rotate, *(shard if shard else (rank, ws)))
-    diag = args.path not in PRODUCT_PATHS or args.ablate != 0
+    diag = args.path not in PRODUCT_PATHS or args.lanes not in PRODUCT_LANES or args.ablate != 0
     eng = (engine_factory or GpuEngine)(local, batches, args.lanes, args.wgs, *((diag,) if diag else ()))
     if hasattr(eng, "set_streams"):
         eng.set_streams(args.streams)

@@ -53,6 +53,7 @@ __device__ __forceinline__ void fill_table(uint8_t* lds, const uint32_t* image) 
     __syncthreads();
 }
 
+#ifdef ENET_HIP_DIAG   // the LDS-stream and direct kernels: 16 / 1, 2, 32, 64 lanes (diagnostics only since round 5)
 // ============================================================ stream kernel
 //
 // One persistent workgroup of W waves per CU.  A wave owns groups g = wv,
@@ -406,6 +407,8 @@ __global__ void __launch_bounds__(G::kThreads) crc32_stream_kernel(PacketArgs pa
     while (!done) unroll_slots<G::kNB>(stage);
 }
 
+#endif  // ENET_HIP_DIAG
+
 #ifdef ENET_HIP_DIAG
 // ============================================================ register-stream kernel
 // (diagnostics library only: a comparison point kept for the sweeps)
@@ -717,6 +720,7 @@ __global__ void __launch_bounds__(G::kThreads) crc32_vstream_kernel(PacketArgs p
 
 #endif  // ENET_HIP_DIAG
 
+#ifdef ENET_HIP_DIAG
 // ============================================================ direct kernel
 //
 // General direct-load path (every block loaded straight into VGPRs, any P):
@@ -804,7 +808,7 @@ __global__ void __launch_bounds__(kThreads) crc32_direct_kernel(PacketArgs pa, K
         finish_dtask<MODE>(pa, tk, reg, tb);
     }
 }
-
+#endif  // ENET_HIP_DIAG
 
 // One lane per DGRAM; segments folded in order and joined by the carry-combine.
 __global__ void __launch_bounds__(kThreads) crc32_gather_kernel(GatherArgs ga, KernelTables tb) {
@@ -1113,6 +1117,7 @@ unsigned grid_for(const enet_hip_context* ctx, uint64_t tasks) {
     return static_cast<unsigned>(std::max<uint64_t>(1, std::min(need, cap)));
 }
 
+#ifdef ENET_HIP_DIAG
 // Stream geometries (waves per CU, blocks per stage, stage buffers).
 // kStreamDefault is what path 0 runs; the others are reachable through
 // enet_hip_set_kernel_path (2 + index) for tuning sweeps.
@@ -1146,20 +1151,22 @@ struct StreamVariant {
         return 0;
     }
 };
+#endif  // ENET_HIP_DIAG
 
-// Kernel paths (enet_hip_set_kernel_path): 2 + k = stream geometry k (k < 6), then
-// 5 register-stream geometries, 4 lean geometries, the vring variants.  The product
-// library builds stream geometry 0 (16 lanes per packet) and lean geometry 0; the
-// rest are sweep-only (ENET_HIP_DIAG).
+// Kernel paths (enet_hip_set_kernel_path): 1 = direct, 2 + k = stream geometry k (k <
+// 6), then 5 register-stream geometries, 4 lean geometries, the vring variants.  The
+// product library builds the default (0), lean geometry 0 and the vring path; the rest,
+// with the lane counts other than 4 and 8 they served, are sweep-only (ENET_HIP_DIAG,
+// since round 5).
 constexpr int kStreamPaths = 6, kVStreamPaths = 5;
 #ifdef ENET_HIP_DIAG
 using StreamGeoms = std::tuple<StreamGeom<16, 1, 2>, StreamGeom<11, 1, 3>, StreamGeom<8, 1, 4>,
                                StreamGeom<8, 2, 2>, StreamGeom<6, 2, 3>, StreamGeom<10, 1, 3>>;
-#else
-using StreamGeoms = std::tuple<StreamGeom<16, 1, 2>>;
 #endif
 constexpr int kNumStreamGeoms = kStreamPaths;
+#ifdef ENET_HIP_DIAG
 constexpr int kStreamDefault = 0;
+#endif
 
 #ifdef ENET_HIP_DIAG
 template <class G>
@@ -1204,15 +1211,17 @@ constexpr int kVringWalkAltPath = kVringWalkPath + 1;   // the same with nontemp
 constexpr int kVringTailFirstPath = kVringWalkAltPath + 1;   // vring, the tail-first stage order
 constexpr int kLinPath = kVringTailFirstPath + 1;      // crc32_lin.hip: linear stream, nontemporal tile DMA
 constexpr int kLinPlainPath = kLinPath + 1;            // the same with default-policy tile DMA
+#ifdef ENET_HIP_DIAG
 constexpr int kMaxPath = kLinPlainPath;
+#endif
 
 // Paths this library builds: all in the diagnostics library; in the product one
-// the default (0), direct (1), stream geometry 0 (2), lean geometry 0 and vring.
+// the default (0), lean geometry 0 and vring.
 bool path_built(int path) {
 #ifdef ENET_HIP_DIAG
     return path >= 0 && path <= kMaxPath;
 #else
-    return path == 0 || path == 1 || path == 2 || path == kLeanPath0 || path == kVringPath;
+    return path == 0 || path == kLeanPath0 || path == kVringPath;
 #endif
 }
 // the binned gather's short-segment bound (segments of at most this many bytes are
@@ -1229,6 +1238,7 @@ int lin_list(enet_hip_context* ctx, const VrBatches& bl, hipStream_t st) {
     return lin_launch_list(ctx->num_cus, st, bl, ctx->d_lin, ctx->d_zero, lin_abl(ctx), ctx->path == kLinPath);
 }
 
+#ifdef ENET_HIP_DIAG
 template <size_t I = 0>
 void launch_stream(int geom, int mode, int abl, int num_cus, uint64_t groups, hipStream_t st,
                    const PacketArgs& pa, const KernelTables& tb) {
@@ -1244,6 +1254,7 @@ void launch_stream(int geom, int mode, int abl, int num_cus, uint64_t groups, hi
     }
 }
 
+#endif  // ENET_HIP_DIAG
 #ifdef ENET_HIP_DIAG
 template <size_t I = 0>
 void launch_vstream(int geom, int mode, int abl, int num_cus, uint64_t groups, hipStream_t st,
@@ -1270,6 +1281,7 @@ int setup_vstream() {
 }
 #endif  // ENET_HIP_DIAG
 
+#ifdef ENET_HIP_DIAG
 template <size_t I = 0>
 int setup_stream() {
     if constexpr (I < std::tuple_size<StreamGeoms>::value) {
@@ -1278,6 +1290,7 @@ int setup_stream() {
     }
     return 0;
 }
+#endif  // ENET_HIP_DIAG
 
 // vring workgroups per CU of one launch (enet_hip_set_tuning's workgroups_per_cu,
 // clamped to 2: the LDS and 64-VGPR budget of two 16-wave workgroups; values 3..8
@@ -1402,6 +1415,10 @@ int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStr
         if (lean_path && pa.lg <= 3)
             return lean_launch(mode, pa.lg, ctx->path == 0 ? 0 : ctx->path - kLeanPath0, ctx->ablation,
                                ctx->num_cus, st, pa, tb);
+#ifndef ENET_HIP_DIAG
+    }
+    return -static_cast<int>(hipErrorInvalidValue);          // (the product takes 4 or 8 lanes: set_tuning)
+#else
         const uint64_t groups = (pa.n + (64u >> pa.lg) - 1) >> (6 - pa.lg);
         const int geom = (ctx->path == 0 || ctx->path >= kLeanPath0) ? kStreamDefault : ctx->path - 2;
         if (geom < kNumStreamGeoms)
@@ -1419,6 +1436,7 @@ int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStr
             hipLaunchKernelGGL(crc32_direct_kernel<1>, dim3(grid), dim3(kThreads), kLdsTableBytes, st, pa, tb);
     }
     return herr(hipGetLastError());
+#endif
 }
 
 int ensure(uint8_t** p, size_t* cap, size_t need) { return ensure_device(p, cap, need); }
@@ -1503,15 +1521,15 @@ int enet_hip_context_create(int device, enet_hip_context** out) {
 #ifdef ENET_HIP_DIAG
         if ((rc = lin_setup())) break;
 #endif
-        if ((rc = setup_stream())) break;
 #ifdef ENET_HIP_DIAG
+        if ((rc = setup_stream())) break;
         if ((rc = setup_vstream())) break;
-#endif
-        if ((rc = lean_setup())) break;
         if ((rc = herr(hipFuncSetAttribute(reinterpret_cast<const void*>(crc32_direct_kernel<0>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTableBytes)))) break;
         if ((rc = herr(hipFuncSetAttribute(reinterpret_cast<const void*>(crc32_direct_kernel<1>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTableBytes)))) break;
+#endif
+        if ((rc = lean_setup())) break;
         if ((rc = herr(hipFuncSetAttribute(reinterpret_cast<const void*>(crc32_gather_kernel),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTableBytes)))) break;
     } while (0);
@@ -1548,8 +1566,13 @@ int enet_hip_context_destroy(enet_hip_context* ctx) {
 
 int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgroups_per_cu) {
     if (!ctx) return -static_cast<int>(hipErrorInvalidValue);
+#ifdef ENET_HIP_DIAG
     if (lanes_per_packet < 0 || lanes_per_packet > 64 || (lanes_per_packet & (lanes_per_packet - 1)))
         return -static_cast<int>(hipErrorInvalidValue);
+#else
+    if (lanes_per_packet != 0 && lanes_per_packet != 4 && lanes_per_packet != 8)   // (the vring / lean lane counts)
+        return -static_cast<int>(hipErrorInvalidValue);
+#endif
     if (workgroups_per_cu < 0 || workgroups_per_cu > 8) return -static_cast<int>(hipErrorInvalidValue);
     ctx->lanes_per_packet = lanes_per_packet;
     ctx->wgs_per_cu = workgroups_per_cu;

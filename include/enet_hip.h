@@ -70,13 +70,15 @@ ENET_HIP_API int enet_hip_context_create(int device, enet_hip_context** out);
 ENET_HIP_API int enet_hip_context_destroy(enet_hip_context* ctx);
 ENET_HIP_API const char* enet_hip_error_string(int code);
 
-/* Tuning knobs (0 = automatic).  lanes_per_packet: 1,2,4,...,64 lanes share one
- * packet (a power of two; default 8, and 4 for the length-binned entries);
- * workgroups_per_cu (0..8): resident workgroups per CU.  The VGPR-ring kernel runs
- * 1 or 2 (values above 2 mean 2 there; default 2 for a launch of several batches,
- * 1 for a single checksum batch, 2 for receive verify and for the binned gather's
- * segment pass -- at 2 the length-binned records run the compact records instance);
- * the direct and gather-join grids use the value as given. */
+/* Tuning knobs (0 = automatic).  lanes_per_packet: 4 or 8 lanes share one packet
+ * (default 8, and 4 for the length-binned entries); libenethip_diag.so also takes
+ * 1, 2, 16, 32 and 64 (the sweep-only direct and LDS-stream kernels), the product
+ * returns -hipErrorInvalidValue for them.  workgroups_per_cu (0..8): resident
+ * workgroups per CU.  The VGPR-ring kernel runs 1 or 2 (values above 2 mean 2
+ * there; default 2 for a launch of several batches, 1 for a single checksum batch,
+ * 2 for receive verify and for the binned gather's segment pass -- at 2 the
+ * length-binned records run the compact records instance); the gather-join grid
+ * uses the value as given. */
 ENET_HIP_API int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet, int workgroups_per_cu);
 
 /* Kernel path for the packet batch entry points (0 = default): checksum batches
@@ -84,13 +86,12 @@ ENET_HIP_API int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet
  * receive verify at 8 lanes (its verify instance) and the length-binned checksum
  * and gather entries (its records instance, 4 lanes by default).  The lean LDS-DMA
  * kernel (crc32_lean.hip) serves receive verify at 4 lanes and the length-binned
- * verify; 16 lanes run the LDS-ring stream kernel, other lane counts the direct
- * kernel.
- * Every path gives the same (correct) checksums.  Built in every library: 1 =
- * direct loads only, 2 = the stream kernel, 13 = the lean kernel, 17 = the vring
- * kernel (for the length-binned entries: its records instance).  Tuning sweeps,
- * libenethip_diag.so only (-1 elsewhere): 2 + k = stream kernel geometry k
- * (k < 11), 13 + g = lean kernel geometry g (g < 4), 18 = vring with nontemporal
+ * verify.  (Diagnostics library: 16 lanes run the LDS-ring stream kernel, other
+ * lane counts the direct kernel.)
+ * Every path gives the same (correct) checksums.  Built in every library: 13 = the
+ * lean kernel, 17 = the vring kernel (for the length-binned entries: its records
+ * instance).  Tuning sweeps, libenethip_diag.so only (-1 elsewhere): 1 = direct
+ * loads only, 2 + k = stream kernel geometry k (k < 11), 13 + g = lean kernel geometry g (g < 4), 18 = vring with nontemporal
  * stage loads, 19 / 20 = vring with each workgroup walking a contiguous range of
  * groups (plain / nontemporal loads), 21 = vring with the tail-first stage order
  * (each group's last stage first: less L2 refetch, more VALU; slower). */

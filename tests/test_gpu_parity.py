@@ -36,12 +36,13 @@ def dctx():
     c.close()
 
 
-PRODUCT_PATHS = (0, 1, 2, 13, 17)   # built in libenethip.so; every other path: libenethip_diag.so only
+PRODUCT_PATHS = (0, 13, 17)   # built in libenethip.so; every other path: libenethip_diag.so only
+PRODUCT_LANES = (0, 4, 8)     # lanes per packet libenethip.so takes; 1, 2, 16, 32, 64: diagnostics only
 
 
-def on(ctx, dctx, path):
-    """The context whose library builds kernel path `path`."""
-    return ctx if path in PRODUCT_PATHS else dctx
+def on(ctx, dctx, path, lanes=0):
+    """The context whose library builds kernel path `path` at `lanes` lanes per packet."""
+    return ctx if path in PRODUCT_PATHS and lanes in PRODUCT_LANES else dctx
 
 
 WGS = (0, 1, 2)    # workgroups per CU of the vring kernel: the default (2), one, two
@@ -79,15 +80,15 @@ def golden_batch(golden):
 
 
 @pytest.mark.parametrize("lanes", [1, 2, 4, 8, 16, 64])
-def test_golden_vectors(ctx, golden, lanes):
+def test_golden_vectors(ctx, dctx, golden, lanes):
     payload, off, lens, exp = golden_batch(golden)
-    got = run_batch(ctx, payload, off, lens, lanes)
+    got = run_batch(on(ctx, dctx, 0, lanes), payload, off, lens, lanes)
     bad = np.nonzero(got != exp)[0]
     assert len(bad) == 0, [(int(i), int(lens[i]), hex(got[i]), hex(exp[i])) for i in bad[:10]]
 
 
 @pytest.mark.parametrize("lanes", [1, 4, 32])
-def test_random_unaligned_sparse(ctx, oracle_lib, lanes):
+def test_random_unaligned_sparse(ctx, dctx, oracle_lib, lanes):
     rng = np.random.default_rng(100 + lanes)
     n = 5000
     lens = rng.integers(0, 5000, size=n).astype(np.uint32)
@@ -99,23 +100,23 @@ def test_random_unaligned_sparse(ctx, oracle_lib, lanes):
     perm = rng.permutation(n)                       # packets in arbitrary order
     off, lens = off[perm], lens[perm]
     payload = rng.integers(0, 256, size=int((off + lens).max()) + 5, dtype=np.uint8)
-    got = run_batch(ctx, payload, off, lens, lanes)
+    got = run_batch(on(ctx, dctx, 0, lanes), payload, off, lens, lanes)
     exp = oracle_lib.batch(payload, off, lens, threads=8)
     assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
 
 
-def test_cfg2_full(ctx, oracle_lib):
+def test_cfg2_full(ctx, dctx, oracle_lib):
     b = workloads.cfg2()
     exp = oracle_lib.batch(b.payload, b.off, b.lens, threads=16)
     for lanes in (1, 4, 8):
-        assert (run_batch(ctx, b.payload, b.off, b.lens, lanes) == exp).all(), lanes
+        assert (run_batch(on(ctx, dctx, 0, lanes), b.payload, b.off, b.lens, lanes) == exp).all(), lanes
 
 
-def test_cfg3_full(ctx, oracle_lib):
+def test_cfg3_full(ctx, dctx, oracle_lib):
     b = workloads.cfg3()
     exp = oracle_lib.batch(b.payload, b.off, b.lens, threads=16)
     for lanes in (2, 4):
-        assert (run_batch(ctx, b.payload, b.off, b.lens, lanes) == exp).all(), lanes
+        assert (run_batch(on(ctx, dctx, 0, lanes), b.payload, b.off, b.lens, lanes) == exp).all(), lanes
 
 
 def run_binned(ctx, payload, off, lens, lanes=0, path=0, wgs=0):
@@ -163,9 +164,9 @@ def test_binned_vring_many_groups(ctx, oracle_lib):
 
 @pytest.mark.parametrize("lanes", [1, 4, 8])
 @pytest.mark.parametrize("path", BINNED_PATHS)
-def test_binned_golden_and_edges(ctx, golden, oracle_lib, lanes, path):
+def test_binned_golden_and_edges(ctx, dctx, golden, oracle_lib, lanes, path):
     payload, off, lens, exp = golden_batch(golden)
-    assert (run_binned(ctx, payload, off, lens, lanes, path) == exp).all()
+    assert (run_binned(on(ctx, dctx, path, lanes), payload, off, lens, lanes, path) == exp).all()
     # lengths over every bin incl. the clamped last one (>= 8160 B), empties, one-packet batches
     rng = np.random.default_rng(7 + lanes)
     n = 20000
@@ -175,8 +176,8 @@ def test_binned_golden_and_edges(ctx, golden, oracle_lib, lanes, path):
     off = rng.integers(0, 1 << 20, size=n).astype(np.uint64)
     payload = rng.integers(0, 256, size=(1 << 20) + 9000, dtype=np.uint8)
     exp = oracle_lib.batch(payload, off, lens, threads=8)
-    assert (run_binned(ctx, payload, off, lens, lanes, path) == exp).all()
-    assert (run_binned(ctx, payload, off[:1], lens[:1], lanes, path) == exp[:1]).all()
+    assert (run_binned(on(ctx, dctx, path, lanes), payload, off, lens, lanes, path) == exp).all()
+    assert (run_binned(on(ctx, dctx, path, lanes), payload, off[:1], lens[:1], lanes, path) == exp[:1]).all()
 
 
 @pytest.mark.parametrize("wgs", [1, 2])
@@ -272,7 +273,7 @@ def test_linearity_and_determinism(ctx):
     ca, cb, cc = (run_batch(ctx, x, off, lens) for x in (a, b_, c))
     cx = run_batch(ctx, a ^ b_ ^ c, off, lens)
     assert (cx == (ca ^ cb ^ cc)).all()
-    assert (run_batch(ctx, a, off, lens, 16, 1) == ca).all()
+    assert (run_batch(ctx, a, off, lens, 4, 1) == ca).all()
 
 
 N_STREAM_GEOMS = 13          # 6 LDS-ring + 5 register-stream geometries + 2 lean-kernel geometries
@@ -288,15 +289,19 @@ def test_stream_geometries(ctx, dctx, golden, oracle_lib, geom):
     exp_b = oracle_lib.batch(b.payload, b.off, b.lens, threads=16)
     small = workloads.mixed(200000, 1, 100, seed=7, len_seed=8)
     exp_s = oracle_lib.batch(small.payload, small.off, small.lens, threads=16)
-    ctx = on(ctx, dctx, 2 + geom)
     try:
-        ctx.set_kernel_path(2 + geom)
         for lanes in (4, 8, 16):
-            assert (run_batch(ctx, payload, off, lens, lanes) == exp).all(), ("golden", lanes)
-            assert (run_batch(ctx, b.payload, b.off, b.lens, lanes) == exp_b).all(), ("mixed", lanes)
-        assert (run_batch(ctx, small.payload, small.off, small.lens, 4) == exp_s).all()
+            c = on(ctx, dctx, 2 + geom, lanes)
+            c.set_kernel_path(2 + geom)
+            assert (run_batch(c, payload, off, lens, lanes) == exp).all(), ("golden", lanes)
+            assert (run_batch(c, b.payload, b.off, b.lens, lanes) == exp_b).all(), ("mixed", lanes)
+        c = on(ctx, dctx, 2 + geom, 4)
+        c.set_kernel_path(2 + geom)
+        assert (run_batch(c, small.payload, small.off, small.lens, 4) == exp_s).all()
     finally:
-        ctx.set_kernel_path(0)
+        for c in (ctx, dctx):
+            c.set_kernel_path(0)
+            c.set_tuning(0, 0)
 
 
 def _verify_expect(oracle_lib, payload, off, lens, slot, conn):
@@ -370,7 +375,7 @@ def _verify_inputs(rng, n):
     return payload, off, lens, slot, conn
 
 
-def test_verify_batch(ctx, oracle_lib):
+def test_verify_batch(ctx, dctx, oracle_lib):
     rng = np.random.default_rng(21)
     n = 4000
     payload, off, lens, slot, conn = _verify_inputs(rng, n)
@@ -386,14 +391,16 @@ def test_verify_batch(ctx, oracle_lib):
     exp_ok, exp_comp = oracle_lib.verify(payload, off, lens, slot, conn)
     assert exp_ok.sum() == n - 300
     for lanes in (1, 4, 8, 16):
-        ctx.set_tuning(lanes, 0)
+        c = on(ctx, dctx, 0, lanes)
+        c.set_tuning(lanes, 0)
         d_ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
         d_comp = torch.zeros(n, dtype=torch.int32, device="cuda")
-        ctx.verify_batch_device(dev(payload), dev(off), dev(lens), dev(slot), dev(conn), n, d_ok, d_comp,
-                                stream=torch.cuda.current_stream().cuda_stream)
+        c.verify_batch_device(dev(payload), dev(off), dev(lens), dev(slot), dev(conn), n, d_ok, d_comp,
+                              stream=torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
         assert (d_ok.cpu().numpy() == exp_ok).all()
         assert (d_comp.cpu().numpy().view(np.uint32) == exp_comp).all()
+        c.set_tuning(0, 0)
 
 
 def _verify_list_batch(oracle_lib, rng, n):
@@ -428,7 +435,7 @@ def _run_verify_list(ctx, batches, with_computed=True):
             for (ok, comp), b in zip(outs, batches)]
 
 
-def test_verify_batch_list(ctx, oracle_lib):
+def test_verify_batch_list(ctx, dctx, oracle_lib):
     """enet_hip_verify_batch_list_device: receive batches of every shape (empty,
     one DGRAM, odd sizes, 20 000 mixed DGRAMs) in one launch, at the default, 4,
     8 and 16 lanes (16: one launch per batch), with and without computed[]; and 70
@@ -437,13 +444,14 @@ def test_verify_batch_list(ctx, oracle_lib):
     batches = [_verify_list_batch(oracle_lib, rng, n) for n in (0, 1, 3, 700, 20_000, 0, 5000, 33)]
     try:
         for lanes in (0, 4, 8, 16):
-            ctx.set_tuning(lanes, 0)
+            c = on(ctx, dctx, 0, lanes)
+            c.set_tuning(lanes, 0)
             for wc in (True, False):
-                for i, ((ok, comp), b) in enumerate(zip(_run_verify_list(ctx, batches, wc), batches)):
+                for i, ((ok, comp), b) in enumerate(zip(_run_verify_list(c, batches, wc), batches)):
                     assert (ok == b[5]).all(), (lanes, wc, i)
                     if wc:
                         assert (comp == b[6]).all(), (lanes, i)
-        ctx.set_tuning(0, 0)
+            c.set_tuning(0, 0)
         many = [_verify_list_batch(oracle_lib, rng, int(rng.integers(0, 900))) for _ in range(70)]
         for i, ((ok, comp), b) in enumerate(zip(_run_verify_list(ctx, many), many)):
             assert (ok == b[5]).all() and (comp == b[6]).all(), i
@@ -453,7 +461,7 @@ def test_verify_batch_list(ctx, oracle_lib):
 
 
 @pytest.mark.parametrize("n", [1, 3000, 70_000])
-def test_verify_binned(ctx, oracle_lib, n):
+def test_verify_binned(ctx, dctx, oracle_lib, n):
     """Binned receive verify: mixed-length DGRAMs (6..1400 B, 2- and 4-byte headers),
     half correctly stamped, the rest corrupted or unstamped; ok/computed in caller order."""
     rng = np.random.default_rng(31 + n)
@@ -465,16 +473,18 @@ def test_verify_binned(ctx, oracle_lib, n):
         payload[o + s:o + s + 4] = np.frombuffer(np.uint32(stamped[i]).tobytes(), np.uint8)
     exp_ok, exp_comp = oracle_lib.verify(payload, off, lens, slot, conn)
     for lanes in (1, 4, 8):
-        ctx.set_tuning(lanes, 0)
+        c = on(ctx, dctx, 0, lanes)
+        c.set_tuning(lanes, 0)
         d_ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
         d_comp = torch.zeros(n, dtype=torch.int32, device="cuda")
-        wsb = ctx.verify_binned_workspace_size(n)
+        wsb = c.verify_binned_workspace_size(n)
         ws = torch.zeros(wsb, dtype=torch.uint8, device="cuda")
-        ctx.verify_batch_device_binned(dev(payload), dev(off), dev(lens), dev(slot), dev(conn), n, d_ok, ws, wsb,
-                                       d_comp, stream=torch.cuda.current_stream().cuda_stream)
+        c.verify_batch_device_binned(dev(payload), dev(off), dev(lens), dev(slot), dev(conn), n, d_ok, ws, wsb,
+                                     d_comp, stream=torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
         assert (d_ok.cpu().numpy() == exp_ok).all(), lanes
         assert (d_comp.cpu().numpy().view(np.uint32) == exp_comp).all(), lanes
+        c.set_tuning(0, 0)
     if n > 1:
         assert 0 < exp_ok.sum() < n
 
@@ -691,11 +701,19 @@ def test_vring_many_groups(ctx, dctx, oracle_lib, path, wgs):
 
 
 def test_product_library_rejects_sweep_paths(ctx):
-    """libenethip.so builds no sweep path (they exist in libenethip_diag.so only)."""
-    for path in (3, 8, 14, 18, 19, 20, 21, 22, 23):
+    """libenethip.so builds no sweep path and no lane count but 4 and 8 (the direct
+    and LDS-stream kernels, paths 1 / 2 and 1, 2, 16, 32, 64 lanes, exist in
+    libenethip_diag.so only since round 5)."""
+    for path in (1, 2, 3, 8, 14, 18, 19, 20, 21, 22, 23):
         with pytest.raises(enethip.ENetHipError):
             ctx.set_kernel_path(path)
     ctx.set_kernel_path(0)
+    for lanes in (1, 2, 16, 32, 64):
+        with pytest.raises(enethip.ENetHipError):
+            ctx.set_tuning(lanes, 0)
+    for lanes in (0, 4, 8):
+        ctx.set_tuning(lanes, 0)
+    ctx.set_tuning(0, 0)
 
 
 def _batch_list_cases(oracle_lib):
@@ -741,16 +759,17 @@ def test_batch_list(ctx, dctx, oracle_lib, path, wgs):
     8 lanes, one or two workgroups per CU; 16 lanes (one launch per batch on the
     stream kernel)."""
     cases = _batch_list_cases(oracle_lib)
-    ctx = on(ctx, dctx, path)
     try:
-        ctx.set_kernel_path(path)
         for lanes in (0, 4, 8, 16):
-            ctx.set_tuning(lanes, wgs)
-            for i, (got, c) in enumerate(zip(_run_list(ctx, cases), cases)):
-                assert (got == c[3]).all(), (path, lanes, i, np.nonzero(got != c[3])[0][:5])
+            c = on(ctx, dctx, path, lanes)
+            c.set_kernel_path(path)
+            c.set_tuning(lanes, wgs)
+            for i, (got, cs) in enumerate(zip(_run_list(c, cases), cases)):
+                assert (got == cs[3]).all(), (path, lanes, i, np.nonzero(got != cs[3])[0][:5])
     finally:
-        ctx.set_kernel_path(0)
-        ctx.set_tuning(0, 0)
+        for c in (ctx, dctx):
+            c.set_kernel_path(0)
+            c.set_tuning(0, 0)
 
 
 @pytest.mark.parametrize("wgs", WGS)
@@ -823,16 +842,17 @@ def test_all_empty_groups_every_path(ctx, dctx, oracle_lib, wgs):
              (payload, off, lens, exp)]
     paths = [0, 1, 17] if wgs else [0, 1] + [2 + g for g in range(N_STREAM_GEOMS)] + [17, 18, 21]
     for path in paths:
-        c = on(ctx, dctx, path)
         try:
-            c.set_kernel_path(path)
             for lanes in (1, 2, 4, 8, 16, 32, 64):
+                c = on(ctx, dctx, path, lanes)
+                c.set_kernel_path(path)
                 for i, (p, o, l, e) in enumerate(cases):
                     got = run_batch(c, p, o, l, lanes, wgs)
                     assert (got == e).all(), (path, lanes, i, np.nonzero(got != e)[0][:5])
         finally:
-            c.set_kernel_path(0)
-            c.set_tuning(0, 0)
+            for c in (ctx, dctx):
+                c.set_kernel_path(0)
+                c.set_tuning(0, 0)
 
 
 def test_verify_dgrams_over_64k(ctx, oracle_lib):

@@ -86,7 +86,7 @@ def main():
     from enethip import workloads
     import oracle as orc
     g = workloads.cfg5(a.messages)
-    ctx = enethip.Context(0, a.lanes, a.wgs, diag=a.path not in (0, 1, 2, 13, 17) or a.ablate != 0)
+    ctx = enethip.Context(0, a.lanes, a.wgs, diag=a.path not in (0, 13, 17) or a.lanes not in (0, 4, 8) or a.ablate != 0)
     if a.path:
         ctx.set_kernel_path(a.path)
     st = torch.cuda.Stream()

@@ -30,7 +30,7 @@ def main():
     ap.add_argument("--binned", action="store_true", help="length-binned entry (one batch per launch)")
     a = ap.parse_args()
     batches = bench.make_batches(a.config, a.rotate, 0)
-    diag = a.ablate != 0 or a.path not in bench.PRODUCT_PATHS   # sweep paths: libenethip_diag.so
+    diag = a.ablate != 0 or a.path not in bench.PRODUCT_PATHS or a.lanes not in bench.PRODUCT_LANES   # sweeps: diag
     eng = bench.GpuEngine(0, batches, a.lanes, a.wgs, diag=diag)
     if a.binned:
         eng.set_binned(True)

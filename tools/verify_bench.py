@@ -43,7 +43,7 @@ def main():
     import enethip
     from enethip import workloads
     import oracle as orc
-    ctx = enethip.Context(0, a.lanes, a.wgs)
+    ctx = enethip.Context(0, a.lanes, a.wgs, diag=a.lanes not in (0, 4, 8) or a.path not in (0, 13, 17))
     ctx.set_kernel_path(a.path)
     st = torch.cuda.Stream()
     off = np.arange(N, dtype=np.uint64) * L
