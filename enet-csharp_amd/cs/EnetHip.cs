@@ -218,6 +218,14 @@ namespace enet
             uint dstAddr, ushort dstPort, nuint* sent);
 
         [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_udp_receive_verify_submit(IntPtr ctx, int fd, byte* arena, nuint stride,
+            nuint maxDgrams, uint* peerConnectIds, nuint peerCount, int timeoutMs, uint* lengths, byte* ok,
+            nuint* received, int slot);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
+        public static extern int enet_hip_udp_receive_verify_complete(IntPtr ctx, int slot);
+
+        [DllImport(LIB, CallingConvention = CallingConvention.Cdecl)]
         public static extern int enet_hip_udp_receive_decompress_verify(IntPtr ctx, int fd, byte* arena,
             nuint stride, nuint maxDgrams, uint* peerConnectIds, nuint peerCount, int timeoutMs, uint* lengths,
             byte* ok, nuint* received);

@@ -52,6 +52,11 @@ struct enet_hip_context {
     hipEvent_t pipe_ev[2] = {nullptr, nullptr}; // the staging of stream s has been copied
     uint8_t* h_out = nullptr;                   // pinned landing zone of the D2H result copies
     size_t h_out_cap = 0;
+    // enet_hip_udp_receive_verify_submit / _complete: slot s's batch in flight on pipe[s]
+    // (its staging in h_pipe[s] / d_pipe[s]): the caller's ok[], the DGRAM count, pending
+    uint8_t* rx_ok[2] = {nullptr, nullptr};
+    size_t rx_n[2] = {0, 0};
+    bool rx_pending[2] = {false, false};
     uint8_t* d_ws = nullptr;                    // gather / binned workspace
     size_t d_ws_cap = 0;
     // fragment reassembly claim words (all ~0 between calls)

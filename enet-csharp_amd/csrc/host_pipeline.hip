@@ -134,6 +134,7 @@ int enet_hip_crc32_batch_host(enet_hip_context* ctx, const uint8_t* bytes, size_
     for (size_t i = 0; i < count; ++i)  // host-side shape check before any launch
         if (offsets[i] > byteCount || lengths[i] > byteCount - offsets[i]) return -static_cast<int>(hipErrorInvalidValue);
     std::lock_guard<std::mutex> lk(ctx->mu);
+    if (ctx->rx_pending[0] || ctx->rx_pending[1]) return -static_cast<int>(hipErrorInvalidValue);   // (async receive slots hold the staging)
     ENH_CHECK(hipSetDevice(ctx->device));
     int rc;
     if ((rc = pipeline_init(ctx))) return rc;
@@ -241,6 +242,7 @@ int enet_hip_crc32_gather_binned_host(enet_hip_context* ctx, const uint8_t* byte
     lo &= ~uint64_t(15);
     const size_t span = static_cast<size_t>(hi - lo);
     std::lock_guard<std::mutex> lk(ctx->mu);
+    if (ctx->rx_pending[0] || ctx->rx_pending[1]) return -static_cast<int>(hipErrorInvalidValue);   // (async receive slots hold the staging)
     ENH_CHECK(hipSetDevice(ctx->device));
     int rc;
     if ((rc = pipeline_init(ctx))) return rc;
@@ -283,29 +285,30 @@ int enet_hip_crc32_gather_binned_host(enet_hip_context* ctx, const uint8_t* byte
     return 0;
 }
 
-int enet_hip_udp_receive_verify(enet_hip_context* ctx, int fd, uint8_t* arena, size_t stride, size_t maxDgrams,
-                                const uint32_t* peerConnectIds, size_t peerCount, int timeoutMs, uint32_t* lengths,
-                                uint8_t* ok, size_t* received) {
-    if (!ctx || !received) return -static_cast<int>(hipErrorInvalidValue);
-    *received = 0;
-    if (!arena || !lengths || !ok || (peerCount && !peerConnectIds) || stride < 16)
-        return -static_cast<int>(hipErrorInvalidValue);
+// The receive batch of slot s (0 or 1): receive, header stage, pitched H2D, GPU verify
+// and D2H of the keep mask into slot s's pinned staging, all queued on pipe[s]; the
+// caller (under ctx->mu) waits with rx_complete.
+static int rx_submit(enet_hip_context* ctx, int slot, int fd, uint8_t* arena, size_t stride, size_t maxDgrams,
+                     const uint32_t* peerConnectIds, size_t peerCount, int timeoutMs, uint32_t* lengths, uint8_t* ok,
+                     size_t* received) {
     size_t n = 0;
     int rc = enet_hip_udp_receive(fd, arena, stride, maxDgrams, lengths, nullptr, nullptr, timeoutMs, &n);
     if (rc) return rc;                                   // -errno
     *received = n;
+    ctx->rx_ok[slot] = ok;
+    ctx->rx_n[slot] = n;
     if (n == 0) return 0;
-    std::lock_guard<std::mutex> lk(ctx->mu);
     ENH_CHECK(hipSetDevice(ctx->device));
     if ((rc = pipeline_init(ctx))) return rc;
-    // pinned staging: off u64 | len | slot | connect | verdict
+    // pinned staging: off u64 | len | slot | connect | verdict | ok (D2H)
     const size_t ho = align16(8 * n), hl = align16(4 * n), hv = align16(n);
-    if ((rc = ensure_pinned(&ctx->h_pipe[0], &ctx->h_pipe_cap[0], ho + 3 * hl + hv))) return rc;
-    uint64_t* h_off = reinterpret_cast<uint64_t*>(ctx->h_pipe[0]);
-    uint32_t* h_len = reinterpret_cast<uint32_t*>(ctx->h_pipe[0] + ho);
-    uint32_t* h_slot = reinterpret_cast<uint32_t*>(ctx->h_pipe[0] + ho + hl);
-    uint32_t* h_conn = reinterpret_cast<uint32_t*>(ctx->h_pipe[0] + ho + 2 * hl);
-    uint8_t* h_verdict = ctx->h_pipe[0] + ho + 3 * hl;
+    if ((rc = ensure_pinned(&ctx->h_pipe[slot], &ctx->h_pipe_cap[slot], ho + 3 * hl + 2 * hv))) return rc;
+    uint64_t* h_off = reinterpret_cast<uint64_t*>(ctx->h_pipe[slot]);
+    uint32_t* h_len = reinterpret_cast<uint32_t*>(ctx->h_pipe[slot] + ho);
+    uint32_t* h_slot = reinterpret_cast<uint32_t*>(ctx->h_pipe[slot] + ho + hl);
+    uint32_t* h_conn = reinterpret_cast<uint32_t*>(ctx->h_pipe[slot] + ho + 2 * hl);
+    uint8_t* h_verdict = ctx->h_pipe[slot] + ho + 3 * hl;
+    uint8_t* h_ok = h_verdict + hv;
     if ((rc = enet_hip_parse_headers(arena, stride, lengths, n, peerConnectIds, peerCount, h_slot, h_conn, h_verdict)))
         return rc;
     size_t maxLen = 16;
@@ -318,23 +321,77 @@ int enet_hip_udp_receive_verify(enet_hip_context* ctx, int fd, uint8_t* arena, s
     }
     // device: [DGRAMs at `pitch` | off | len | slot | connect | ok]
     const size_t db = align16(n * pitch + 16);
-    if ((rc = ensure_device(&ctx->d_pipe[0], &ctx->d_pipe_cap[0], db + ho + 3 * hl + hv))) return rc;
-    uint8_t* d = ctx->d_pipe[0];
+    if ((rc = ensure_device(&ctx->d_pipe[slot], &ctx->d_pipe_cap[slot], db + ho + 3 * hl + hv))) return rc;
+    uint8_t* d = ctx->d_pipe[slot];
     uint64_t* d_off = reinterpret_cast<uint64_t*>(d + db);
     uint32_t* d_len = reinterpret_cast<uint32_t*>(d + db + ho);
     uint32_t* d_slot = reinterpret_cast<uint32_t*>(d + db + ho + hl);
     uint32_t* d_conn = reinterpret_cast<uint32_t*>(d + db + ho + 2 * hl);
     uint8_t* d_ok = d + db + ho + 3 * hl;
-    hipStream_t st = ctx->pipe[0];
+    hipStream_t st = ctx->pipe[slot];
     // only the first maxLen bytes of every stride-sized receive slot cross PCIe
     ENH_CHECK(hipMemcpy2DAsync(d, pitch, arena, stride, maxLen, n, hipMemcpyHostToDevice, st));
     ENH_CHECK(hipMemcpyAsync(d_off, h_off, ho + 3 * hl, hipMemcpyHostToDevice, st));   // off | len | slot | connect
     if ((rc = enet_hip_verify_batch_device(ctx, d, d_off, d_len, d_slot, d_conn, n, d_ok, nullptr, st))) return rc;
-    ENH_CHECK(hipMemcpyAsync(ok, d_ok, n, hipMemcpyDeviceToHost, st));
-    ENH_CHECK(hipStreamSynchronize(st));
-    for (size_t i = 0; i < n; ++i)
-        if (h_verdict[i] != ENET_HIP_DGRAM_CHECKSUM) ok[i] = 0;
+    ENH_CHECK(hipMemcpyAsync(h_ok, d_ok, n, hipMemcpyDeviceToHost, st));
+    ctx->rx_pending[slot] = true;
     return 0;
+}
+
+// slot s's keep mask into the caller's ok[] once its stream is done (header-stage drops: 0)
+static int rx_complete(enet_hip_context* ctx, int slot) {
+    if (!ctx->rx_pending[slot]) return 0;                // (an empty batch: nothing queued)
+    ctx->rx_pending[slot] = false;
+    ENH_CHECK(hipSetDevice(ctx->device));
+    ENH_CHECK(hipStreamSynchronize(ctx->pipe[slot]));
+    const size_t n = ctx->rx_n[slot];
+    const size_t ho = align16(8 * n), hl = align16(4 * n), hv = align16(n);
+    const uint8_t* h_verdict = ctx->h_pipe[slot] + ho + 3 * hl;
+    const uint8_t* h_ok = h_verdict + hv;
+    for (size_t i = 0; i < n; ++i) ctx->rx_ok[slot][i] = h_verdict[i] == ENET_HIP_DGRAM_CHECKSUM ? h_ok[i] : 0u;
+    return 0;
+}
+
+int enet_hip_udp_receive_verify(enet_hip_context* ctx, int fd, uint8_t* arena, size_t stride, size_t maxDgrams,
+                                const uint32_t* peerConnectIds, size_t peerCount, int timeoutMs, uint32_t* lengths,
+                                uint8_t* ok, size_t* received) {
+    if (!ctx || !received) return -static_cast<int>(hipErrorInvalidValue);
+    *received = 0;
+    if (!arena || !lengths || !ok || (peerCount && !peerConnectIds) || stride < 16)
+        return -static_cast<int>(hipErrorInvalidValue);
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (ctx->rx_pending[0] || ctx->rx_pending[1]) return -static_cast<int>(hipErrorInvalidValue);   // (async slots in flight)
+    int rc = rx_submit(ctx, 0, fd, arena, stride, maxDgrams, peerConnectIds, peerCount, timeoutMs, lengths, ok,
+                       received);
+    if (rc) {
+        ctx->rx_pending[0] = false;
+        return rc;
+    }
+    return rx_complete(ctx, 0);
+}
+
+int enet_hip_udp_receive_verify_submit(enet_hip_context* ctx, int fd, uint8_t* arena, size_t stride, size_t maxDgrams,
+                                       const uint32_t* peerConnectIds, size_t peerCount, int timeoutMs,
+                                       uint32_t* lengths, uint8_t* ok, size_t* received, int slot) {
+    if (!ctx || !received) return -static_cast<int>(hipErrorInvalidValue);
+    *received = 0;
+    if (!arena || !lengths || !ok || (peerCount && !peerConnectIds) || stride < 16 || slot < 0 || slot > 1)
+        return -static_cast<int>(hipErrorInvalidValue);
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (ctx->rx_pending[slot]) return -static_cast<int>(hipErrorInvalidValue);   // (complete it first)
+    const int rc = rx_submit(ctx, slot, fd, arena, stride, maxDgrams, peerConnectIds, peerCount, timeoutMs, lengths,
+                             ok, received);
+    if (rc && ctx->rx_pending[slot]) {                   // (a failure after the launch: drain it)
+        (void)hipStreamSynchronize(ctx->pipe[slot]);
+        ctx->rx_pending[slot] = false;
+    }
+    return rc;
+}
+
+int enet_hip_udp_receive_verify_complete(enet_hip_context* ctx, int slot) {
+    if (!ctx || slot < 0 || slot > 1) return -static_cast<int>(hipErrorInvalidValue);
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    return rx_complete(ctx, slot);
 }
 
 int enet_hip_udp_receive_decompress_verify(enet_hip_context* ctx, int fd, uint8_t* arena, size_t stride,
@@ -350,6 +407,7 @@ int enet_hip_udp_receive_decompress_verify(enet_hip_context* ctx, int fd, uint8_
     *received = n;
     if (n == 0) return 0;
     std::lock_guard<std::mutex> lk(ctx->mu);
+    if (ctx->rx_pending[0] || ctx->rx_pending[1]) return -static_cast<int>(hipErrorInvalidValue);   // (async receive slots hold the staging)
     ENH_CHECK(hipSetDevice(ctx->device));
     if ((rc = pipeline_init(ctx))) return rc;
     // pinned staging: off u64 | len | slot | connect | verdict, then the compressed
@@ -490,6 +548,7 @@ int enet_hip_udp_compress_stamp_send(enet_hip_context* ctx, int fd, uint8_t* byt
     int rc;
     {
         std::lock_guard<std::mutex> lk(ctx->mu);
+        if (ctx->rx_pending[0] || ctx->rx_pending[1]) return -static_cast<int>(hipErrorInvalidValue);   // (async receive slots hold the staging)
         ENH_CHECK(hipSetDevice(ctx->device));
         if ((rc = pipeline_init(ctx))) return rc;
         const size_t ab = align16(total + 16), ho = align16(8 * n), hl = align16(4 * n);

@@ -46,6 +46,7 @@ EXPORTED_SYMBOLS = (
     "enet_hip_crc32_gather_binned_host", "enet_hip_udp_receive", "enet_hip_parse_headers", "enet_hip_udp_send",
     "enet_hip_stamp_callback", "enet_hip_verify_callback", "enet_hip_udp_receive_verify", "enet_hip_udp_stamp_send",
     "enet_hip_udp_receive_decompress_verify", "enet_hip_udp_compress_stamp_send",
+    "enet_hip_udp_receive_verify_submit", "enet_hip_udp_receive_verify_complete",
 )
 
 # include/enet_hip.h socket-harness constants
@@ -176,7 +177,12 @@ def load(path: str | None = None, diag: bool = False) -> ctypes.CDLL:
     L.enet_hip_udp_receive_verify.argtypes = [vp, i32, vp, sz, sz, vp, sz, i32, vp, vp, szp]
     L.enet_hip_udp_stamp_send.restype = i32
     L.enet_hip_udp_stamp_send.argtypes = [vp, i32, vp, sz, vp, vp, sz, vp, vp, sz, u32, ctypes.c_uint16, szp]
-    # (an ENET_HIP_LIBRARY build from before round 5 lacks these two: measurement A/B only)
+    # (an ENET_HIP_LIBRARY build from before round 5 lacks these: measurement A/B only)
+    if p in (os.path.join(PKG_ROOT, "libenethip.so"), DIAG_LIB_PATH) or hasattr(L, "enet_hip_udp_receive_verify_submit"):
+        L.enet_hip_udp_receive_verify_submit.restype = i32
+        L.enet_hip_udp_receive_verify_submit.argtypes = [vp, i32, vp, sz, sz, vp, sz, i32, vp, vp, szp, i32]
+        L.enet_hip_udp_receive_verify_complete.restype = i32
+        L.enet_hip_udp_receive_verify_complete.argtypes = [vp, i32]
     if p in (os.path.join(PKG_ROOT, "libenethip.so"), DIAG_LIB_PATH) or hasattr(L, "enet_hip_udp_compress_stamp_send"):
         L.enet_hip_udp_receive_decompress_verify.restype = i32
         L.enet_hip_udp_receive_decompress_verify.argtypes = [vp, i32, vp, sz, sz, vp, sz, i32, vp, vp, szp]
@@ -241,6 +247,7 @@ class Context:
     def __init__(self, device: int = 0, lanes_per_packet: int = 0, workgroups_per_cu: int = 0, diag: bool = False):
         self.lib = load(diag=diag)
         self.diag = diag
+        self._rx = [None, None]                                 # receive slots' ok[] in flight
         h = ctypes.c_void_p()
         _check("enet_hip_context_create", self.lib.enet_hip_context_create(int(device), ctypes.byref(h)))
         self.handle = h
@@ -410,6 +417,26 @@ class Context:
             self.handle, int(fd), _ptr(payload), int(payload.nbytes), _ptr(seg_off), _ptr(seg_len), len(seg_off),
             _ptr(seg_first), _ptr(slot_off), len(seg_first) - 1, int(addr), int(port), ctypes.byref(sent)))
         return sent.value
+
+    def udp_receive_verify_submit(self, slot: int, fd: int, arena, stride: int, max_dgrams: int, peer_connect_ids,
+                                  timeout_ms: int = 0):
+        """-> (count, lengths[count], ok[count]) with ok[] filled only by
+        udp_receive_verify_complete(slot): the receive and its queued GPU verify of slot
+        0 or 1 (the GPU work overlaps the caller's next receive)."""
+        peers = _u(peer_connect_ids, np.uint32)
+        lens = np.zeros(max(1, max_dgrams), np.uint32)
+        ok = np.zeros(max(1, max_dgrams), np.uint8)
+        got = ctypes.c_size_t(0)
+        _check("enet_hip_udp_receive_verify_submit", self.lib.enet_hip_udp_receive_verify_submit(
+            self.handle, int(fd), _ptr(arena), int(stride), int(max_dgrams), _ptr(peers) if len(peers) else None,
+            len(peers), int(timeout_ms), _ptr(lens), _ptr(ok), ctypes.byref(got), int(slot)))
+        self._rx[slot] = ok                                     # (held until its complete)
+        n = got.value
+        return n, lens[:n], ok[:n]
+
+    def udp_receive_verify_complete(self, slot: int) -> None:
+        _check("enet_hip_udp_receive_verify_complete", self.lib.enet_hip_udp_receive_verify_complete(self.handle, int(slot)))
+        self._rx[slot] = None
 
     def udp_receive_decompress_verify(self, fd: int, arena, stride: int, max_dgrams: int, peer_connect_ids,
                                       timeout_ms: int = 0):

@@ -355,6 +355,25 @@ ENET_HIP_API int enet_hip_udp_receive_verify(enet_hip_context* ctx, int fd, uint
                                              size_t maxDgrams, const uint32_t* peerConnectIds, size_t peerCount,
                                              int timeoutMs, uint32_t* lengths, uint8_t* ok, size_t* received);
 
+/* enet_hip_udp_receive_verify in two halves, so that the GPU work of one batch
+ * overlaps the socket receive of the next.  A host keeps two receive arenas (pinned:
+ * enet_hip_host_alloc) and uses them in turn as slot 0 and slot 1:
+ *   submit(slot 0, arena A); loop { submit(slot 1, arena B); complete(slot 0) ->
+ *   process A; submit(slot 0, arena A); complete(slot 1) -> process B; }
+ * _submit receives and runs the header stage like enet_hip_udp_receive_verify
+ * (lengths[] and *received are set when it returns), queues the pitched H2D, the GPU
+ * verify and the D2H of the keep mask on the context's pipeline stream `slot`, and
+ * returns without waiting; _complete(slot) waits for that batch and writes ok[] (the
+ * header stage's drops 0).  arena, lengths and ok of a slot stay the caller's until
+ * its _complete.  -hipErrorInvalidValue for a slot already in flight, and from the
+ * other host-memory entry points of the context while a slot is in flight (they
+ * share its staging). */
+ENET_HIP_API int enet_hip_udp_receive_verify_submit(enet_hip_context* ctx, int fd, uint8_t* arena, size_t stride,
+                                                    size_t maxDgrams, const uint32_t* peerConnectIds,
+                                                    size_t peerCount, int timeoutMs, uint32_t* lengths, uint8_t* ok,
+                                                    size_t* received, int slot);
+ENET_HIP_API int enet_hip_udp_receive_verify_complete(enet_hip_context* ctx, int slot);
+
 /* Send side on the GPU: every DGRAM's CRC over its gather list
  * (enet_hip_crc32_gather_binned_host), written into its slot as protocol.cs:1697
  * does (slot bytes hold connectID or 0 on entry; `bytes` is modified), then

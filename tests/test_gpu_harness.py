@@ -305,3 +305,83 @@ def test_gpu_compress_stamp_send_and_decompress_verify(ctx, oracle_lib, corrupt)
         free_pinned(p)
         rx.close()
         tx.close()
+
+
+def test_gpu_receive_verify_submit_complete_two_slots(ctx, oracle_lib):  # noqa: F811
+    """enet_hip_udp_receive_verify_submit / _complete: batches received into two arenas
+    in turn, each one's GPU verify in flight while the next is received; every keep
+    mask equal to the oracle's (header stage restated: expected_keep), corrupted and odd
+    DGRAMs among them.  While a slot is in flight the synchronous receive and the other
+    host-memory entries refuse (they share its staging), and a slot cannot be submitted
+    twice."""
+    sb = workloads.send_batch(2400, seed=95)
+    g = sb.gather
+    rng = np.random.default_rng(96)
+    rx, tx, port = sockets()
+    arenas = [pinned(STRIDE * 512), pinned(STRIDE * 512)]
+    try:
+        # stamp on the CPU (the oracle), corrupt 60 DGRAMs, then send in bursts of 300
+        stamps = oracle_stamps(oracle_lib, sb)
+        pos = g.seg_off[g.seg_first[:-1]].astype(np.int64) + sb.slot_off.astype(np.int64)
+        for d in range(sb.n):
+            g.payload[pos[d]:pos[d] + 4] = np.frombuffer(np.uint32(stamps[d]).tobytes(), np.uint8)
+        for d in rng.choice(sb.n, 60, replace=False):
+            s = int(g.seg_first[d]) + int(rng.integers(0, 3))
+            if g.seg_len[s]:
+                g.payload[int(g.seg_off[s]) + int(rng.integers(0, int(g.seg_len[s])))] ^= np.uint8(4)
+        pending = {}
+        got = 0
+        kept = 0
+        bursts = list(range(0, sb.n, 300))
+        for k, a in enumerate(bursts):
+            b = min(sb.n, a + 300)
+            assert enethip.udp_send(tx.fileno(), g.payload, g.seg_off, g.seg_len, g.seg_first[a:b + 1],
+                                    LOOPBACK, port) == b - a
+            if k == len(bursts) - 1:
+                for dg in odd_dgrams(sb.peers):
+                    tx.sendto(dg, ("127.0.0.1", port))
+            slot = k & 1
+            arena = arenas[slot][0]
+            rows = 0
+            while rows < b - a:
+                if slot in pending:                               # the slot's previous batch first
+                    arena_p, n_p, lens_p, ok_p = pending.pop(slot)
+                    ctx.udp_receive_verify_complete(slot)
+                    assert (ok_p == expected_keep(oracle_lib, arena_p, STRIDE, lens_p, sb.peers)).all()
+                    kept += int(ok_p.sum())
+                n, lens, ok = ctx.udp_receive_verify_submit(slot, rx.fileno(), arena, STRIDE, 512, sb.peers,
+                                                            timeout_ms=2000)
+                assert n > 0
+                if slot == 0 and k == 0:                          # in flight: the others refuse
+                    with pytest.raises(enethip.ENetHipError):
+                        ctx.udp_receive_verify_submit(slot, rx.fileno(), arenas[1][0], STRIDE, 512, sb.peers)
+                    with pytest.raises(enethip.ENetHipError):
+                        ctx.udp_receive_verify(rx.fileno(), arenas[1][0], STRIDE, 512, sb.peers)
+                pending[slot] = (arena, n, lens.copy(), ok)
+                got += n
+                rows += n
+                if rows < b - a:                                  # more of this burst: complete now
+                    arena_p, n_p, lens_p, ok_p = pending.pop(slot)
+                    ctx.udp_receive_verify_complete(slot)
+                    assert (ok_p == expected_keep(oracle_lib, arena_p, STRIDE, lens_p, sb.peers)).all()
+                    kept += int(ok_p.sum())
+        for slot, (arena_p, n_p, lens_p, ok_p) in list(pending.items()):
+            ctx.udp_receive_verify_complete(slot)
+            assert (ok_p == expected_keep(oracle_lib, arena_p, STRIDE, lens_p, sb.peers)).all()
+            kept += int(ok_p.sum())
+        # the odd DGRAMs may still be queued: drain them through slot 0
+        while got < sb.n + len(odd_dgrams(sb.peers)):
+            n, lens, ok = ctx.udp_receive_verify_submit(0, rx.fileno(), arenas[0][0], STRIDE, 512, sb.peers,
+                                                        timeout_ms=2000)
+            assert n > 0
+            ctx.udp_receive_verify_complete(0)
+            assert (ok == expected_keep(oracle_lib, arenas[0][0], STRIDE, lens, sb.peers)).all()
+            kept += int(ok.sum())
+            got += n
+        assert got == sb.n + len(odd_dgrams(sb.peers))
+        assert sb.n - 60 <= kept < sb.n                           # the corrupted ones dropped
+    finally:
+        for _, p in arenas:
+            free_pinned(p)
+        rx.close()
+        tx.close()

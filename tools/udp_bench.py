@@ -7,6 +7,9 @@ Receive side: a sender thread streams pre-stamped ENet DGRAMs (workloads.send_ba
 drains the socket for SECONDS per mode:
   gpu      enet_hip_udp_receive_verify (recvmmsg -> header stage -> pitched H2D ->
            GPU verify -> keep mask);
+  gpu2     the same in two halves over two arenas in turn
+           (enet_hip_udp_receive_verify_submit / _complete): the GPU work of one batch
+           overlaps the receive of the next;
   callback enet_hip_udp_receive + header stage + enet_hip_verify_callback (the
            per-DGRAM path ENet runs today: enet_hip_crc32 per DGRAM);
   port     the same with the oracle's byte-serial restatement of packet.cs:142-160
@@ -89,13 +92,34 @@ def port_verify(ol, arena, lens, slot, conn, verdict):
 def receive_mode(mode, ctx, sb, ol):
     rx, tx, port = sockets()
     arena, p = pinned(STRIDE * 8192)
+    arena2, p2 = pinned(STRIDE * 8192) if mode == "gpu2" else (None, None)
     snd = Sender(tx, port, sb)
     snd.start()
     got = kept = nbytes = calls = 0
     bad = 0
+    pend = {}                                       # gpu2: slot -> (count, lengths, ok) in flight
+    rs = 0                                          # gpu2: the slot to submit next
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < SECONDS:
-        if mode == "gpu":
+    while time.perf_counter() - t0 < SECONDS or pend:
+        if mode == "gpu2":
+            if time.perf_counter() - t0 < SECONDS:
+                if rs in pend:                      # (two in flight: the older one first)
+                    n, lens, ok = pend.pop(rs)
+                    ctx.udp_receive_verify_complete(rs)
+                else:
+                    n = 0
+                n2, lens2, ok2 = ctx.udp_receive_verify_submit(rs, rx.fileno(), (arena, arena2)[rs], STRIDE,
+                                                               8192, sb.peers, timeout_ms=100)
+                if n2:
+                    pend[rs] = (n2, lens2.copy(), ok2)
+                rs ^= 1
+                if n == 0:
+                    continue
+            else:                                   # time is up: the slots still in flight
+                s0 = next(iter(pend))
+                n, lens, ok = pend.pop(s0)
+                ctx.udp_receive_verify_complete(s0)
+        elif mode == "gpu":
             n, lens, ok = ctx.udp_receive_verify(rx.fileno(), arena, STRIDE, 8192, sb.peers, timeout_ms=100)
         else:
             n, lens, _, _ = enethip.udp_receive(rx.fileno(), arena, STRIDE, 8192, timeout_ms=100)
@@ -116,6 +140,7 @@ def receive_mode(mode, ctx, sb, ol):
     rx.close()
     tx.close()
     free(p)
+    free(p2)
     assert bad == 0, f"{mode}: {bad} stamped DGRAMs dropped"
     return {"side": "receive", "mode": mode, "seconds": round(dt, 2), "dgrams": got, "kept": kept,
             "dgrams_per_s": round(got / dt), "GBps": round(nbytes / dt / 1e9, 3),
@@ -177,7 +202,7 @@ def main():
     ctx = enethip.Context(0)
     print(json.dumps({"cores": len(os.sched_getaffinity(0)), "dgrams_per_batch": sb.n,
                       "dgram_bytes": sb.gather.dgram_bytes}), flush=True)
-    for mode in ("recv", "gpu", "callback", "port"):
+    for mode in ("recv", "gpu", "gpu2", "callback", "port"):
         print(json.dumps(receive_mode(mode, ctx, sb, ol)), flush=True)
     sb2 = workloads.send_batch(int(os.environ.get("UDP_BENCH_DGRAMS", "65536")), body=(1188, 1188), seed=10)
     for mode in ("gpu", "callback"):
