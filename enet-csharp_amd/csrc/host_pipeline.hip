@@ -355,8 +355,8 @@ static int rx_complete(enet_hip_context* ctx, int slot) {
 int enet_hip_udp_receive_verify(enet_hip_context* ctx, int fd, uint8_t* arena, size_t stride, size_t maxDgrams,
                                 const uint32_t* peerConnectIds, size_t peerCount, int timeoutMs, uint32_t* lengths,
                                 uint8_t* ok, size_t* received) {
+    if (received) *received = 0;
     if (!ctx || !received) return -static_cast<int>(hipErrorInvalidValue);
-    *received = 0;
     if (!arena || !lengths || !ok || (peerCount && !peerConnectIds) || stride < 16)
         return -static_cast<int>(hipErrorInvalidValue);
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -373,8 +373,8 @@ int enet_hip_udp_receive_verify(enet_hip_context* ctx, int fd, uint8_t* arena, s
 int enet_hip_udp_receive_verify_submit(enet_hip_context* ctx, int fd, uint8_t* arena, size_t stride, size_t maxDgrams,
                                        const uint32_t* peerConnectIds, size_t peerCount, int timeoutMs,
                                        uint32_t* lengths, uint8_t* ok, size_t* received, int slot) {
+    if (received) *received = 0;
     if (!ctx || !received) return -static_cast<int>(hipErrorInvalidValue);
-    *received = 0;
     if (!arena || !lengths || !ok || (peerCount && !peerConnectIds) || stride < 16 || slot < 0 || slot > 1)
         return -static_cast<int>(hipErrorInvalidValue);
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -397,8 +397,8 @@ int enet_hip_udp_receive_verify_complete(enet_hip_context* ctx, int slot) {
 int enet_hip_udp_receive_decompress_verify(enet_hip_context* ctx, int fd, uint8_t* arena, size_t stride,
                                            size_t maxDgrams, const uint32_t* peerConnectIds, size_t peerCount,
                                            int timeoutMs, uint32_t* lengths, uint8_t* ok, size_t* received) {
+    if (received) *received = 0;
     if (!ctx || !received) return -static_cast<int>(hipErrorInvalidValue);
-    *received = 0;
     if (!arena || !lengths || !ok || (peerCount && !peerConnectIds) || stride < kRecvBuffer)
         return -static_cast<int>(hipErrorInvalidValue);
     size_t n = 0;

@@ -84,6 +84,15 @@ def test_errors_without_device():
     # argument errors are reported as -hipErrorInvalidValue before touching a device
     assert lib.enet_hip_crc32_batch_device(None, None, None, None, 1, None, None) == -1
     assert lib.enet_hip_set_tuning(None, 4, 2) == -1
+    # the round-5 socket pipelines: a null context or a missing output is refused first
+    got = ctypes.c_size_t(7)
+    assert lib.enet_hip_udp_receive_verify_submit(None, 0, None, 4096, 1, None, 0, 0, None, None,
+                                                  ctypes.byref(got), 0) == -1 and got.value == 0
+    assert lib.enet_hip_udp_receive_verify_complete(None, 0) == -1
+    assert lib.enet_hip_udp_receive_decompress_verify(None, 0, None, 4096, 1, None, 0, 0, None, None,
+                                                      ctypes.byref(got)) == -1
+    assert lib.enet_hip_udp_compress_stamp_send(None, 0, None, 0, None, None, 0, None, None, 0, 0, 0,
+                                                ctypes.byref(got)) == -1
     assert enethip.error_string(0) == "success"
 
 
