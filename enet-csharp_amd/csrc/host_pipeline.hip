@@ -363,7 +363,8 @@ int enet_hip_udp_receive_verify(enet_hip_context* ctx, int fd, uint8_t* arena, s
     if (ctx->rx_pending[0] || ctx->rx_pending[1]) return -static_cast<int>(hipErrorInvalidValue);   // (async slots in flight)
     int rc = rx_submit(ctx, 0, fd, arena, stride, maxDgrams, peerConnectIds, peerCount, timeoutMs, lengths, ok,
                        received);
-    if (rc) {
+    if (rc) {                                            // (whatever was queued before the failure: drained)
+        if (ctx->pipe[0]) (void)hipStreamSynchronize(ctx->pipe[0]);
         ctx->rx_pending[0] = false;
         return rc;
     }
@@ -381,8 +382,8 @@ int enet_hip_udp_receive_verify_submit(enet_hip_context* ctx, int fd, uint8_t* a
     if (ctx->rx_pending[slot]) return -static_cast<int>(hipErrorInvalidValue);   // (complete it first)
     const int rc = rx_submit(ctx, slot, fd, arena, stride, maxDgrams, peerConnectIds, peerCount, timeoutMs, lengths,
                              ok, received);
-    if (rc && ctx->rx_pending[slot]) {                   // (a failure after the launch: drain it)
-        (void)hipStreamSynchronize(ctx->pipe[slot]);
+    if (rc) {                                            // (whatever was queued before the failure: drained)
+        if (ctx->pipe[slot]) (void)hipStreamSynchronize(ctx->pipe[slot]);
         ctx->rx_pending[slot] = false;
     }
     return rc;
