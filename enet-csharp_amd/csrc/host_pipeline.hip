@@ -285,9 +285,25 @@ int enet_hip_crc32_gather_binned_host(enet_hip_context* ctx, const uint8_t* byte
     return 0;
 }
 
-// The receive batch of slot s (0 or 1): receive, header stage, pitched H2D, GPU verify
-// and D2H of the keep mask into slot s's pinned staging, all queued on pipe[s]; the
-// caller (under ctx->mu) waits with rx_complete.
+// The device address of pinned host memory (hipHostMalloc'd or registered), or null for
+// pageable memory: the kernels can then read it in place over PCIe.
+static uint8_t* pinned_device_view(void* host) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, host) != hipSuccess) {
+        (void)hipGetLastError();                         // (pageable memory: not an error here)
+        return nullptr;
+    }
+    return a.type == hipMemoryTypeHost ? static_cast<uint8_t*>(a.devicePointer) : nullptr;
+}
+
+// The receive batch of slot s (0 or 1): receive, header stage, GPU verify and the keep
+// mask into slot s's pinned staging, all queued on pipe[s]; the caller (under ctx->mu)
+// waits with rx_complete.  A pinned arena (the usual case: enet_hip_host_alloc) is
+// verified in place: the kernel reads the DGRAMs at their arena offsets and the metadata
+// from the slot's pinned staging over PCIe, and writes the keep mask straight into it --
+// one launch and no copies, where the copy form queues a pitched H2D, a metadata H2D and
+// a D2H around it (each several microseconds for a batch of a few dozen DGRAMs).  A
+// pageable arena takes the copy form: only each DGRAM slot's first maxLen bytes cross.
 static int rx_submit(enet_hip_context* ctx, int slot, int fd, uint8_t* arena, size_t stride, size_t maxDgrams,
                      const uint32_t* peerConnectIds, size_t peerCount, int timeoutMs, uint32_t* lengths, uint8_t* ok,
                      size_t* received) {
@@ -311,6 +327,22 @@ static int rx_submit(enet_hip_context* ctx, int slot, int fd, uint8_t* arena, si
     uint8_t* h_ok = h_verdict + hv;
     if ((rc = enet_hip_parse_headers(arena, stride, lengths, n, peerConnectIds, peerCount, h_slot, h_conn, h_verdict)))
         return rc;
+    hipStream_t st = ctx->pipe[slot];
+    uint8_t* zc = pinned_device_view(arena);
+    uint8_t* zs = zc ? pinned_device_view(ctx->h_pipe[slot]) : nullptr;
+    if (zc && zs) {
+        for (size_t i = 0; i < n; ++i) {
+            h_off[i] = i * stride;
+            h_len[i] = h_verdict[i] == ENET_HIP_DGRAM_CHECKSUM ? lengths[i] : 0u;   // header-stage drops: no slot
+        }
+        if ((rc = enet_hip_verify_batch_device(ctx, zc, reinterpret_cast<uint64_t*>(zs), reinterpret_cast<uint32_t*>(zs + ho),
+                                               reinterpret_cast<uint32_t*>(zs + ho + hl),
+                                               reinterpret_cast<uint32_t*>(zs + ho + 2 * hl), n, zs + ho + 3 * hl + hv,
+                                               nullptr, st)))
+            return rc;
+        ctx->rx_pending[slot] = true;
+        return 0;
+    }
     size_t maxLen = 16;
     for (size_t i = 0; i < n; ++i)
         if (h_verdict[i] == ENET_HIP_DGRAM_CHECKSUM) maxLen = std::max<size_t>(maxLen, lengths[i]);
@@ -328,7 +360,6 @@ static int rx_submit(enet_hip_context* ctx, int slot, int fd, uint8_t* arena, si
     uint32_t* d_slot = reinterpret_cast<uint32_t*>(d + db + ho + hl);
     uint32_t* d_conn = reinterpret_cast<uint32_t*>(d + db + ho + 2 * hl);
     uint8_t* d_ok = d + db + ho + 3 * hl;
-    hipStream_t st = ctx->pipe[slot];
     // only the first maxLen bytes of every stride-sized receive slot cross PCIe
     ENH_CHECK(hipMemcpy2DAsync(d, pitch, arena, stride, maxLen, n, hipMemcpyHostToDevice, st));
     ENH_CHECK(hipMemcpyAsync(d_off, h_off, ho + 3 * hl, hipMemcpyHostToDevice, st));   // off | len | slot | connect

@@ -346,11 +346,13 @@ ENET_HIP_API int enet_hip_verify_callback(uint8_t* arena, size_t stride, const u
                                           const uint32_t* slotOffsets, const uint32_t* connectIds,
                                           const uint8_t* verdict, size_t count, uint8_t* ok);
 
-/* Receive side on the GPU, socket to keep mask: enet_hip_udp_receive into `arena`
- * (pinned: enet_hip_host_alloc), the header stage, one pitched H2D (only each slot's
- * first maxLen bytes cross PCIe), receive verify of the whole batch
- * (enet_hip_verify_batch_device) and D2H: ok[i] = 1 where ENet keeps DGRAM i.  The
- * arena is not modified.  Synchronous. */
+/* Receive side on the GPU, socket to keep mask: enet_hip_udp_receive into `arena`,
+ * the header stage, receive verify of the whole batch (enet_hip_verify_batch_device):
+ * ok[i] = 1 where ENet keeps DGRAM i.  A pinned arena (enet_hip_host_alloc, or host
+ * memory registered with HIP) is verified in place: the kernel reads the DGRAMs and the
+ * metadata over PCIe and writes the keep mask into pinned staging, with no copies.  A
+ * pageable arena takes one pitched H2D (only each slot's first maxLen bytes cross PCIe)
+ * and a D2H of the keep mask.  The arena is not modified.  Synchronous. */
 ENET_HIP_API int enet_hip_udp_receive_verify(enet_hip_context* ctx, int fd, uint8_t* arena, size_t stride,
                                              size_t maxDgrams, const uint32_t* peerConnectIds, size_t peerCount,
                                              int timeoutMs, uint32_t* lengths, uint8_t* ok, size_t* received);
@@ -361,8 +363,9 @@ ENET_HIP_API int enet_hip_udp_receive_verify(enet_hip_context* ctx, int fd, uint
  *   submit(slot 0, arena A); loop { submit(slot 1, arena B); complete(slot 0) ->
  *   process A; submit(slot 0, arena A); complete(slot 1) -> process B; }
  * _submit receives and runs the header stage like enet_hip_udp_receive_verify
- * (lengths[] and *received are set when it returns), queues the pitched H2D, the GPU
- * verify and the D2H of the keep mask on the context's pipeline stream `slot`, and
+ * (lengths[] and *received are set when it returns), queues the GPU verify (in place
+ * on a pinned arena; else with the pitched H2D and the keep mask's D2H) on the
+ * context's pipeline stream `slot`, and
  * returns without waiting; _complete(slot) waits for that batch and writes ok[] (the
  * header stage's drops 0).  arena, lengths and ok of a slot stay the caller's until
  * its _complete.  -hipErrorInvalidValue for a slot already in flight, and from the

@@ -107,17 +107,19 @@ def test_gather_binned_host_full_cfg5(ctx, oracle_lib):  # noqa: F811
     assert (ctx.gather_binned_host(payload, offs, lens, sl) == exp[100:300]).all()
 
 
-@pytest.mark.parametrize("corrupt", [0, 61])
-def test_gpu_stamp_send_and_receive_verify(ctx, oracle_lib, corrupt):  # noqa: F811
+@pytest.mark.parametrize("corrupt,kind", [(0, "pinned"), (61, "pinned"), (61, "pageable")])
+def test_gpu_stamp_send_and_receive_verify(ctx, oracle_lib, corrupt, kind):  # noqa: F811
     """The socket harness around the GPU: enet_hip_udp_stamp_send (GPU stamp,
     protocol.cs:1690-1698, then sendmmsg) and enet_hip_udp_receive_verify (recvmmsg,
-    header stage, pitched H2D, GPU verify, protocol.cs:1052-1068): stamps and keep
-    mask equal to the oracle's, header-stage drops included."""
+    header stage, GPU verify, protocol.cs:1052-1068): stamps and keep mask equal to the
+    oracle's, header-stage drops included.  A pinned arena is verified in place (the
+    kernel reads it over PCIe, every batch reusing the same arena); a pageable one
+    takes the pitched-H2D copy form."""
     sb = workloads.send_batch(3000, seed=70 + corrupt)
     g = sb.gather
     exp_stamp = oracle_stamps(oracle_lib, sb)
     rx, tx, port = sockets()
-    arena, p = pinned(STRIDE * 512)
+    arena, p = pinned(STRIDE * 512) if kind == "pinned" else (np.zeros(STRIDE * 512, np.uint8), None)
     try:
         rng = np.random.default_rng(corrupt)
         recv_rows, recv_lens, oks = [], [], []
@@ -159,7 +161,8 @@ def test_gpu_stamp_send_and_receive_verify(ctx, oracle_lib, corrupt):  # noqa: F
         assert (ok2 == exp).all(), np.nonzero(ok2 != exp)[0][:10]
         assert exp[-5:].sum() == 0
     finally:
-        free_pinned(p)
+        if p is not None:
+            free_pinned(p)
         rx.close()
         tx.close()
 

@@ -15,6 +15,9 @@ drains the socket for SECONDS per mode:
   port     the same with the oracle's byte-serial restatement of packet.cs:142-160
            (the reference's own loop, the CPU baseline);
   recv     enet_hip_udp_receive alone (the socket's own ceiling).
+UDP_BENCH_CALLS=1: instead, the cost of one receive call (gpu, callback) on a socket
+already holding k = 8, 32, 64 DGRAMs (the streaming rates above are bound by the sender
+thread: every mode but port keeps up with it).
 Send side: stamp + send of the whole batch, GPU (enet_hip_udp_stamp_send) against the
 callback stamp (enet_hip_stamp_callback + enet_hip_udp_send), a receiver thread
 draining the socket.  One JSON line per mode; every kept / stamped DGRAM is checked
@@ -194,6 +197,41 @@ def send_mode(mode, ctx, sb, ol):
             "received_by_drain": dr.got}
 
 
+def call_latency(ctx, sb, mode, k, reps=300):
+    """One receive call on a socket already holding k DGRAMs (sent just before, so the
+    socket is not the limit): the per-batch cost of each receive form, recvmmsg
+    included, median and 10th percentile over `reps` calls."""
+    rx, tx, port = sockets()
+    arena, p = pinned(STRIDE * 1024)
+    g = sb.gather
+    ts = []
+    try:
+        for r in range(reps + 10):
+            a = (r * k) % (sb.n - k)
+            sent = enethip.udp_send(tx.fileno(), g.payload, g.seg_off, g.seg_len, g.seg_first[a:a + k + 1],
+                                    LOOPBACK, port)
+            assert sent == k
+            t0 = time.perf_counter()
+            if mode == "gpu":
+                n, lens, ok = ctx.udp_receive_verify(rx.fileno(), arena, STRIDE, k, sb.peers, timeout_ms=100)
+            else:
+                n, lens, _, _ = enethip.udp_receive(rx.fileno(), arena, STRIDE, k, timeout_ms=100)
+                slot, conn, verdict = enethip.parse_headers(arena, STRIDE, lens, sb.peers)
+                ok = enethip.verify_callback(arena, STRIDE, lens, slot, conn, verdict)
+            t1 = time.perf_counter()
+            assert n == k and int(ok.sum()) == k, (mode, k, n, int(ok.sum()))
+            if r >= 10:
+                ts.append(t1 - t0)
+    finally:
+        rx.close()
+        tx.close()
+        free(p)
+    ts = np.array(ts) * 1e6
+    return {"side": "receive-call", "mode": mode, "dgrams_per_call": k, "calls": reps,
+            "median_us": round(float(np.median(ts)), 1), "p10_us": round(float(np.percentile(ts, 10)), 1),
+            "median_GBps": round(k * 1200 / float(np.median(ts)) / 1e3, 3)}
+
+
 def main():
     sb = workloads.send_batch(int(os.environ.get("UDP_BENCH_DGRAMS", "65536")), body=(1188, 1188), seed=9)
     enethip.stamp_callback(sb.gather.payload, sb.gather.seg_off, sb.gather.seg_len, sb.gather.seg_first,
@@ -202,6 +240,12 @@ def main():
     ctx = enethip.Context(0)
     print(json.dumps({"cores": len(os.sched_getaffinity(0)), "dgrams_per_batch": sb.n,
                       "dgram_bytes": sb.gather.dgram_bytes}), flush=True)
+    if os.environ.get("UDP_BENCH_CALLS"):            # per-call costs only
+        for k in (8, 32, 64):
+            for mode in ("gpu", "callback"):
+                print(json.dumps(call_latency(ctx, sb, mode, k)), flush=True)
+        ctx.close()
+        return
     for mode in ("recv", "gpu", "gpu2", "callback", "port"):
         print(json.dumps(receive_mode(mode, ctx, sb, ol)), flush=True)
     sb2 = workloads.send_batch(int(os.environ.get("UDP_BENCH_DGRAMS", "65536")), body=(1188, 1188), seed=10)
