@@ -31,6 +31,11 @@ namespace enethip {
 
 constexpr size_t kChunkBytes = size_t(16) << 20;   // payload per pipeline chunk
 constexpr size_t kChunkMaxPackets = size_t(1) << 18;
+// the largest arena span the gather host entry reads in place (pinned arenas)
+#ifndef ENET_HIP_GATHER_INPLACE_SPAN
+#define ENET_HIP_GATHER_INPLACE_SPAN (size_t(4) << 20)
+#endif
+constexpr size_t kGatherInPlaceSpan = ENET_HIP_GATHER_INPLACE_SPAN;
 
 int pipeline_init(enet_hip_context* ctx) {
     for (int s = 0; s < 2; ++s) {
@@ -212,6 +217,17 @@ int enet_hip_crc32_batch_multi(enet_hip_context* const* contexts, int contextCou
     return 0;
 }
 
+// The device address of pinned host memory (hipHostMalloc'd or registered), or null for
+// pageable memory: the kernels can then read it in place over PCIe.
+static uint8_t* pinned_device_view(void* host) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, host) != hipSuccess) {
+        (void)hipGetLastError();                         // (pageable memory: not an error here)
+        return nullptr;
+    }
+    return a.type == hipMemoryTypeHost ? static_cast<uint8_t*>(a.devicePointer) : nullptr;
+}
+
 int enet_hip_crc32_gather_binned_host(enet_hip_context* ctx, const uint8_t* bytes, size_t byteCount,
                                       const uint64_t* segOffsets, const uint32_t* segLengths, size_t segCount,
                                       const uint32_t* segFirst, size_t dgramCount, uint32_t* out) {
@@ -232,11 +248,12 @@ int enet_hip_crc32_gather_binned_host(enet_hip_context* ctx, const uint8_t* byte
     // aligned start so the device copy keeps the host's alignment mod 16); their
     // offsets are rebased onto it.  A send loop that stamps a long arena in slices
     // then copies each slice's bytes, not the whole arena per call.
-    uint64_t lo = byteCount, hi = 0;
+    uint64_t lo = byteCount, hi = 0, used = 0;
     for (size_t s = s_lo; s < s_hi; ++s)
         if (segLengths[s]) {
             lo = std::min<uint64_t>(lo, segOffsets[s]);
             hi = std::max<uint64_t>(hi, segOffsets[s] + segLengths[s]);
+            used += segLengths[s];
         }
     if (hi <= lo) lo = hi = 0;
     lo &= ~uint64_t(15);
@@ -246,6 +263,44 @@ int enet_hip_crc32_gather_binned_host(enet_hip_context* ctx, const uint8_t* byte
     ENH_CHECK(hipSetDevice(ctx->device));
     int rc;
     if ((rc = pipeline_init(ctx))) return rc;
+    // A pinned arena is read in place over PCIe when that moves fewer bytes or saves the
+    // copies' fixed cost: a span up to kGatherInPlaceSpan, or segments covering under 4/5 of
+    // their span (the kernels read about 38 GB/s of used bytes in place, the copy engines
+    // 46 GB/s of the whole span: profiles/r05_rx_zero_copy/).  The segment tables go to
+    // pinned staging (a host memcpy), the kernels read them there and write the CRCs into
+    // pinned memory -- one stream, no copies (round 5)
+    const bool in_place = span <= kGatherInPlaceSpan || 5u * used < 4u * static_cast<uint64_t>(span);
+    uint8_t* zb = in_place ? pinned_device_view(const_cast<uint8_t*>(bytes)) : nullptr;
+    if (zb) {
+        const size_t sf = align16(4 * (dgramCount + 1)), so = align16(8 * ns + 8), sl = align16(4 * ns + 4);
+        if ((rc = ensure_pinned(&ctx->h_pipe[1], &ctx->h_pipe_cap[1], sf + so + sl))) return rc;
+        if ((rc = ensure_pinned(&ctx->h_out, &ctx->h_out_cap, 4 * dgramCount))) return rc;
+        const size_t wsb = enet_hip_gather_binned_workspace_size(ns);
+        if ((rc = ensure_device(&ctx->d_ws, &ctx->d_ws_cap, wsb + 16))) return rc;
+        uint8_t* zs = pinned_device_view(ctx->h_pipe[1]);
+        uint8_t* zo = pinned_device_view(ctx->h_out);
+        if (zs && zo) {
+            uint32_t* h_sf = reinterpret_cast<uint32_t*>(ctx->h_pipe[1]);
+            uint64_t* h_so = reinterpret_cast<uint64_t*>(ctx->h_pipe[1] + sf);
+            uint32_t* h_sl = reinterpret_cast<uint32_t*>(ctx->h_pipe[1] + sf + so);
+            for (size_t d = 0; d <= dgramCount; ++d) h_sf[d] = static_cast<uint32_t>(segFirst[d] - s_lo);
+            for (size_t s = 0; s < ns; ++s) {
+                h_sl[s] = segLengths[s_lo + s];
+                h_so[s] = h_sl[s] ? segOffsets[s_lo + s] : 0u;
+            }
+            hipStream_t s0 = ctx->pipe[0];
+            if ((rc = enet_hip_crc32_gather_binned_device(
+                     ctx, zb, ns ? reinterpret_cast<uint64_t*>(zs + sf) : nullptr,
+                     ns ? reinterpret_cast<uint32_t*>(zs + sf + so) : nullptr, ns, reinterpret_cast<uint32_t*>(zs),
+                     dgramCount, reinterpret_cast<uint32_t*>(zo), ctx->d_ws, ctx->d_ws_cap, s0))) {
+                (void)hipStreamSynchronize(s0);
+                return rc;
+            }
+            ENH_CHECK(hipStreamSynchronize(s0));
+            memcpy(out, ctx->h_out, 4 * dgramCount);
+            return 0;
+        }
+    }
     // device: [arena span | segOffsets | segLengths | segFirst | out], then the binned workspace
     const size_t a = align16(span + 16), so = align16(8 * ns + 8), sl = align16(4 * ns + 4);
     const size_t sf = align16(4 * (dgramCount + 1)), ob = align16(4 * dgramCount);
@@ -283,17 +338,6 @@ int enet_hip_crc32_gather_binned_host(enet_hip_context* ctx, const uint8_t* byte
     ENH_CHECK(hipStreamSynchronize(s0));
     memcpy(out, ctx->h_out, 4 * dgramCount);
     return 0;
-}
-
-// The device address of pinned host memory (hipHostMalloc'd or registered), or null for
-// pageable memory: the kernels can then read it in place over PCIe.
-static uint8_t* pinned_device_view(void* host) {
-    hipPointerAttribute_t a{};
-    if (hipPointerGetAttributes(&a, host) != hipSuccess) {
-        (void)hipGetLastError();                         // (pageable memory: not an error here)
-        return nullptr;
-    }
-    return a.type == hipMemoryTypeHost ? static_cast<uint8_t*>(a.devicePointer) : nullptr;
 }
 
 // The receive batch of slot s (0 or 1): receive, header stage, GPU verify and the keep

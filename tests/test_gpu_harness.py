@@ -107,6 +107,34 @@ def test_gather_binned_host_full_cfg5(ctx, oracle_lib):  # noqa: F811
     assert (ctx.gather_binned_host(payload, offs, lens, sl) == exp[100:300]).all()
 
 
+def test_gather_binned_host_in_place(ctx, oracle_lib):  # noqa: F811
+    """A pinned arena whose used span is at most 4 MiB is read in place over PCIe (no
+    copies): random gather lists (0-65 buffers, empty buffers and DGRAMs,
+    segments ending at the arena's last byte), slices of the list, and the same arena
+    rewritten between calls -- against the oracle's gather."""
+    rng = np.random.default_rng(68)
+    n = (1 << 20) + 5                                        # (not a multiple of 16)
+    arr, p = pinned(n)
+    try:
+        for rep in range(3):
+            arr[:] = rng.integers(0, 256, size=n, dtype=np.uint8)
+            cnt = rng.integers(0, 66, size=400)
+            sf = np.zeros(401, np.uint32)
+            np.cumsum(cnt, out=sf[1:])
+            ns = int(sf[-1])
+            lens = np.where(rng.integers(0, 6, size=ns) == 0, 0, rng.integers(1, 1400, size=ns)).astype(np.uint32)
+            offs = rng.integers(0, n - 1400, size=ns).astype(np.uint64)
+            tail = rng.choice(ns, 5, replace=False)              # segments that end on the last byte
+            offs[tail] = n - lens[tail]
+            exp = oracle_lib.gather(arr, offs, lens, sf)
+            got = ctx.gather_binned_host(arr, offs, lens, sf)
+            assert (got == exp).all(), (rep, np.nonzero(got != exp)[0][:10])
+            sl = sf[50 * rep:50 * rep + 201]
+            assert (ctx.gather_binned_host(arr, offs, lens, sl) == exp[50 * rep:50 * rep + 200]).all()
+    finally:
+        free_pinned(p)
+
+
 @pytest.mark.parametrize("corrupt,kind", [(0, "pinned"), (61, "pinned"), (61, "pageable")])
 def test_gpu_stamp_send_and_receive_verify(ctx, oracle_lib, corrupt, kind):  # noqa: F811
     """The socket harness around the GPU: enet_hip_udp_stamp_send (GPU stamp,

@@ -127,9 +127,41 @@ def case_cfg5(ctx, reps):
             "arena_GBps": round(g.payload.nbytes / dt / 1e9, 2)}
 
 
+def case_cfg5_slices(ctx, reps):
+    """The first k DGRAMs of cfg5 (used arena span about 1.4 KB per DGRAM), pinned: the
+    span sizes around the in-place threshold of the gather host entry."""
+    lib = ctx.lib
+    g = workloads.cfg5()
+    hp = Pinned(lib, g.payload)
+    ho, hl, hf = Pinned(lib, g.seg_off), Pinned(lib, g.seg_len), Pinned(lib, g.seg_first)
+    out = Pinned(lib, np.zeros(g.n, np.uint32))
+    exp = oracle.OracleLib().gather(g.payload, g.seg_off, g.seg_len, g.seg_first)
+    rows = []
+    for k in (64, 768, 3072, 12288, 49152, g.n):
+        call = lambda: lib.enet_hip_crc32_gather_binned_host(  # noqa: E731
+            ctx.handle, hp.ptr, g.payload.nbytes, ho.ptr, hl.ptr, len(g.seg_off), hf.ptr, k, out.ptr)
+        assert call() == 0
+        assert (out.arr[:k] == exp[:k]).all(), f"cfg5 slice {k} differs from the oracle"
+        s0, s1 = int(g.seg_first[0]), int(g.seg_first[k])
+        used = g.seg_len[s0:s1] > 0
+        span = int((g.seg_off[s0:s1][used] + g.seg_len[s0:s1][used]).max() - g.seg_off[s0:s1][used].min())
+        dt = timed(call, reps if k < g.n else max(3, reps // 4))
+        rows.append({"case": "cfg5 slice, enet_hip_crc32_gather_binned_host, pinned", "dgrams": k,
+                     "span_bytes": span, "us_per_call": round(dt * 1e6, 1),
+                     "span_GBps": round(span / dt / 1e9, 2)})
+    for x in (hp, ho, hl, hf, out):
+        x.free()
+    return rows
+
+
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
     ctx = enethip.Context(0)
+    if os.environ.get("PCIE_BENCH_SLICES"):
+        for r in case_cfg5_slices(ctx, reps):
+            print(json.dumps(r), flush=True)
+        ctx.close()
+        return
     for case in (case_pcie, case_cfg2, case_cfg5):
         print(json.dumps(case(ctx, reps)), flush=True)
     ctx.close()

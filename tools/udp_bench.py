@@ -17,7 +17,8 @@ drains the socket for SECONDS per mode:
   recv     enet_hip_udp_receive alone (the socket's own ceiling).
 UDP_BENCH_CALLS=1: instead, the cost of one receive call (gpu, callback) on a socket
 already holding k = 8, 32, 64 DGRAMs (the streaming rates above are bound by the sender
-thread: every mode but port keeps up with it).
+thread: every mode but port keeps up with it).  UDP_BENCH_SEND_CALLS=1: the cost of one
+stamp + send call (gpu, callback) over k = 8 ... 65536 DGRAMs of a pinned send batch.
 Send side: stamp + send of the whole batch, GPU (enet_hip_udp_stamp_send) against the
 callback stamp (enet_hip_stamp_callback + enet_hip_udp_send), a receiver thread
 draining the socket.  One JSON line per mode; every kept / stamped DGRAM is checked
@@ -232,6 +233,49 @@ def call_latency(ctx, sb, mode, k, reps=300):
             "median_GBps": round(k * 1200 / float(np.median(ts)) / 1e3, 3)}
 
 
+def send_call_latency(ctx, sb, mode, k, reps):
+    """One stamp + send call over the first k DGRAMs of a pinned send batch: the GPU
+    stamp (enet_hip_udp_stamp_send) or the CPU callback stamp + enet_hip_udp_send;
+    median and 10th percentile over `reps` calls (the slots restored between calls,
+    outside the timing), a receiver thread draining the socket."""
+    rx, tx, port = sockets()
+    dr = Drain(rx)
+    dr.start()
+    g = sb.gather
+    base = g.payload.copy()
+    arena, p = pinned(len(base))
+    arena[:] = base
+    sf = g.seg_first[:k + 1]
+    pos = (g.seg_off[g.seg_first[:k]] + sb.slot_off[:k]).astype(np.int64)
+    ts = []
+    try:
+        for r in range(reps + 3):
+            arena[pos[:, None] + np.arange(4)] = base[pos[:, None] + np.arange(4)]
+            t0 = time.perf_counter()
+            if mode == "gpu":
+                sent = ctx.udp_stamp_send(tx.fileno(), arena, g.seg_off, g.seg_len, sf, sb.slot_off[:k], LOOPBACK, port)
+            else:
+                enethip.stamp_callback(arena, g.seg_off, g.seg_len, sf, sb.slot_off[:k])
+                sent = enethip.udp_send(tx.fileno(), arena, g.seg_off, g.seg_len, sf, LOOPBACK, port)
+            t1 = time.perf_counter()
+            assert sent == k
+            if r >= 3:
+                ts.append(t1 - t0)
+        got = arena[pos[:, None] + np.arange(4)].copy()
+        ref = base.copy()
+        enethip.stamp_callback(ref, g.seg_off, g.seg_len, sf, sb.slot_off[:k])
+        assert (got == ref[pos[:, None] + np.arange(4)]).all(), f"{mode} stamp differs"
+    finally:
+        dr.stop = True
+        dr.join()
+        rx.close()
+        tx.close()
+        free(p)
+    ts = np.array(ts) * 1e6
+    return {"side": "send-call", "mode": mode, "dgrams_per_call": k, "calls": reps,
+            "median_us": round(float(np.median(ts)), 1), "p10_us": round(float(np.percentile(ts, 10)), 1)}
+
+
 def main():
     sb = workloads.send_batch(int(os.environ.get("UDP_BENCH_DGRAMS", "65536")), body=(1188, 1188), seed=9)
     enethip.stamp_callback(sb.gather.payload, sb.gather.seg_off, sb.gather.seg_len, sb.gather.seg_first,
@@ -240,6 +284,13 @@ def main():
     ctx = enethip.Context(0)
     print(json.dumps({"cores": len(os.sched_getaffinity(0)), "dgrams_per_batch": sb.n,
                       "dgram_bytes": sb.gather.dgram_bytes}), flush=True)
+    if os.environ.get("UDP_BENCH_SEND_CALLS"):       # per-call send costs only
+        sb2 = workloads.send_batch(int(os.environ.get("UDP_BENCH_DGRAMS", "65536")), body=(1188, 1188), seed=10)
+        for k, reps in ((8, 300), (64, 300), (512, 100), (4096, 30), (65536, 10)):
+            for mode in ("gpu", "callback"):
+                print(json.dumps(send_call_latency(ctx, sb2, mode, min(k, sb2.n), reps)), flush=True)
+        ctx.close()
+        return
     if os.environ.get("UDP_BENCH_CALLS"):            # per-call costs only
         for k in (8, 32, 64):
             for mode in ("gpu", "callback"):
