@@ -131,18 +131,64 @@ using namespace enethip;
 
 extern "C" {
 
+// The device address of pinned host memory (hipHostMalloc'd or registered), or null for
+// pageable memory: the kernels can then read it in place over PCIe.
+static uint8_t* pinned_device_view(void* host) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, host) != hipSuccess) {
+        (void)hipGetLastError();                         // (pageable memory: not an error here)
+        return nullptr;
+    }
+    return a.type == hipMemoryTypeHost ? static_cast<uint8_t*>(a.devicePointer) : nullptr;
+}
+
 int enet_hip_crc32_batch_host(enet_hip_context* ctx, const uint8_t* bytes, size_t byteCount,
                               const uint64_t* offsets, const uint32_t* lengths, size_t count, uint32_t* out) {
     if (!ctx) return -static_cast<int>(hipErrorInvalidValue);
     if (count == 0) return 0;
     if (!bytes || !offsets || !lengths || !out) return -static_cast<int>(hipErrorInvalidValue);
-    for (size_t i = 0; i < count; ++i)  // host-side shape check before any launch
+    uint64_t lo = byteCount, hi = 0, used = 0;
+    for (size_t i = 0; i < count; ++i) {  // host-side shape check before any launch
         if (offsets[i] > byteCount || lengths[i] > byteCount - offsets[i]) return -static_cast<int>(hipErrorInvalidValue);
+        if (lengths[i]) {
+            lo = std::min<uint64_t>(lo, offsets[i]);
+            hi = std::max<uint64_t>(hi, offsets[i] + lengths[i]);
+            used += lengths[i];
+        }
+    }
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (ctx->rx_pending[0] || ctx->rx_pending[1]) return -static_cast<int>(hipErrorInvalidValue);   // (async receive slots hold the staging)
     ENH_CHECK(hipSetDevice(ctx->device));
     int rc;
     if ((rc = pipeline_init(ctx))) return rc;
+    // a pinned arena, small or sparsely used: the kernel reads it in place (the gather
+    // host entry's rule and measurements); offsets and lengths through
+    // pinned staging, the CRCs into pinned memory
+    const uint64_t span = hi > lo ? hi - lo : 0;
+    if (span <= kGatherInPlaceSpan || 5u * used < 4u * span) {
+        uint8_t* zb = pinned_device_view(const_cast<uint8_t*>(bytes));
+        const size_t ho = align16(8 * count);
+        if (zb) {
+            if ((rc = ensure_pinned(&ctx->h_pipe[0], &ctx->h_pipe_cap[0], ho + 4 * count))) return rc;
+            if ((rc = ensure_pinned(&ctx->h_out, &ctx->h_out_cap, 4 * count))) return rc;
+        }
+        uint8_t* zs = zb ? pinned_device_view(ctx->h_pipe[0]) : nullptr;
+        uint8_t* zo = zb ? pinned_device_view(ctx->h_out) : nullptr;
+        if (zb && zs && zo) {
+            memcpy(ctx->h_pipe[0], offsets, 8 * count);
+            memcpy(ctx->h_pipe[0] + ho, lengths, 4 * count);
+            hipStream_t st = ctx->pipe[0];
+            if ((rc = enet_hip_crc32_batch_device(ctx, zb, reinterpret_cast<uint64_t*>(zs),
+                                                  reinterpret_cast<uint32_t*>(zs + ho), count,
+                                                  reinterpret_cast<uint32_t*>(zo), st))) {
+                (void)hipStreamSynchronize(st);
+                return rc;
+            }
+            ENH_CHECK(hipStreamSynchronize(st));
+            memcpy(out, ctx->h_out, 4 * count);
+            return 0;
+        }
+    }
     const std::vector<Chunk> plan = plan_chunks(offsets, lengths, count, byteCount);
     size_t span_max = 0, pk_max = 0;
     for (const Chunk& c : plan) {
@@ -215,17 +261,6 @@ int enet_hip_crc32_batch_multi(enet_hip_context* const* contexts, int contextCou
     for (int rc : rcs)
         if (rc) return rc;
     return 0;
-}
-
-// The device address of pinned host memory (hipHostMalloc'd or registered), or null for
-// pageable memory: the kernels can then read it in place over PCIe.
-static uint8_t* pinned_device_view(void* host) {
-    hipPointerAttribute_t a{};
-    if (hipPointerGetAttributes(&a, host) != hipSuccess) {
-        (void)hipGetLastError();                         // (pageable memory: not an error here)
-        return nullptr;
-    }
-    return a.type == hipMemoryTypeHost ? static_cast<uint8_t*>(a.devicePointer) : nullptr;
 }
 
 int enet_hip_crc32_gather_binned_host(enet_hip_context* ctx, const uint8_t* bytes, size_t byteCount,

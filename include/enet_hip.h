@@ -152,7 +152,9 @@ ENET_HIP_API int enet_hip_crc32_batch_device_binned(enet_hip_context* ctx, const
  * on two streams -- H2D of a chunk's byte span and metadata, the checksum kernel,
  * D2H of its CRCs -- so one chunk's copy overlaps the previous chunk's kernel.
  * Host buffers allocated with enet_hip_host_alloc are pinned and give the full
- * PCIe rate. */
+ * PCIe rate.  A pinned `bytes` whose packets span at most 4 MiB, or cover under 4/5 of
+ * their span, is read in place by the kernel over PCIe instead (no copies of the
+ * bytes; 21-22 against 29-31 us for 8 packets). */
 ENET_HIP_API int enet_hip_crc32_batch_host(enet_hip_context* ctx, const uint8_t* bytes, size_t byteCount,
                                            const uint64_t* offsets, const uint32_t* lengths,
                                            size_t count, uint32_t* out);
@@ -279,7 +281,9 @@ ENET_HIP_API int enet_hip_range_decompress_device(enet_hip_context* ctx, const u
  * the binned gather CRC runs on the GPU, out[] is copied back.  The DGRAMs use
  * segments segFirst[0] .. segFirst[dgramCount]-1 of the segCount given (a send
  * batch may be a slice of a longer list; checked).  Synchronous; pinned host
- * memory (enet_hip_host_alloc) gives the full PCIe rate. */
+ * memory (enet_hip_host_alloc) gives the full PCIe rate.  A pinned arena whose used
+ * segments span at most 4 MiB, or cover under 4/5 of their span, is read in place by
+ * the kernels over PCIe instead (no copies of the arena). */
 ENET_HIP_API int enet_hip_crc32_gather_binned_host(enet_hip_context* ctx, const uint8_t* bytes, size_t byteCount,
                                                    const uint64_t* segOffsets, const uint32_t* segLengths,
                                                    size_t segCount, const uint32_t* segFirst, size_t dgramCount,

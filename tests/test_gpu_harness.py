@@ -44,6 +44,31 @@ def test_batch_host_cfg2_pipelined(ctx, oracle_lib):  # noqa: F811
         free_pinned(p)
 
 
+def test_batch_host_in_place(ctx, oracle_lib):  # noqa: F811
+    """A pinned arena whose packets span at most 4 MiB, or cover under 4/5 of their span,
+    is read in place over PCIe: packets at any alignment, overlapping,
+    empty, ending on the arena's last byte; a sparse list over a 24-MiB span; the arena
+    rewritten between calls -- against the oracle."""
+    rng = np.random.default_rng(69)
+    n = (24 << 20) + 7
+    arr, p = pinned(n)
+    try:
+        for rep in range(2):
+            arr[:] = rng.integers(0, 256, size=n, dtype=np.uint8)
+            k = 3000
+            lens = np.where(rng.integers(0, 8, size=k) == 0, 0, rng.integers(1, 1500, size=k)).astype(np.uint32)
+            off = rng.integers(0, (3 << 20), size=k).astype(np.uint64)       # dense: a 3-MiB span
+            off[:3] = n - lens[:3]                                        # (and three at the very end)
+            exp = oracle_lib.batch(arr, off, lens)
+            assert (ctx.crc32_batch_host(arr, off, lens) == exp).all(), rep
+            off2 = rng.integers(0, n - 1500, size=k).astype(np.uint64)    # sparse over 24 MiB
+            exp2 = oracle_lib.batch(arr, off2, lens)
+            assert (ctx.crc32_batch_host(arr, off2, lens) == exp2).all(), rep
+            assert (ctx.crc32_batch_host(arr, off2[5:6], lens[5:6]) == exp2[5:6]).all()
+    finally:
+        free_pinned(p)
+
+
 def test_batch_host_chunks_and_orders(ctx, oracle_lib):  # noqa: F811
     """Many chunks (300 K mixed packets, pageable memory), packets in arbitrary order
     (the one-span fallback), a single packet and empty packets."""

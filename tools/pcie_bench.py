@@ -154,11 +154,33 @@ def case_cfg5_slices(ctx, reps):
     return rows
 
 
+def case_cfg2_slices(ctx, reps):
+    """The first k packets of cfg2 (1200 B each, contiguous), pinned, through
+    enet_hip_crc32_batch_host: in place up to a 4-MiB span, copied beyond."""
+    lib = ctx.lib
+    b = workloads.cfg2()
+    hp, ho, hl = Pinned(lib, b.payload), Pinned(lib, b.off), Pinned(lib, b.lens)
+    out = Pinned(lib, np.zeros(b.n, np.uint32))
+    exp = oracle.OracleLib().batch(b.payload, b.off, b.lens, threads=8)
+    rows = []
+    for k in (8, 64, 512, 3495, 3496, 16384, b.n):
+        call = lambda: lib.enet_hip_crc32_batch_host(ctx.handle, hp.ptr, b.payload.nbytes, ho.ptr, hl.ptr,  # noqa: E731
+                                                     k, out.ptr)
+        assert call() == 0
+        assert (out.arr[:k] == exp[:k]).all(), f"cfg2 slice {k} differs from the oracle"
+        dt = timed(call, reps if k < 16384 else max(3, reps // 4))
+        rows.append({"case": "cfg2 slice, enet_hip_crc32_batch_host, pinned", "packets": k, "span_bytes": 1200 * k,
+                     "us_per_call": round(dt * 1e6, 1), "GBps": round(1200 * k / dt / 1e9, 2)})
+    for x in (hp, ho, hl, out):
+        x.free()
+    return rows
+
+
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
     ctx = enethip.Context(0)
     if os.environ.get("PCIE_BENCH_SLICES"):
-        for r in case_cfg5_slices(ctx, reps):
+        for r in case_cfg2_slices(ctx, reps) + case_cfg5_slices(ctx, reps):
             print(json.dumps(r), flush=True)
         ctx.close()
         return
