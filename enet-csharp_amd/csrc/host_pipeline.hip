@@ -131,15 +131,17 @@ using namespace enethip;
 
 extern "C" {
 
-// The device address of pinned host memory (hipHostMalloc'd or registered), or null for
-// pageable memory: the kernels can then read it in place over PCIe.
-static uint8_t* pinned_device_view(void* host) {
+// The device address of pinned host memory (hipHostMalloc'd or registered) that was
+// allocated under `device`, or null -- pageable memory, or pinned memory of another
+// device's context, which that device's page tables may not map: the kernels of `device`
+// can then read the memory in place over PCIe.
+static uint8_t* pinned_device_view(void* host, int device) {
     hipPointerAttribute_t a{};
     if (hipPointerGetAttributes(&a, host) != hipSuccess) {
         (void)hipGetLastError();                         // (pageable memory: not an error here)
         return nullptr;
     }
-    return a.type == hipMemoryTypeHost ? static_cast<uint8_t*>(a.devicePointer) : nullptr;
+    return a.type == hipMemoryTypeHost && a.device == device ? static_cast<uint8_t*>(a.devicePointer) : nullptr;
 }
 
 int enet_hip_crc32_batch_host(enet_hip_context* ctx, const uint8_t* bytes, size_t byteCount,
@@ -166,14 +168,14 @@ int enet_hip_crc32_batch_host(enet_hip_context* ctx, const uint8_t* bytes, size_
     // pinned staging, the CRCs into pinned memory
     const uint64_t span = hi > lo ? hi - lo : 0;
     if (span <= kGatherInPlaceSpan || 5u * used < 4u * span) {
-        uint8_t* zb = pinned_device_view(const_cast<uint8_t*>(bytes));
+        uint8_t* zb = pinned_device_view(const_cast<uint8_t*>(bytes), ctx->device);
         const size_t ho = align16(8 * count);
         if (zb) {
             if ((rc = ensure_pinned(&ctx->h_pipe[0], &ctx->h_pipe_cap[0], ho + 4 * count))) return rc;
             if ((rc = ensure_pinned(&ctx->h_out, &ctx->h_out_cap, 4 * count))) return rc;
         }
-        uint8_t* zs = zb ? pinned_device_view(ctx->h_pipe[0]) : nullptr;
-        uint8_t* zo = zb ? pinned_device_view(ctx->h_out) : nullptr;
+        uint8_t* zs = zb ? pinned_device_view(ctx->h_pipe[0], ctx->device) : nullptr;
+        uint8_t* zo = zb ? pinned_device_view(ctx->h_out, ctx->device) : nullptr;
         if (zb && zs && zo) {
             memcpy(ctx->h_pipe[0], offsets, 8 * count);
             memcpy(ctx->h_pipe[0] + ho, lengths, 4 * count);
@@ -305,15 +307,15 @@ int enet_hip_crc32_gather_binned_host(enet_hip_context* ctx, const uint8_t* byte
     // pinned staging (a host memcpy), the kernels read them there and write the CRCs into
     // pinned memory -- one stream, no copies (round 5)
     const bool in_place = span <= kGatherInPlaceSpan || 5u * used < 4u * static_cast<uint64_t>(span);
-    uint8_t* zb = in_place ? pinned_device_view(const_cast<uint8_t*>(bytes)) : nullptr;
+    uint8_t* zb = in_place ? pinned_device_view(const_cast<uint8_t*>(bytes), ctx->device) : nullptr;
     if (zb) {
         const size_t sf = align16(4 * (dgramCount + 1)), so = align16(8 * ns + 8), sl = align16(4 * ns + 4);
         if ((rc = ensure_pinned(&ctx->h_pipe[1], &ctx->h_pipe_cap[1], sf + so + sl))) return rc;
         if ((rc = ensure_pinned(&ctx->h_out, &ctx->h_out_cap, 4 * dgramCount))) return rc;
         const size_t wsb = enet_hip_gather_binned_workspace_size(ns);
         if ((rc = ensure_device(&ctx->d_ws, &ctx->d_ws_cap, wsb + 16))) return rc;
-        uint8_t* zs = pinned_device_view(ctx->h_pipe[1]);
-        uint8_t* zo = pinned_device_view(ctx->h_out);
+        uint8_t* zs = pinned_device_view(ctx->h_pipe[1], ctx->device);
+        uint8_t* zo = pinned_device_view(ctx->h_out, ctx->device);
         if (zs && zo) {
             uint32_t* h_sf = reinterpret_cast<uint32_t*>(ctx->h_pipe[1]);
             uint64_t* h_so = reinterpret_cast<uint64_t*>(ctx->h_pipe[1] + sf);
@@ -407,8 +409,8 @@ static int rx_submit(enet_hip_context* ctx, int slot, int fd, uint8_t* arena, si
     if ((rc = enet_hip_parse_headers(arena, stride, lengths, n, peerConnectIds, peerCount, h_slot, h_conn, h_verdict)))
         return rc;
     hipStream_t st = ctx->pipe[slot];
-    uint8_t* zc = pinned_device_view(arena);
-    uint8_t* zs = zc ? pinned_device_view(ctx->h_pipe[slot]) : nullptr;
+    uint8_t* zc = pinned_device_view(arena, ctx->device);
+    uint8_t* zs = zc ? pinned_device_view(ctx->h_pipe[slot], ctx->device) : nullptr;
     if (zc && zs) {
         for (size_t i = 0; i < n; ++i) {
             h_off[i] = i * stride;
