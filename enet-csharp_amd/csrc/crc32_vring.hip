@@ -1168,7 +1168,17 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
         else cstages = pstages;
         const uint32_t init = lds_load(init_addr(clz));
         reg = lane_k() == 0u ? (nb ? init : 0xFFFFFFFFu) : 0u;      // packet.cs:144 (empty packet: ~crc = 0)
-        {
+        // a group whose packets all start and end on 16-byte boundaries has no partly
+        // covered piece: one ballot instead of the per-lane search and its wave reduction
+        // (cfg2: VALU -4.2 %, profiles/r05_edge_ballot/).  Not in receive verify, whose
+        // every packet holds a slot, nor in the records instance, whose length-binned
+        // packets of mixed lengths (cfg3) rarely are aligned at both ends (there the
+        // ballot only adds work: cfg3 binned -0.7 %)
+        constexpr bool kEdgeBallot = !VF && BIN != 1;
+        const bool may_edge = ce != clz && ((clz | ce) & 15u) != 0u;
+        if (kEdgeBallot && __builtin_amdgcn_ballot_w64(may_edge) == 0u) {
+            emask = 0u;
+        } else {
             const uint32_t e = next_edge_lane_bits();
             emask = wave_or_u(e);
         }
