@@ -292,6 +292,8 @@ def main():
         ctx.close()
         return
     if os.environ.get("UDP_BENCH_CALLS"):            # per-call costs only
+        if os.environ.get("UDP_BENCH_PATH"):          # (a kernel path for the GPU verify: 13 = lean)
+            ctx.set_kernel_path(int(os.environ["UDP_BENCH_PATH"]))
         for k in (8, 32, 64):
             for mode in ("gpu", "callback"):
                 print(json.dumps(call_latency(ctx, sb, mode, k)), flush=True)
