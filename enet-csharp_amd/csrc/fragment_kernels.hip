@@ -211,11 +211,29 @@ __global__ void __launch_bounds__(256) frag_decide_slots_kernel(FragArgs a) {
     }
 }
 
+// unaligned 16-byte access (gfx950 unaligned mode); (A/B build ENET_HIP_FRAG_NT: both
+// streamed with the nontemporal policy)
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+__device__ __forceinline__ u32x4v load16(const uint8_t* p) {
+#ifdef ENET_HIP_FRAG_NT
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x4u*>(p));
+#else
+    u32x4v v;
+    __builtin_memcpy(&v, p, 16);
+    return v;
+#endif
+}
+__device__ __forceinline__ void store16(uint8_t* p, u32x4v v) {
+#ifdef ENET_HIP_FRAG_NT
+    __builtin_nontemporal_store(static_cast<u32x4u>(v), reinterpret_cast<u32x4u*>(p));
+#else
+    __builtin_memcpy(p, &v, 16);
+#endif
+}
+
 __device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint32_t L, uint32_t x) {
     if (x + 16u <= L) {
-        u32x4v v;
-        __builtin_memcpy(&v, src + x, 16);                // unaligned 16-byte access (gfx950 unaligned mode)
-        __builtin_memcpy(dst + x, &v, 16);
+        store16(dst + x, load16(src + x));
     } else {
         for (uint32_t b = x; b < L; ++b) dst[b] = src[b];
     }
@@ -290,11 +308,11 @@ __global__ void __launch_bounds__(256) frag_copy_kernel(FragArgs a) {
             chunk(two ? k + 64u : k, L1, s1, d1, x1);
             const bool f0 = x0 + 16u <= L0, f1 = two && x1 + 16u <= L1;
             u32x4v v0 = {0u, 0u, 0u, 0u}, v1 = {0u, 0u, 0u, 0u};
-            if (f0) __builtin_memcpy(&v0, a.bytes + s0 + x0, 16);
-            if (f1) __builtin_memcpy(&v1, a.bytes + s1 + x1, 16);
-            if (f0) __builtin_memcpy(a.msg_bytes + d0 + x0, &v0, 16);
+            if (f0) v0 = load16(a.bytes + s0 + x0);
+            if (f1) v1 = load16(a.bytes + s1 + x1);
+            if (f0) store16(a.msg_bytes + d0 + x0, v0);
             else copy_span(a.bytes + s0, a.msg_bytes + d0, L0, x0);
-            if (f1) __builtin_memcpy(a.msg_bytes + d1 + x1, &v1, 16);
+            if (f1) store16(a.msg_bytes + d1 + x1, v1);
             else if (two) copy_span(a.bytes + s1, a.msg_bytes + d1, L1, x1);
         }
     }
