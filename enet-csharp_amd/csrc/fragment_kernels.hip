@@ -211,24 +211,16 @@ __global__ void __launch_bounds__(256) frag_decide_slots_kernel(FragArgs a) {
     }
 }
 
-// unaligned 16-byte access (gfx950 unaligned mode); (A/B build ENET_HIP_FRAG_NT: both
-// streamed with the nontemporal policy)
+// Unaligned 16-byte access (gfx950 unaligned mode), both ways with the nontemporal
+// policy: every fragment byte is read once and written once, so neither side is worth
+// keeping in L2 (cfg5 151.1 against 159.7 us with the default policy,
+// profiles/r05_frag_nt/)
 typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
 __device__ __forceinline__ u32x4v load16(const uint8_t* p) {
-#ifdef ENET_HIP_FRAG_NT
     return __builtin_nontemporal_load(reinterpret_cast<const u32x4u*>(p));
-#else
-    u32x4v v;
-    __builtin_memcpy(&v, p, 16);
-    return v;
-#endif
 }
 __device__ __forceinline__ void store16(uint8_t* p, u32x4v v) {
-#ifdef ENET_HIP_FRAG_NT
     __builtin_nontemporal_store(static_cast<u32x4u>(v), reinterpret_cast<u32x4u*>(p));
-#else
-    __builtin_memcpy(p, &v, 16);
-#endif
 }
 
 __device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint32_t L, uint32_t x) {
