@@ -321,20 +321,22 @@ __device__ __forceinline__ uint32_t vr_tz7_mul(uint32_t reg, uint32_t c) {
 template <bool SMALL = false>
 __device__ __forceinline__ uint32_t vr_unstep_tz(uint32_t reg, uint32_t tz, uint32_t tzbase) {
     if (tz & 16u) reg = vr_tz_mul<0>(reg, tzbase);
-    if (tz & 8u) reg = vr_tz_mul<1>(reg, tzbase);
-    if constexpr (SMALL) {
-        if (tz & 7u) reg = vr_tz7_mul(reg, tz & 7u);
-        return reg;
-    }
-    if (tz & 4u) {
+    if (tz & 15u) {                                          // (one test for the smaller steps: cfg2's tz is 0 or 16)
+        if (tz & 8u) reg = vr_tz_mul<1>(reg, tzbase);
+        if constexpr (SMALL) {
+            if (tz & 7u) reg = vr_tz7_mul(reg, tz & 7u);
+        } else {
+            if (tz & 4u) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) reg = unstep_byte(reg);
+                for (int j = 0; j < 4; ++j) reg = unstep_byte(reg);
+            }
+            if (tz & 2u) {
+                reg = unstep_byte(reg);
+                reg = unstep_byte(reg);
+            }
+            if (tz & 1u) reg = unstep_byte(reg);
+        }
     }
-    if (tz & 2u) {
-        reg = unstep_byte(reg);
-        reg = unstep_byte(reg);
-    }
-    if (tz & 1u) reg = unstep_byte(reg);
     return reg;
 }
 
@@ -1253,13 +1255,15 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
             // (lane-uniform byte order: per-lane rotations hoisted out of the loop cost
             // ten VGPRs; four lookups per packet can afford the bank conflicts)
             const uint32_t kk = o ? o : 1u;
+            // the four columns free_col(4 (kk - 1) + b) = 32 (kk - 1) + 8 b (+ 4 for kk <= 4),
+            // one per byte of `cols`: each lookup's perm takes its column byte from there
+            static_assert(kCorrCol == 0u, "column bytes below assume the correction columns start at 0");
+            const uint32_t cols = (32u * (kk - 1u) + (kk <= 4u ? 4u : 0u)) * 0x01010101u + 0x18100800u;
             uint32_t x[4];
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
-                const uint32_t c = kCorrCol + 4u * (kk - 1u) + static_cast<uint32_t>(b);
-                const uint32_t col = 4u * (c < 16u ? 2u * c + 1u : 2u * c);     // free_col(c)
-                const uint32_t sel = 0x0C0C0000u | ((4u + b) << 8);          // byte1 = byte b of reg, byte0 = column
-                x[b] = lds_load(__builtin_amdgcn_perm(reg, col, sel));
+                const uint32_t sel = 0x0C0C0000u | ((4u + b) << 8) | static_cast<uint32_t>(b);   // byte1 = byte b of reg, byte0 = column b
+                x[b] = lds_load(__builtin_amdgcn_perm(reg, cols, sel));
             }
             const uint32_t corr = xor3(x[0], x[1], x[2]) ^ x[3];
             if constexpr (!(ABL & 16)) reg = o ? corr : reg;
