@@ -11,11 +11,14 @@
 //     1690-1698) from host memory: arena and segment metadata H2D, the binned gather
 //     CRC on the GPU, D2H.
 //   * enet_hip_udp_receive_verify / enet_hip_udp_stamp_send: the socket harness of
-//     host_io.cpp around the GPU -- recvmmsg into a pinned arena, ENet's header stage,
-//     one pitched H2D (only each DGRAM slot's first maxLen bytes cross PCIe), receive
-//     verify (c/protocol.cs:1052-1068) and D2H of the keep mask; and the GPU stamp
+//     host_io.cpp around the GPU -- recvmmsg into the arena, ENet's header stage,
+//     receive verify (c/protocol.cs:1052-1068) in place on a pinned arena (or behind
+//     one pitched H2D and a D2H of the keep mask for a pageable one); and the GPU stamp
 //     (c/protocol.cs:1690-1698) of a send batch followed by sendmmsg.
-// Calls on one context serialize on its mutex; every call is synchronous.
+//   * Pinned arenas of the context's device that are small or sparsely used are read in
+//     place over PCIe by the batch and gather host entries too: no copies.
+// Calls on one context serialize on its mutex; every call is synchronous except the
+// two-slot receive's submit / complete halves.
 #include <hip/hip_runtime.h>
 #include <errno.h>
 #include <string.h>
