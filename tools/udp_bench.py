@@ -71,6 +71,13 @@ def sockets():
     return rx, tx, rx.getsockname()[1]
 
 
+def sockets_tx():
+    tx = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    tx.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 64 << 20)
+    tx.bind(("127.0.0.1", 0))
+    return tx
+
+
 class Sender(threading.Thread):
     def __init__(self, tx, port, sb):
         super().__init__(daemon=True)
@@ -93,12 +100,20 @@ def port_verify(ol, arena, lens, slot, conn, verdict):
     return ok
 
 
+SENDERS = int(os.environ.get("UDP_BENCH_SENDERS", "1"))
+
+
 def receive_mode(mode, ctx, sb, ol):
     rx, tx, port = sockets()
     arena, p = pinned(STRIDE * 8192)
     arena2, p2 = pinned(STRIDE * 8192) if mode == "gpu2" else (None, None)
-    snd = Sender(tx, port, sb)
-    snd.start()
+    # UDP_BENCH_SENDERS > 1: more sender threads (each its own socket), so that the
+    # receiver, not the sender, bounds the rate and the socket queue holds larger batches
+    txs = [tx] + [sockets_tx() for _ in range(SENDERS - 1)]
+    snds = [Sender(t, port, sb) for t in txs]
+    for snd_i in snds:
+        snd_i.start()
+    snd = snds[0]
     got = kept = nbytes = calls = 0
     bad = 0
     pend = {}                                       # gpu2: slot -> (count, lengths, ok) in flight
@@ -139,16 +154,20 @@ def receive_mode(mode, ctx, sb, ol):
         bad += n - int(ok.sum())
         nbytes += int(lens[lens != enethip.DGRAM_TRUNCATED].astype(np.uint64).sum())
     dt = time.perf_counter() - t0
-    snd.stop = True
-    snd.join()
+    for snd_i in snds:
+        snd_i.stop = True
+    for snd_i in snds:
+        snd_i.join()
     rx.close()
-    tx.close()
+    for t in txs:
+        t.close()
     free(p)
     free(p2)
     assert bad == 0, f"{mode}: {bad} stamped DGRAMs dropped"
     return {"side": "receive", "mode": mode, "seconds": round(dt, 2), "dgrams": got, "kept": kept,
             "dgrams_per_s": round(got / dt), "GBps": round(nbytes / dt / 1e9, 3),
-            "mean_batch": round(got / max(1, calls), 1), "sender_dgrams_per_s": round(snd.sent / dt)}
+            "mean_batch": round(got / max(1, calls), 1), "senders": len(snds),
+            "sender_dgrams_per_s": round(sum(x.sent for x in snds) / dt)}
 
 
 class Drain(threading.Thread):
@@ -297,8 +316,14 @@ def main():
                 print(json.dumps(call_latency(ctx, sb, mode, k)), flush=True)
         ctx.close()
         return
-    for mode in ("recv", "gpu", "gpu2", "callback", "port"):
+    modes = ("recv", "gpu", "gpu2", "callback", "port")
+    if os.environ.get("UDP_BENCH_RECV_MODES"):       # (a subset of the receive modes, and no send side)
+        modes = tuple(os.environ["UDP_BENCH_RECV_MODES"].split(","))
+    for mode in modes:
         print(json.dumps(receive_mode(mode, ctx, sb, ol)), flush=True)
+    if os.environ.get("UDP_BENCH_RECV_MODES"):
+        ctx.close()
+        return
     sb2 = workloads.send_batch(int(os.environ.get("UDP_BENCH_DGRAMS", "65536")), body=(1188, 1188), seed=10)
     for mode in ("gpu", "callback"):
         print(json.dumps(send_mode(mode, ctx, sb2, ol)), flush=True)
