@@ -439,17 +439,24 @@ def lin_abl(ablate: int) -> int:
     return (3 if v & 2 else 1) if v & 1 else 0
 
 
-def load_traffic(cfg: str, binned: bool = False):
+def load_traffic(cfg: str, binned: bool = False, lib_sha256: str | None = None):
     """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/), or None
     when there is none for this entry: profiles/traffic_<cfg>.json is the plain /
     batch-list entry's, traffic_<cfg>_binned.json the length-binned entry's, and each
-    file's "binned" tag must agree with its name."""
+    file's "binned" tag must agree with its name.  The pass records the sha256 of the
+    library it ran (tools/traffic.py): a record of any other build -- an older pass, a
+    rebuilt library, the diagnostics library -- is not this run's traffic, so None
+    (VERDICT r5 #2)."""
     p = os.path.join(ROOT, "profiles", f"traffic_{cfg}{'_binned' if binned else ''}.json")
     try:
         doc = json.load(open(p))
     except (OSError, ValueError):
         return None
-    return doc if bool(doc.get("binned", False)) == bool(binned) else None
+    if bool(doc.get("binned", False)) != bool(binned):
+        return None
+    if lib_sha256 is None or doc.get("library_sha256") != lib_sha256:
+        return None
+    return doc
 
 
 def cpu_line(cpu: dict) -> dict:
@@ -605,7 +612,8 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
         cpu = (cpu_factory or cpu_baseline)(batches[0], args.cpu_seconds, args.cpu_threads)
 
     if rank == 0:
-        traffic = load_traffic(args.config, args.binned)
+        import enethip
+        traffic = load_traffic(args.config, args.binned, enethip.library_sha256(diag))
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -651,6 +659,10 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": (None if not (traffic or {}).get("hbm_bytes_per_batch") else
                             round(traffic["hbm_bytes_per_batch"] * per_launch / float(batches[0].payload_bytes))),
+                "traffic_source": (None if not traffic else
+                                   f"profiles/traffic_{args.config}{'_binned' if args.binned else ''}.json "
+                                   f"(FETCH_SIZE pass of library sha256 {traffic['library_sha256'][:12]}, "
+                                   f"the build this run loaded)"),
                 "kernel": kernel_name(args, per_launch_steps > 1),
                 "kernel_ms": round(r_ms, 5),
                 "kernel_ms_timing": f"HIP events around {nk} serial launches on the launch stream",

@@ -52,11 +52,20 @@ struct enet_hip_context {
     hipEvent_t pipe_ev[2] = {nullptr, nullptr}; // the staging of stream s has been copied
     uint8_t* h_out = nullptr;                   // pinned landing zone of the D2H result copies
     size_t h_out_cap = 0;
-    // enet_hip_udp_receive_verify_submit / _complete: slot s's batch in flight on pipe[s]
-    // (its staging in h_pipe[s] / d_pipe[s]): the caller's ok[], the DGRAM count, pending
+    // enet_hip_udp_receive_verify(_submit / _complete): slot s's batch in flight on its own
+    // stream rx_st[s] with its own pinned / device staging (rx_h[s] / rx_d[s]), apart from
+    // the pipe / h_pipe / d_pipe / h_out the send and batch host entries use, so those run
+    // while a slot is in flight.  The caller's ok[], the DGRAM count, pending;
+    // rx_busy[s]: the slot is reserved by a receive whose socket wait runs outside mu
     uint8_t* rx_ok[2] = {nullptr, nullptr};
     size_t rx_n[2] = {0, 0};
     bool rx_pending[2] = {false, false};
+    bool rx_busy[2] = {false, false};
+    hipStream_t rx_st[2] = {nullptr, nullptr};
+    uint8_t* rx_h[2] = {nullptr, nullptr};
+    size_t rx_h_cap[2] = {0, 0};
+    uint8_t* rx_d[2] = {nullptr, nullptr};
+    size_t rx_d_cap[2] = {0, 0};
     uint8_t* d_ws = nullptr;                    // gather / binned workspace
     size_t d_ws_cap = 0;
     // fragment reassembly claim words (all ~0 between calls)

@@ -24,6 +24,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -43,6 +44,7 @@ constexpr size_t kGatherInPlaceSpan = ENET_HIP_GATHER_INPLACE_SPAN;
 int pipeline_init(enet_hip_context* ctx) {
     for (int s = 0; s < 2; ++s) {
         if (!ctx->pipe[s]) ENH_CHECK(hipStreamCreateWithFlags(&ctx->pipe[s], hipStreamNonBlocking));
+        if (!ctx->rx_st[s]) ENH_CHECK(hipStreamCreateWithFlags(&ctx->rx_st[s], hipStreamNonBlocking));
         if (!ctx->pipe_ev[s]) ENH_CHECK(hipEventCreateWithFlags(&ctx->pipe_ev[s], hipEventDisableTiming));
     }
     return 0;
@@ -50,6 +52,16 @@ int pipeline_init(enet_hip_context* ctx) {
 
 void pipeline_release(enet_hip_context* ctx) {
     for (int s = 0; s < 2; ++s) {
+        if (ctx->rx_st[s]) {
+            (void)hipStreamSynchronize(ctx->rx_st[s]);
+            (void)hipStreamDestroy(ctx->rx_st[s]);
+        }
+        (void)hipFree(ctx->rx_d[s]);
+        (void)hipHostFree(ctx->rx_h[s]);
+        ctx->rx_st[s] = nullptr;
+        ctx->rx_d[s] = nullptr;
+        ctx->rx_h[s] = nullptr;
+        ctx->rx_d_cap[s] = ctx->rx_h_cap[s] = 0;
         if (ctx->pipe[s]) (void)hipStreamSynchronize(ctx->pipe[s]);
         (void)hipFree(ctx->d_pipe[s]);
         (void)hipHostFree(ctx->h_pipe[s]);
@@ -162,7 +174,6 @@ int enet_hip_crc32_batch_host(enet_hip_context* ctx, const uint8_t* bytes, size_
         }
     }
     std::lock_guard<std::mutex> lk(ctx->mu);
-    if (ctx->rx_pending[0] || ctx->rx_pending[1]) return -static_cast<int>(hipErrorInvalidValue);   // (async receive slots hold the staging)
     ENH_CHECK(hipSetDevice(ctx->device));
     int rc;
     if ((rc = pipeline_init(ctx))) return rc;
@@ -299,7 +310,6 @@ int enet_hip_crc32_gather_binned_host(enet_hip_context* ctx, const uint8_t* byte
     lo &= ~uint64_t(15);
     const size_t span = static_cast<size_t>(hi - lo);
     std::lock_guard<std::mutex> lk(ctx->mu);
-    if (ctx->rx_pending[0] || ctx->rx_pending[1]) return -static_cast<int>(hipErrorInvalidValue);   // (async receive slots hold the staging)
     ENH_CHECK(hipSetDevice(ctx->device));
     int rc;
     if ((rc = pipeline_init(ctx))) return rc;
@@ -380,40 +390,37 @@ int enet_hip_crc32_gather_binned_host(enet_hip_context* ctx, const uint8_t* byte
     return 0;
 }
 
-// The receive batch of slot s (0 or 1): receive, header stage, GPU verify and the keep
-// mask into slot s's pinned staging, all queued on pipe[s]; the caller (under ctx->mu)
-// waits with rx_complete.  A pinned arena (the usual case: enet_hip_host_alloc) is
-// verified in place: the kernel reads the DGRAMs at their arena offsets and the metadata
-// from the slot's pinned staging over PCIe, and writes the keep mask straight into it --
-// one launch and no copies, where the copy form queues a pitched H2D, a metadata H2D and
-// a D2H around it (each several microseconds for a batch of a few dozen DGRAMs).  A
+// The receive batch of slot s (0 or 1), once the socket receive has returned its n
+// DGRAMs: header stage, GPU verify and the keep mask into slot s's own pinned staging,
+// all queued on its own stream rx_st[s]; the caller holds ctx->mu and waits with
+// rx_complete.  A pinned arena (the usual case: enet_hip_host_alloc) is verified in
+// place: the kernel reads the DGRAMs at their arena offsets and the metadata from the
+// slot's pinned staging over PCIe, and writes the keep mask straight into it -- one
+// launch and no copies, where the copy form queues a pitched H2D, a metadata H2D and a
+// D2H around it (each several microseconds for a batch of a few dozen DGRAMs).  A
 // pageable arena takes the copy form: only each DGRAM slot's first maxLen bytes cross.
-static int rx_submit(enet_hip_context* ctx, int slot, int fd, uint8_t* arena, size_t stride, size_t maxDgrams,
-                     const uint32_t* peerConnectIds, size_t peerCount, int timeoutMs, uint32_t* lengths, uint8_t* ok,
-                     size_t* received) {
-    size_t n = 0;
-    int rc = enet_hip_udp_receive(fd, arena, stride, maxDgrams, lengths, nullptr, nullptr, timeoutMs, &n);
-    if (rc) return rc;                                   // -errno
-    *received = n;
+static int rx_stage(enet_hip_context* ctx, int slot, uint8_t* arena, size_t stride, size_t n,
+                    const uint32_t* peerConnectIds, size_t peerCount, uint32_t* lengths, uint8_t* ok) {
     ctx->rx_ok[slot] = ok;
     ctx->rx_n[slot] = n;
     if (n == 0) return 0;
     ENH_CHECK(hipSetDevice(ctx->device));
+    int rc;
     if ((rc = pipeline_init(ctx))) return rc;
     // pinned staging: off u64 | len | slot | connect | verdict | ok (D2H)
     const size_t ho = align16(8 * n), hl = align16(4 * n), hv = align16(n);
-    if ((rc = ensure_pinned(&ctx->h_pipe[slot], &ctx->h_pipe_cap[slot], ho + 3 * hl + 2 * hv))) return rc;
-    uint64_t* h_off = reinterpret_cast<uint64_t*>(ctx->h_pipe[slot]);
-    uint32_t* h_len = reinterpret_cast<uint32_t*>(ctx->h_pipe[slot] + ho);
-    uint32_t* h_slot = reinterpret_cast<uint32_t*>(ctx->h_pipe[slot] + ho + hl);
-    uint32_t* h_conn = reinterpret_cast<uint32_t*>(ctx->h_pipe[slot] + ho + 2 * hl);
-    uint8_t* h_verdict = ctx->h_pipe[slot] + ho + 3 * hl;
+    if ((rc = ensure_pinned(&ctx->rx_h[slot], &ctx->rx_h_cap[slot], ho + 3 * hl + 2 * hv))) return rc;
+    uint64_t* h_off = reinterpret_cast<uint64_t*>(ctx->rx_h[slot]);
+    uint32_t* h_len = reinterpret_cast<uint32_t*>(ctx->rx_h[slot] + ho);
+    uint32_t* h_slot = reinterpret_cast<uint32_t*>(ctx->rx_h[slot] + ho + hl);
+    uint32_t* h_conn = reinterpret_cast<uint32_t*>(ctx->rx_h[slot] + ho + 2 * hl);
+    uint8_t* h_verdict = ctx->rx_h[slot] + ho + 3 * hl;
     uint8_t* h_ok = h_verdict + hv;
     if ((rc = enet_hip_parse_headers(arena, stride, lengths, n, peerConnectIds, peerCount, h_slot, h_conn, h_verdict)))
         return rc;
-    hipStream_t st = ctx->pipe[slot];
+    hipStream_t st = ctx->rx_st[slot];
     uint8_t* zc = pinned_device_view(arena, ctx->device);
-    uint8_t* zs = zc ? pinned_device_view(ctx->h_pipe[slot], ctx->device) : nullptr;
+    uint8_t* zs = zc ? pinned_device_view(ctx->rx_h[slot], ctx->device) : nullptr;
     if (zc && zs) {
         for (size_t i = 0; i < n; ++i) {
             h_off[i] = i * stride;
@@ -437,8 +444,8 @@ static int rx_submit(enet_hip_context* ctx, int slot, int fd, uint8_t* arena, si
     }
     // device: [DGRAMs at `pitch` | off | len | slot | connect | ok]
     const size_t db = align16(n * pitch + 16);
-    if ((rc = ensure_device(&ctx->d_pipe[slot], &ctx->d_pipe_cap[slot], db + ho + 3 * hl + hv))) return rc;
-    uint8_t* d = ctx->d_pipe[slot];
+    if ((rc = ensure_device(&ctx->rx_d[slot], &ctx->rx_d_cap[slot], db + ho + 3 * hl + hv))) return rc;
+    uint8_t* d = ctx->rx_d[slot];
     uint64_t* d_off = reinterpret_cast<uint64_t*>(d + db);
     uint32_t* d_len = reinterpret_cast<uint32_t*>(d + db + ho);
     uint32_t* d_slot = reinterpret_cast<uint32_t*>(d + db + ho + hl);
@@ -458,13 +465,39 @@ static int rx_complete(enet_hip_context* ctx, int slot) {
     if (!ctx->rx_pending[slot]) return 0;                // (an empty batch: nothing queued)
     ctx->rx_pending[slot] = false;
     ENH_CHECK(hipSetDevice(ctx->device));
-    ENH_CHECK(hipStreamSynchronize(ctx->pipe[slot]));
+    ENH_CHECK(hipStreamSynchronize(ctx->rx_st[slot]));
     const size_t n = ctx->rx_n[slot];
     const size_t ho = align16(8 * n), hl = align16(4 * n), hv = align16(n);
-    const uint8_t* h_verdict = ctx->h_pipe[slot] + ho + 3 * hl;
+    const uint8_t* h_verdict = ctx->rx_h[slot] + ho + 3 * hl;
     const uint8_t* h_ok = h_verdict + hv;
     for (size_t i = 0; i < n; ++i) ctx->rx_ok[slot][i] = h_verdict[i] == ENET_HIP_DGRAM_CHECKSUM ? h_ok[i] : 0u;
     return 0;
+}
+
+// A receive on slot s: the slot is reserved under ctx->mu (neither pending nor reserved
+// by another receive), the socket wait -- up to timeoutMs, or forever when it is
+// negative -- runs with mu released, so another thread's stamp_send, range coder or batch
+// call on the same context is not held behind it, then the header stage and
+// the launch run under mu again.  A failed staging drains what it queued.
+static int rx_receive_submit(enet_hip_context* ctx, int slot, int fd, uint8_t* arena, size_t stride,
+                             size_t maxDgrams, const uint32_t* peerConnectIds, size_t peerCount, int timeoutMs,
+                             uint32_t* lengths, uint8_t* ok, size_t* received, std::unique_lock<std::mutex>& lk) {
+    lk.lock();
+    if (ctx->rx_pending[slot] || ctx->rx_busy[slot]) return -static_cast<int>(hipErrorInvalidValue);   // (complete it first)
+    ctx->rx_busy[slot] = true;
+    lk.unlock();
+    size_t n = 0;
+    const int rrc = enet_hip_udp_receive(fd, arena, stride, maxDgrams, lengths, nullptr, nullptr, timeoutMs, &n);
+    lk.lock();
+    ctx->rx_busy[slot] = false;
+    if (rrc) return rrc;                                 // -errno
+    *received = n;
+    const int rc = rx_stage(ctx, slot, arena, stride, n, peerConnectIds, peerCount, lengths, ok);
+    if (rc) {                                            // (whatever was queued before the failure: drained)
+        if (ctx->rx_st[slot]) (void)hipStreamSynchronize(ctx->rx_st[slot]);
+        ctx->rx_pending[slot] = false;
+    }
+    return rc;
 }
 
 int enet_hip_udp_receive_verify(enet_hip_context* ctx, int fd, uint8_t* arena, size_t stride, size_t maxDgrams,
@@ -474,15 +507,10 @@ int enet_hip_udp_receive_verify(enet_hip_context* ctx, int fd, uint8_t* arena, s
     if (!ctx || !received) return -static_cast<int>(hipErrorInvalidValue);
     if (!arena || !lengths || !ok || (peerCount && !peerConnectIds) || stride < 16)
         return -static_cast<int>(hipErrorInvalidValue);
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    if (ctx->rx_pending[0] || ctx->rx_pending[1]) return -static_cast<int>(hipErrorInvalidValue);   // (async slots in flight)
-    int rc = rx_submit(ctx, 0, fd, arena, stride, maxDgrams, peerConnectIds, peerCount, timeoutMs, lengths, ok,
-                       received);
-    if (rc) {                                            // (whatever was queued before the failure: drained)
-        if (ctx->pipe[0]) (void)hipStreamSynchronize(ctx->pipe[0]);
-        ctx->rx_pending[0] = false;
-        return rc;
-    }
+    std::unique_lock<std::mutex> lk(ctx->mu, std::defer_lock);
+    const int rc = rx_receive_submit(ctx, 0, fd, arena, stride, maxDgrams, peerConnectIds, peerCount, timeoutMs,
+                                     lengths, ok, received, lk);
+    if (rc) return rc;
     return rx_complete(ctx, 0);
 }
 
@@ -493,15 +521,9 @@ int enet_hip_udp_receive_verify_submit(enet_hip_context* ctx, int fd, uint8_t* a
     if (!ctx || !received) return -static_cast<int>(hipErrorInvalidValue);
     if (!arena || !lengths || !ok || (peerCount && !peerConnectIds) || stride < 16 || slot < 0 || slot > 1)
         return -static_cast<int>(hipErrorInvalidValue);
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    if (ctx->rx_pending[slot]) return -static_cast<int>(hipErrorInvalidValue);   // (complete it first)
-    const int rc = rx_submit(ctx, slot, fd, arena, stride, maxDgrams, peerConnectIds, peerCount, timeoutMs, lengths,
-                             ok, received);
-    if (rc) {                                            // (whatever was queued before the failure: drained)
-        if (ctx->pipe[slot]) (void)hipStreamSynchronize(ctx->pipe[slot]);
-        ctx->rx_pending[slot] = false;
-    }
-    return rc;
+    std::unique_lock<std::mutex> lk(ctx->mu, std::defer_lock);
+    return rx_receive_submit(ctx, slot, fd, arena, stride, maxDgrams, peerConnectIds, peerCount, timeoutMs, lengths,
+                             ok, received, lk);
 }
 
 int enet_hip_udp_receive_verify_complete(enet_hip_context* ctx, int slot) {
@@ -523,7 +545,6 @@ int enet_hip_udp_receive_decompress_verify(enet_hip_context* ctx, int fd, uint8_
     *received = n;
     if (n == 0) return 0;
     std::lock_guard<std::mutex> lk(ctx->mu);
-    if (ctx->rx_pending[0] || ctx->rx_pending[1]) return -static_cast<int>(hipErrorInvalidValue);   // (async receive slots hold the staging)
     ENH_CHECK(hipSetDevice(ctx->device));
     if ((rc = pipeline_init(ctx))) return rc;
     // pinned staging: off u64 | len | slot | connect | verdict, then the compressed
@@ -664,7 +685,6 @@ int enet_hip_udp_compress_stamp_send(enet_hip_context* ctx, int fd, uint8_t* byt
     int rc;
     {
         std::lock_guard<std::mutex> lk(ctx->mu);
-        if (ctx->rx_pending[0] || ctx->rx_pending[1]) return -static_cast<int>(hipErrorInvalidValue);   // (async receive slots hold the staging)
         ENH_CHECK(hipSetDevice(ctx->device));
         if ((rc = pipeline_init(ctx))) return rc;
         const size_t ab = align16(total + 16), ho = align16(8 * n), hl = align16(4 * n);
@@ -697,17 +717,26 @@ int enet_hip_udp_compress_stamp_send(enet_hip_context* ctx, int fd, uint8_t* byt
         memcpy(out_len.data(), hp + ab + ho + hl, 4 * n);
         memcpy(comp.data(), hp + ab + ho + 2 * hl, total);
     }
-    // protocol.cs:1670-1676: keep the compressed form only when it is shorter; the flag
-    // goes into the header before the CRC (it is part of the checksummed bytes)
-    std::vector<uint8_t> keep(n);
+    // protocol.cs:1670-1676: keep the compressed form only when it is shorter.  The
+    // reference builds headerFlags fresh for every send, so the flag bit is SET for a kept
+    // DGRAM and CLEARED for the others (a reused or retried arena may carry it from an
+    // earlier send: sent uncompressed but flagged, the receiver would decompress plain
+    // commands and drop it -- ADVICE r5).  It goes into the header before the CRC (it is
+    // part of the checksummed bytes); a failed CRC call restores the caller's header bytes.
+    constexpr uint8_t kFlagByte = static_cast<uint8_t>(kHeaderFlagCompressed >> 8);
+    std::vector<uint8_t> keep(n), hdr0(n);
     for (size_t d = 0; d < n; ++d) {
         keep[d] = out_len[d] > 0u && out_len[d] < in_len[d];
-        if (keep[d]) bytes[segOffsets[segFirst[d]]] |= static_cast<uint8_t>(kHeaderFlagCompressed >> 8);
+        uint8_t& h = bytes[segOffsets[segFirst[d]]];
+        hdr0[d] = h;
+        h = keep[d] ? static_cast<uint8_t>(h | kFlagByte) : static_cast<uint8_t>(h & ~kFlagByte);
     }
     std::vector<uint32_t> crc(n);
     if ((rc = enet_hip_crc32_gather_binned_host(ctx, bytes, byteCount, segOffsets, segLengths, segCount, segFirst, n,
-                                                crc.data())))
+                                                crc.data()))) {
+        for (size_t d = n; d-- > 0;) bytes[segOffsets[segFirst[d]]] = hdr0[d];   // (reverse: shared first buffers end as they began)
         return rc;
+    }
     for (size_t d = 0; d < n; ++d)                        // protocol.cs:1697: the slot := the CRC
         memcpy(bytes + segOffsets[segFirst[d]] + slotOffsets[d], &crc[d], 4);
     // protocol.cs:1700-1705: the wire form -- the first buffer, then the compressed

@@ -84,6 +84,19 @@ class ENetBuffer(ctypes.Structure):
 _libs: dict = {}
 
 
+def library_sha256(diag: bool = False, path: str | None = None) -> str | None:
+    """sha256 of the library file load() would open (None if absent).  Measurements
+    committed under profiles/ (the traffic passes) record it, and bench.py uses a record
+    only with the very build it was taken with (VERDICT r5 #2)."""
+    import hashlib
+    p = path or (DIAG_LIB_PATH if diag else LIB_PATH)
+    try:
+        with open(p, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()
+    except OSError:
+        return None
+
+
 def load(path: str | None = None, diag: bool = False) -> ctypes.CDLL:
     """The product library (or, diag=True, the diagnostics build)."""
     key = path or (DIAG_LIB_PATH if diag else LIB_PATH)

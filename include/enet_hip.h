@@ -356,7 +356,10 @@ ENET_HIP_API int enet_hip_verify_callback(uint8_t* arena, size_t stride, const u
  * memory registered with HIP) is verified in place: the kernel reads the DGRAMs and the
  * metadata over PCIe and writes the keep mask into pinned staging, with no copies.  A
  * pageable arena takes one pitched H2D (only each slot's first maxLen bytes cross PCIe)
- * and a D2H of the keep mask.  The arena is not modified.  Synchronous. */
+ * and a D2H of the keep mask.  The arena is not modified.  Synchronous.  Runs as slot 0
+ * of the two-slot form below (-hipErrorInvalidValue while slot 0 is in flight).  The
+ * socket wait (up to timeoutMs; forever when negative) holds no lock of the context:
+ * another thread's send or batch call on the same context runs meanwhile. */
 ENET_HIP_API int enet_hip_udp_receive_verify(enet_hip_context* ctx, int fd, uint8_t* arena, size_t stride,
                                              size_t maxDgrams, const uint32_t* peerConnectIds, size_t peerCount,
                                              int timeoutMs, uint32_t* lengths, uint8_t* ok, size_t* received);
@@ -369,12 +372,13 @@ ENET_HIP_API int enet_hip_udp_receive_verify(enet_hip_context* ctx, int fd, uint
  * _submit receives and runs the header stage like enet_hip_udp_receive_verify
  * (lengths[] and *received are set when it returns), queues the GPU verify (in place
  * on a pinned arena; else with the pitched H2D and the keep mask's D2H) on the
- * context's pipeline stream `slot`, and
- * returns without waiting; _complete(slot) waits for that batch and writes ok[] (the
- * header stage's drops 0).  arena, lengths and ok of a slot stay the caller's until
- * its _complete.  -hipErrorInvalidValue for a slot already in flight, and from the
- * other host-memory entry points of the context while a slot is in flight (they
- * share its staging). */
+ * slot's own stream, and returns without waiting; _complete(slot) waits for that batch
+ * and writes ok[] (the header stage's drops 0).  arena, lengths and ok of a slot stay
+ * the caller's until its _complete.  -hipErrorInvalidValue for a slot already in
+ * flight (or still receiving on another thread).  Each slot has its own stream and
+ * staging, apart from the other host-memory entry points' (round 6): a host sends
+ * (enet_hip_udp_stamp_send, _compress_stamp_send) and runs batch calls on the same
+ * context while slots are in flight, and a receive's socket wait holds no lock. */
 ENET_HIP_API int enet_hip_udp_receive_verify_submit(enet_hip_context* ctx, int fd, uint8_t* arena, size_t stride,
                                                     size_t maxDgrams, const uint32_t* peerConnectIds,
                                                     size_t peerCount, int timeoutMs, uint32_t* lengths, uint8_t* ok,

@@ -132,15 +132,34 @@ def test_cpu_line_states_quota_and_speedup():
     assert th == (min(info["affinity_cores"], int(np.ceil(q))) if q else info["affinity_cores"])
 
 
-def test_traffic_files_match_their_entry():
+def test_traffic_files_match_their_entry_and_build(tmp_path, monkeypatch):
     """profiles/traffic_<cfg>.json belongs to the plain / list entry and
-    traffic_<cfg>_binned.json to the binned one; bench.py hands each line its own."""
+    traffic_<cfg>_binned.json to the binned one; bench.py hands each line its own, and
+    only when the record's library_sha256 is the build the run loaded (VERDICT r5 #2:
+    a stale pass of an older build is not this run's traffic)."""
     import bench
-    t3b = bench.load_traffic("cfg3", binned=True)
-    assert t3b is not None and t3b["binned"] is True
-    assert bench.load_traffic("cfg3", binned=False) is None or bench.load_traffic("cfg3")["binned"] is False
-    t2 = bench.load_traffic("cfg2")
-    assert t2 is not None and not t2.get("binned", False)
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    (prof / "traffic_cfg2.json").write_text(json.dumps({"hbm_bytes_per_batch": 86e6, "library_sha256": "aa"}))
+    (prof / "traffic_cfg3_binned.json").write_text(json.dumps({"hbm_bytes_per_batch": 1.0, "binned": True,
+                                                                "library_sha256": "aa"}))
+    (prof / "traffic_cfg3.json").write_text(json.dumps({"hbm_bytes_per_batch": 1.0, "binned": True,
+                                                         "library_sha256": "aa"}))   # (mislabelled)
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert bench.load_traffic("cfg2", False, "aa")["hbm_bytes_per_batch"] == 86e6
+    assert bench.load_traffic("cfg2", False, "bb") is None             # another build
+    assert bench.load_traffic("cfg2", False, None) is None             # library not found
+    assert bench.load_traffic("cfg3", True, "aa")["binned"] is True
+    assert bench.load_traffic("cfg3", False, "aa") is None             # tag disagrees with the name
+    assert bench.load_traffic("cfg4", False, "aa") is None             # no record
+
+
+def test_committed_traffic_records_name_their_build():
+    """Every committed traffic record names the library build it was measured with."""
+    import glob
+    for f in glob.glob(os.path.join(ROOT, "profiles", "traffic_*.json")):
+        d = json.load(open(f))
+        assert len(d.get("library_sha256") or "") == 64, f
 
 
 def test_one_rank_line_carries_the_cpu_baseline(monkeypatch):

@@ -4,6 +4,8 @@ batches (cfg2 in full, many chunks, offsets out of order, multi-context shards),
 the host gather lists at full cfg5 size (4096 x 64 KiB messages = 200 704
 DGRAMs), and the GPU stamp / receive-verify over a loopback socket."""
 import socket
+import threading
+import time
 
 import numpy as np
 import pytest
@@ -367,9 +369,9 @@ def test_gpu_receive_verify_submit_complete_two_slots(ctx, oracle_lib):  # noqa:
     """enet_hip_udp_receive_verify_submit / _complete: batches received into two arenas
     in turn, each one's GPU verify in flight while the next is received; every keep
     mask equal to the oracle's (header stage restated: expected_keep), corrupted and odd
-    DGRAMs among them.  While a slot is in flight the synchronous receive and the other
-    host-memory entries refuse (they share its staging), and a slot cannot be submitted
-    twice."""
+    DGRAMs among them.  While slot 0 is in flight the synchronous receive (which runs as
+    slot 0) refuses and the slot cannot be submitted twice; the send and batch host
+    entries, which have staging of their own (round 6), run and are exact."""
     sb = workloads.send_batch(2400, seed=95)
     g = sb.gather
     rng = np.random.default_rng(96)
@@ -413,6 +415,12 @@ def test_gpu_receive_verify_submit_complete_two_slots(ctx, oracle_lib):  # noqa:
                         ctx.udp_receive_verify_submit(slot, rx.fileno(), arenas[1][0], STRIDE, 512, sb.peers)
                     with pytest.raises(enethip.ENetHipError):
                         ctx.udp_receive_verify(rx.fileno(), arenas[1][0], STRIDE, 512, sb.peers)
+                    # the host batch and gather entries run beside the slot in flight
+                    hb = workloads.fixed(300, 700, seed=98)
+                    assert (ctx.crc32_batch_host(hb.payload, hb.off, hb.lens) ==
+                            oracle_lib.batch(hb.payload, hb.off, hb.lens)).all()
+                    assert (ctx.gather_binned_host(g.payload, g.seg_off, g.seg_len, g.seg_first[:101]) ==
+                            oracle_lib.gather(g.payload, g.seg_off, g.seg_len, g.seg_first[:101])).all()
                 pending[slot] = (arena, n, lens.copy(), ok)
                 got += n
                 rows += n
@@ -439,5 +447,118 @@ def test_gpu_receive_verify_submit_complete_two_slots(ctx, oracle_lib):  # noqa:
     finally:
         for _, p in arenas:
             free_pinned(p)
+        rx.close()
+        tx.close()
+
+
+def test_send_runs_while_receive_waits(ctx, oracle_lib):  # noqa: F811
+    """a receive's socket wait holds no lock of the context.  One
+    thread blocks in enet_hip_udp_receive_verify on an idle socket (3 s timeout); on the
+    same context another thread's enet_hip_udp_stamp_send and host batch call finish
+    while it still waits, with stamps equal to the oracle's; the receive then times out
+    with nothing received."""
+    sb = workloads.send_batch(400, seed=97)
+    g = sb.gather
+    exp = oracle_stamps(oracle_lib, sb)
+    rx1, tx1, port1 = sockets()
+    rx2, tx2, port2 = sockets()
+    arena, p = pinned(STRIDE * 64)
+    res = {}
+
+    def waiter():
+        t0 = time.perf_counter()
+        try:
+            res["rx"] = ctx.udp_receive_verify(rx1.fileno(), arena, STRIDE, 64, sb.peers, timeout_ms=3000)
+        except Exception as e:                                   # (reported by the main thread)
+            res["err"] = e
+        res["secs"] = time.perf_counter() - t0
+
+    th = threading.Thread(target=waiter)
+    try:
+        th.start()
+        time.sleep(0.3)                                          # the waiter is in its socket wait
+        t0 = time.perf_counter()
+        sent = ctx.udp_stamp_send(tx2.fileno(), g.payload, g.seg_off, g.seg_len, g.seg_first, sb.slot_off,
+                                  LOOPBACK, port2)
+        hb = workloads.fixed(200, 900, seed=99)
+        crcs = ctx.crc32_batch_host(hb.payload, hb.off, hb.lens)
+        dt = time.perf_counter() - t0
+        assert th.is_alive(), "the receive returned before the sends ran"
+        assert dt < 1.5, dt                                      # not held behind the 3-s wait
+        assert sent == sb.n
+        assert (slots_of(sb) == exp).all()
+        assert (crcs == oracle_lib.batch(hb.payload, hb.off, hb.lens)).all()
+        th.join(10)
+        assert not th.is_alive()
+        assert "err" not in res, res.get("err")
+        assert res["rx"][0] == 0 and res["secs"] >= 2.5          # timed out, nothing received
+    finally:
+        th.join(10)
+        free_pinned(p)
+        for s_ in (rx1, tx1, rx2, tx2):
+            s_.close()
+
+
+def test_in_place_arenas_ending_on_a_page(ctx, oracle_lib):  # noqa: F811
+    """the in-place paths on pinned arenas whose size is a whole number
+    of pages, with packets and segments that end exactly on the arena's last byte (ragged
+    and 16-byte-aligned ends, unaligned starts), so an over-read by a whole 16-B granule
+    would leave the allocation instead of landing in the page's slack.  Batch and gather
+    host entries against the oracle; the receive case is
+    test_receive_verify_dgram_ending_on_the_arena."""
+    rng = np.random.default_rng(100)
+    for n in (1 << 20, 4 << 20):                                # (both at most the 4-MiB in-place span)
+        arr, p = pinned(n)
+        try:
+            arr[:] = rng.integers(0, 256, size=n, dtype=np.uint8)
+            tails = np.array([1, 2, 15, 16, 17, 31, 32, 33, 63, 64, 65, 255, 1199, 1200, 1399, 4096], np.uint32)
+            k = 600
+            lens = np.concatenate([tails, rng.integers(0, 1500, size=k).astype(np.uint32)])
+            off = np.concatenate([n - tails.astype(np.uint64),
+                                  rng.integers(0, n - 1500, size=k).astype(np.uint64)])
+            assert (ctx.crc32_batch_host(arr, off, lens) == oracle_lib.batch(arr, off, lens)).all(), n
+            # one packet alone, ending on the last byte (the smallest launch)
+            for t in (3, 16, 1201):
+                o1, l1 = np.array([n - t], np.uint64), np.array([t], np.uint32)
+                assert (ctx.crc32_batch_host(arr, o1, l1) == oracle_lib.batch(arr, o1, l1)).all(), (n, t)
+            # gather lists whose LAST segments end on the last byte
+            cnt = rng.integers(1, 6, size=200)
+            sf = np.zeros(201, np.uint32)
+            np.cumsum(cnt, out=sf[1:])
+            ns = int(sf[-1])
+            sl = rng.integers(0, 1400, size=ns).astype(np.uint32)
+            so = rng.integers(0, n - 1400, size=ns).astype(np.uint64)
+            last = sf[1:] - 1
+            sl[last[:16]] = tails
+            so[last[:16]] = n - tails.astype(np.uint64)
+            assert (ctx.gather_binned_host(arr, so, sl, sf) == oracle_lib.gather(arr, so, sl, sf)).all(), n
+        finally:
+            free_pinned(p)
+
+
+def test_receive_verify_dgram_ending_on_the_arena(ctx, oracle_lib):  # noqa: F811
+    """The in-place receive verify on a pinned arena of exactly 8 receive slots (32 KiB,
+    page-multiple): the 8th DGRAM fills its 4096-B slot, so it ends on the arena's last
+    byte; ragged lengths before it.  Keep mask against the oracle (expected_keep)."""
+    rng = np.random.default_rng(101)
+    rx, tx, port = sockets()
+    arena, p = pinned(STRIDE * 8)
+    try:
+        lens = [17, 100, 1201, 1399, 33, 4095, 2049, STRIDE]
+        for L in lens:
+            body = bytearray(rng.integers(0, 256, size=L, dtype=np.uint8).tobytes())
+            body[0:2] = (0x0FFF).to_bytes(2, "big")               # no peer: connectID 0 in the slot
+            body[2:6] = b"\0\0\0\0"
+            body[2:6] = int(oracle_lib.crc32(bytes(body))).to_bytes(4, "little")
+            tx.sendto(bytes(body), ("127.0.0.1", port))
+        # (loopback queues all 8 before the call: one recvmmsg takes them in order, the
+        # full one into slot 7)
+        n, ln, ok = ctx.udp_receive_verify(rx.fileno(), arena, STRIDE, 8, [], timeout_ms=2000)
+        assert n == len(lens)
+        assert list(ln) == lens
+        assert (ok == expected_keep(oracle_lib, arena, STRIDE, ln, [])).all()
+        assert ok.all()
+    finally:
+        free_pinned(p)
         rx.close()
         tx.close()

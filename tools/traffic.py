@@ -12,6 +12,17 @@ import glob
 import json
 import sys
 from collections import defaultdict
+import os as _os
+
+
+def product_library_sha256():
+    """sha256 of the product library the pass ran (enet-csharp_amd/libenethip.so, or
+    ENET_HIP_LIBRARY): bench.py reads this record only with that same build."""
+    import sys as _sys
+    root = _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__)))
+    _sys.path.insert(0, _os.path.join(root, "enet-csharp_amd"))
+    import enethip
+    return enethip.library_sha256()
 
 
 def main():
@@ -43,6 +54,7 @@ def main():
         "probe_calibration": None if probe is None else round(probe * 2048 / probe_bytes, 4),
         "traffic_over_algorithmic": None if stream is None else round(stream * 2048 / payload, 4),
         "dispatches": {k: len(v) for k, v in vals.items()},
+        "library_sha256": product_library_sha256(),
     }
     print(json.dumps(doc, indent=1))
     if out:

@@ -14,6 +14,17 @@ import glob
 import json
 import re
 from collections import defaultdict
+import os as _os
+
+
+def product_library_sha256():
+    """sha256 of the product library the pass ran (enet-csharp_amd/libenethip.so, or
+    ENET_HIP_LIBRARY): bench.py reads this record only with that same build."""
+    import sys as _sys
+    root = _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__)))
+    _sys.path.insert(0, _os.path.join(root, "enet-csharp_amd"))
+    import enethip
+    return enethip.library_sha256()
 
 
 def main():
@@ -55,6 +66,7 @@ def main():
         # the length-binned entries run bin_tile_kernel: tag them whatever the flag said
         # (bench.py --binned reads traffic_<cfg>_binned.json and checks this tag)
         "binned": bool(a.binned or any("bin_tile_kernel" in k for k in per_kernel)),
+        "library_sha256": product_library_sha256(),
         "traffic_over_algorithmic": round(hbm / a.bytes, 4),
         "probe_calibration": (round(sum(probe) / len(probe) * 2048 / a.probe_bytes, 4)
                               if probe and a.probe_bytes else None),
