@@ -408,8 +408,6 @@ def kernel_name(args, list_launch: bool = False) -> str:
     crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT, VF, DYN>; DYN = 1 / 2, the chip-wide
     / pair rounds, when the diagnostics ablation 524288 / 8388608 selects them)."""
     path = getattr(args, "path", 0)
-    if path in (22, 23) and not args.binned:
-        return f"crc32_lin_kernel<{lin_abl(args.ablate)}, {1 if path == 22 else 0}>"
     if list_launch and path == 13 and args.lanes in (0, 4, 8) and not args.binned:
         # batch lists: the lean kernel's list instance, 8 lanes per packet unless set
         return f"crc32_lean_list_kernel<{3 if args.lanes in (0, 8) else 2}, 16, 2>"
@@ -431,12 +429,6 @@ def kernel_name(args, list_launch: bool = False) -> str:
     nt, rot = (1 if path == 18 else 0), (1 if path == 21 else 0)
     dyn = dyn if not (nt or rot or (args.ablate & ~(524288 | 8388608))) else 0
     return f"crc32_vring_kernel<{lg}, 0, {nt}, 0, 0, 0, {rot}, 0, {dyn}>"
-
-
-def lin_abl(ablate: int) -> int:
-    """The linear kernel's ablation instance for an enet_hip_diag_ablation value."""
-    v = (ablate >> 11) & 255
-    return (3 if v & 2 else 1) if v & 1 else 0
 
 
 def load_traffic(cfg: str, binned: bool = False, lib_sha256: str | None = None):

@@ -21,7 +21,6 @@ struct enet_hip_context {
     uint32_t* d_basis = nullptr; // lean-kernel table basis, kBasisDwords per image
     uint32_t* d_basis2 = nullptr; // vring-kernel table basis, kVrBasisDwords per image
     uint32_t* d_tz = nullptr;    // vring-kernel zero-byte multiplier tables (kTzTableDwords + kTzSmallDwords)
-    uint32_t* d_lin = nullptr;   // linear-kernel LDS image (crc32_lin.hip), kImageDwords
     int lanes_per_packet = 0;    // 0 = auto
     int wgs_per_cu = 0;          // 0 = auto (vring: 2; direct / gather kernels)
     int path = 0;                // enet_hip_set_kernel_path

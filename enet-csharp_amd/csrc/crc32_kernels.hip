@@ -30,7 +30,6 @@
 
 #include "crc32_device.hpp"
 #include "crc32_math.hpp"
-#include "crc32_lin.hpp"
 #include "crc32_lean.hpp"
 #include "crc32_vring.hpp"
 #include "crc32_stream_common.hpp"
@@ -987,15 +986,12 @@ constexpr int kImages = 4;                             // P = 1, 4, 8, 16
 constexpr int kImageP[kImages] = {1, 4, 8, 16};
 
 struct HostTables {
-    std::vector<uint32_t> image, xn, init, basis, basis2, tz, lin;
+    std::vector<uint32_t> image, xn, init, basis, basis2, tz;
     bool basis_ok = true;   // the bases rebuild every image dword the lean / vring kernels read
     HostTables()
         : image(static_cast<size_t>(kImages) * kImageDwords), xn(2 * kXnEntries), init(64),
           basis(static_cast<size_t>(kImages) * kBasisDwords), basis2(static_cast<size_t>(kImages) * kVrBasisDwords),
-          tz(kTzTableDwords + kTzSmallDwords), lin(kImageDwords) {
-#ifdef ENET_HIP_DIAG
-        if (lin_image(lin.data())) basis_ok = false;   // (the linear-stream kernel: diagnostics only)
-#endif
+          tz(kTzTableDwords + kTzSmallDwords) {
         init[0] = 0xFFFFFFFFu;
         for (int r = 1; r < 64; ++r) init[r] = unstep_zero(init[r - 1]);
         std::vector<uint32_t> cinv(kCinvEntries);
@@ -1209,10 +1205,10 @@ constexpr int kVringAltPath = kVringPath + 1;           // the same with nontemp
 constexpr int kVringWalkPath = kVringAltPath + 1;       // vring, workgroups walking contiguous group ranges
 constexpr int kVringWalkAltPath = kVringWalkPath + 1;   // the same with nontemporal stage loads
 constexpr int kVringTailFirstPath = kVringWalkAltPath + 1;   // vring, the tail-first stage order
-constexpr int kLinPath = kVringTailFirstPath + 1;      // crc32_lin.hip: linear stream, nontemporal tile DMA
-constexpr int kLinPlainPath = kLinPath + 1;            // the same with default-policy tile DMA
+// (paths 22 / 23, round 4's linear-stream kernel, were removed in round 6: closed by its
+// gate)
 #ifdef ENET_HIP_DIAG
-constexpr int kMaxPath = kLinPlainPath;
+constexpr int kMaxPath = kVringTailFirstPath;
 #endif
 
 // Paths this library builds: all in the diagnostics library; in the product one
@@ -1229,13 +1225,6 @@ bool path_built(int path) {
 uint32_t gather_small(const enet_hip_context* ctx) {
     return ctx->gather_small >= 0 && static_cast<uint32_t>(ctx->gather_small) < kGatherSmall
                ? static_cast<uint32_t>(ctx->gather_small) : kGatherSmall;
-}
-bool lin_path(const enet_hip_context* ctx) { return ctx->path == kLinPath || ctx->path == kLinPlainPath; }
-// the linear kernel's ablation (diagnostics: enet_hip_diag_ablation 2048 = no boundary
-// passes, + 4096 = no fold lookups either; wrong CRCs by design)
-int lin_abl(const enet_hip_context* ctx) { return (ctx->vr_abl & 1) ? ((ctx->vr_abl & 2) ? 3 : 1) : 0; }
-int lin_list(enet_hip_context* ctx, const VrBatches& bl, hipStream_t st) {
-    return lin_launch_list(ctx->num_cus, st, bl, ctx->d_lin, ctx->d_zero, lin_abl(ctx), ctx->path == kLinPath);
 }
 
 #ifdef ENET_HIP_DIAG
@@ -1400,12 +1389,6 @@ int launch_packets(enet_hip_context* ctx, int mode, const PacketArgs& pa, hipStr
     // length-binned records (its records instance: cfg3 at 4 lanes 59.4 us against the
     // lean kernel's 63.3 since the in-place edge masks, profiles/r03_cfg3_binned/;
     // the lean kernel on paths 13-16)
-    if (mode == 0 && !pa.meta4 && ctx->ablation == 0 && lin_path(ctx)) {
-        VrBatches bl{};
-        bl.count = 1;
-        bl.b[0] = VrBatch{pa.bytes, pa.off, pa.len, pa.out, pa.n, 0u};
-        return lin_list(ctx, bl, st);
-    }
     if (mode == 0 && (pa.lg == 2 || pa.lg == 3) && ctx->ablation == 0 && vring_path(ctx))
         return vring_launch(pa.lg, ctx->num_cus * vring_wgs(ctx, 1),
                             with_claim(ctx, pa.meta4 ? bin_variant(ctx) : vring_variant(ctx, false), st), st, pa, tb,
@@ -1506,10 +1489,8 @@ int enet_hip_context_create(int device, enet_hip_context** out) {
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_basis2), ht.basis2.size() * 4)))) break;
         if ((rc = herr(hipMemcpy(ctx->d_basis2, ht.basis2.data(), ht.basis2.size() * 4, hipMemcpyHostToDevice)))) break;
 #ifdef ENET_HIP_DIAG
-        // the linear-stream image and the dynamic-round claim words: diagnostics paths
-        // only (the product library builds neither kernel -- ADVICE r4)
-        if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_lin), ht.lin.size() * 4)))) break;
-        if ((rc = herr(hipMemcpy(ctx->d_lin, ht.lin.data(), ht.lin.size() * 4, hipMemcpyHostToDevice)))) break;
+        // the dynamic-round claim words: diagnostics paths only (the product library
+        // builds no dynamic-round kernel -- ADVICE r4)
         const size_t claim_bytes = static_cast<size_t>(kVrClaimLines) * kVrClaimWords * 4;
         if ((rc = herr(hipMalloc(reinterpret_cast<void**>(&ctx->d_rounds), claim_bytes)))) break;
         if ((rc = herr(hipMemset(ctx->d_rounds, 0, claim_bytes)))) break;
@@ -1518,9 +1499,6 @@ int enet_hip_context_create(int device, enet_hip_context** out) {
         if ((rc = herr(hipMemset(ctx->d_pairs, 0, pair_bytes)))) break;
 #endif
         if ((rc = vring_setup())) break;
-#ifdef ENET_HIP_DIAG
-        if ((rc = lin_setup())) break;
-#endif
 #ifdef ENET_HIP_DIAG
         if ((rc = setup_stream())) break;
         if ((rc = setup_vstream())) break;
@@ -1552,7 +1530,6 @@ int enet_hip_context_destroy(enet_hip_context* ctx) {
     (void)hipFree(ctx->d_basis);
     (void)hipFree(ctx->d_basis2);
     (void)hipFree(ctx->d_tz);
-    (void)hipFree(ctx->d_lin);
     (void)hipFree(ctx->d_rounds);
     (void)hipFree(ctx->d_pairs);
     pipeline_release(ctx);
@@ -1657,17 +1634,6 @@ int enet_hip_crc32_batch_list_device(enet_hip_context* ctx, const ENetHipBatch* 
         for (size_t b0 = 0; b0 < batchCount; b0 += kLeanMaxBatches) {
             const int rc = lean_launch_list(llg, ctx->num_cus, st, batches + b0,
                                             std::min<size_t>(batchCount - b0, kLeanMaxBatches), tb);
-            if (rc) return rc;
-        }
-        return 0;
-    }
-    if (ctx->ablation == 0 && lin_path(ctx)) {
-        for (size_t b0 = 0; b0 < batchCount; b0 += kVrMaxBatches) {
-            VrBatches bl{};
-            for (size_t b = b0; b < std::min(batchCount, b0 + kVrMaxBatches); ++b)
-                bl.b[bl.count++] = VrBatch{batches[b].bytes, batches[b].offsets, batches[b].lengths, batches[b].out,
-                                           static_cast<uint64_t>(batches[b].count), 0u};
-            const int rc = lin_list(ctx, bl, st);
             if (rc) return rc;
         }
         return 0;

@@ -1300,12 +1300,10 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     // loop head is reached only from a completed ring turn (no path with the drained
     // loads of the last turn in flight: tools/isa_inflight_check.py)
     mark(4);                                                 // (streaming starts)
-    for (;;) {
+    do {
         iteration(std::integral_constant<uint32_t, 0>{});
-        if (done) break;
-        iteration(std::integral_constant<uint32_t, 1>{});
-        if (done) break;
-    }
+        if (!done) iteration(std::integral_constant<uint32_t, 1>{});
+    } while (!done);
     trace_end();
 }
 
@@ -1339,7 +1337,17 @@ const void* vring_pick_v(bool trace, const VrVariant& v) {
 }
 // compact: BIN = 2 (two workgroups per CU).  (diagnostics: abl 2 = no fold lookups, 19 =
 // no masks, lookups or end corrections, + 64 = CRCs stored in record order, at 4 lanes)
-const void* vring_pick_bin(int lg, int dyn, int abl = 0, bool compact = false) {
+const void* vring_pick_bin(int lg, int dyn, int abl = 0, bool compact = false, bool trace = false) {
+#ifdef ENET_HIP_DIAG
+    // the per-wave timeline of the records instance (tools/bin_timeline.py)
+    if (trace) {
+        if (abl || dyn) return nullptr;
+        if (compact) return lg == 2 ? vring_fn<2, 1, 0, 0, 2>() : vring_fn<3, 1, 0, 0, 2>();
+        return lg == 2 ? vring_fn<2, 1, 0, 0, 1>() : vring_fn<3, 1, 0, 0, 1>();
+    }
+#else
+    if (trace) return nullptr;
+#endif
     if (abl == 0 && compact) return lg == 2 ? vring_fn<2, 0, 0, 0, 2>(dyn) : vring_fn<3, 0, 0, 0, 2>(dyn);
     if (abl == 0) return lg == 2 ? vring_fn<2, 0, 0, 0, 1>(dyn) : vring_fn<3, 0, 0, 0, 1>(dyn);
 #ifdef ENET_HIP_DIAG
@@ -1428,6 +1436,8 @@ int vring_setup() {
                 if ((rc = set(vring_pick_bin(lg, d, abl), kVrLdsBin))) return rc;
                 if ((rc = set(vring_pick_bin(lg, d, abl, true), kVrLdsBinC))) return rc;
             }
+            if ((rc = set(vring_pick_bin(lg, d, 0, false, true), kVrLdsBin))) return rc;
+            if ((rc = set(vring_pick_bin(lg, d, 0, true, true), kVrLdsBinC))) return rc;
             for (int t = 0; t < 2; ++t)
                 for (int nt = 0; nt < 2; ++nt)
                     for (int abl : kAbl)
@@ -1474,7 +1484,8 @@ int vring_launch_list(int lg, int max_wgs, const VrVariant& v, hipStream_t st, c
         grid &= ~1u;
         grid = std::max(grid, 1u);
     }
-    const void* fn = bin ? vring_pick_bin(lg, vring_dyn(w), w.abl, w.compact) : vring_pick(lg, trace != nullptr, w);
+    const void* fn = bin ? vring_pick_bin(lg, vring_dyn(w), w.abl, w.compact, trace != nullptr)
+                         : vring_pick(lg, trace != nullptr, w);
     if (!fn) return -static_cast<int>(hipErrorInvalidValue);   // a variant this library does not build
     // slots are 32-bit: a workgroup's slot count (rounds x 16) must fit
     if ((a.groups / (static_cast<uint64_t>(grid) * kVrW) + 3u) * kVrW > 0xFFFFFFF0ull)
@@ -1523,7 +1534,9 @@ int vring_launch(int lg, int max_wgs, const VrVariant& v, hipStream_t st, const 
     // binned records: the record array rides in the offsets field (BIN instance)
     bl.b[0] = pa.meta4 ? VrBatch{pa.bytes, reinterpret_cast<const uint64_t*>(pa.meta4), nullptr, pa.out, pa.n, 0u}
                        : VrBatch{pa.bytes, pa.off, pa.len, pa.out, pa.n, 0u};
-    return vring_launch_list(lg, max_wgs, v, st, bl, tb, basis2, pa.meta4 ? nullptr : pa.trace, pa.meta4 != nullptr);
+    // (records: the trace instance only in the diagnostics library, where enet_hip_diag_trace
+    // can set a trace buffer)
+    return vring_launch_list(lg, max_wgs, v, st, bl, tb, basis2, pa.trace, pa.meta4 != nullptr);
 }
 
 }  // namespace enethip

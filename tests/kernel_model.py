@@ -921,124 +921,3 @@ def vr_unstep_tz(reg: int, tz: int, tabs=None, small=None) -> int:
     for _ in range(tz & 7):
         reg = unstep_zero(reg)
     return reg
-
-
-# ---------------------------------------------------------------- linear-stream kernel
-# crc32_lin.hip (round 4): each wave streams the contiguous byte span of a unit of
-# consecutive packets (sorted, non-overlapping) through its LDS tiles, packet
-# boundaries or not.  Lane l folds super-block l (LIN_SB bytes = 4 blocks) of a tile
-# as one serial chain from zero: S[q] after q blocks, c = S[4].  Boundary passes,
-# one lane per packet, turn chain states into each packet's CRC:
-#   tb(B) = exactfold(block_q, m, S[q]) = reg(0, SB[0:s'])     (the prefix up to B)
-#   hb(B) = suffix_fold(block_q, m)     = reg(0, block_q[m:32]) (one 32-lookup pass
-#           gives both: byte k < m feeds tb through T_{m-1-k}, byte k >= m feeds hb)
-#   head  H = c ^ (hb ^ S[q+1]) x^(8 32(3-q)) ^ INITS[128-s']  = reg(~0, SB[s':128])
-#   Horner acc = acc x^(8 128) ^ c_X over the packet's full super-blocks
-#   tail  state = tb(e) ^ adv_m(acc x^(8 32 q)) (end not on a super-block boundary)
-#   one super-block: state = tb(e) ^ adv_L(tb(s)) ^ INITS[L]
-LIN_SB = 128
-LIN_TILE = 64 * LIN_SB
-
-
-def adv(v: int, n: int) -> int:
-    """reg(v, 0^n): n zero bytes through the register."""
-    for _ in range(n):
-        v = zstep(v)
-    return v
-
-
-def lin_exactfold(block: bytes, m: int, inj: int) -> int:
-    """reg(inj, block[0:m]) by position-exact slicing tables: byte k < m through
-    T_{m-1-k}, the register's bytes injected into the first four; for m < 4 the
-    register's unconsumed bytes remain shifted down (inj >> 8m)."""
-    acc = (inj >> (8 * m)) if m < 4 else 0
-    for k in range(m):
-        b = block[k] ^ (((inj >> (8 * k)) & 0xFF) if k < 4 else 0)
-        acc ^= TS[m - 1 - k][b]
-    return acc
-
-
-def lin_suffix_fold(block: bytes, m: int) -> int:
-    """reg(0, block[m:32]), i.e. the block with bytes < m zeroed (zero leading bytes
-    leave a zero register unchanged)."""
-    acc = 0
-    for k in range(m, 32):
-        acc ^= TS[31 - k][block[k]]
-    return acc
-
-
-def lin_adv_small(v: int, n: int) -> int:
-    """adv(v, n) for n < 128 as the kernel does it: n = 32a + b, the b zero bytes by
-    the slicing tables (lin_exactfold of zeros), then x^(256a) by a multiplier table."""
-    a, b = divmod(n, 32)
-    v = lin_exactfold(bytes(32), b, v)
-    return mulmod(v, x8n(32 * a)) if a else v
-
-
-LIN_X = {k: x8n(k) for k in (32, 64, 96, 128)}       # x^(8k): k zero bytes
-LIN_INITS = [adv(0xFFFFFFFF, n) for n in range(256)]
-
-
-def lin_unit(arena: bytes, offs, lens, base: int = 0):
-    """What crc32_lin_kernel computes for one unit: packets (offs[i], lens[i]) of
-    `arena`, sorted and non-overlapping; `base` = the arena's device address mod 128
-    (tiles start at the 128-byte line at or before the first packet).  Pieces (16 B)
-    wholly outside [first start, last end) read as zero, the others as the arena's
-    bytes -- the boundary passes must ignore what lies outside each packet.
-    Returns the wire CRCs."""
-    n = len(offs)
-    out = [0] * n
-    live = [i for i in range(n) if lens[i]]
-    if not live:
-        return out
-    first = offs[live[0]]
-    E = max(offs[i] + lens[i] for i in live)
-    A = ((base + first) & ~127) - base                     # arena index of tile 0
-    lo16 = ((base + first) & ~15) - base
-    ntiles = (E - A + LIN_TILE - 1) // LIN_TILE
-    region = bytearray(ntiles * LIN_TILE)
-    for p in range(0, len(region), 16):                    # the DMA: pieces, zero page outside
-        a = A + p
-        if a + 16 > lo16 and a < E:
-            chunk = arena[max(a, 0):a + 16]
-            region[p + (max(a, 0) - a):p + (max(a, 0) - a) + len(chunk)] = chunk
-    nsb = len(region) // LIN_SB
-    S = []
-    for X in range(nsb):                                   # the fold: per lane, one chain
-        st = [0]
-        for q in range(4):
-            blk = region[LIN_SB * X + 32 * q:LIN_SB * X + 32 * q + 32]
-            st.append(lin_exactfold(blk, 32, st[-1]))
-        S.append(st)
-
-    def bpass(B):                                          # boundary at region offset B
-        X, sp = divmod(B, LIN_SB)
-        q, m = divmod(sp, 32)
-        if X >= nsb:                                       # (the region's end)
-            return None, None, X, sp, q, m
-        blk = region[LIN_SB * X + 32 * q:LIN_SB * X + 32 * q + 32]
-        return lin_exactfold(blk, m, S[X][q]), lin_suffix_fold(blk, m), X, sp, q, m
-
-    for i in live:
-        s, e, L = offs[i] - A, offs[i] + lens[i] - A, lens[i]
-        tbs, hbs, Xs, sp, qs, ms = bpass(s)
-        tbe, _, Xe, ep, qe, me = bpass(e)
-        if ep == 0:                                        # end on a super-block boundary:
-            Xe, ep, qe, me = Xe - 1, LIN_SB, 3, 32         # last full SB = Xe - 1
-        if Xs == Xe:
-            if ep == LIN_SB:                               # head only
-                state = S[Xs][4] ^ mulmod(hbs ^ S[Xs][qs + 1], x8n(32 * (3 - qs))) ^ LIN_INITS[LIN_SB - sp]
-            else:
-                state = tbe ^ lin_adv_small(tbs, L) ^ LIN_INITS[L]
-        else:
-            acc = S[Xs][4] ^ mulmod(hbs ^ S[Xs][qs + 1], x8n(32 * (3 - qs))) ^ LIN_INITS[LIN_SB - sp]
-            last_full = Xe if ep == LIN_SB else Xe - 1
-            for X in range(Xs + 1, last_full + 1):
-                acc = mulmod(acc, LIN_X[128]) ^ S[X][4]
-            if ep == LIN_SB:
-                state = acc
-            else:
-                state = tbe ^ lin_exactfold(bytes(32), me, mulmod(acc, x8n(32 * qe)) if qe else acc)
-        out[i] = finalize(state)
-    return out
-

@@ -454,31 +454,3 @@ def test_gather_join_fold_small_matches_oracle(oracle_lib):
         for a, L in segs:
             reg = km.fold_small(reg, arena, a, L)
         assert km.finalize(reg) == oracle_lib.crc32(b"".join(arena[a:a + L] for a, L in segs))
-
-
-def test_lin_model_matches_oracle():
-    """The linear-stream kernel's arithmetic (kernel_model.lin_unit: packet-blind
-    super-block chains, boundary passes, heads, Horner, tails, one-super-block
-    packets) against the oracle on sorted units with gaps, empty and tiny packets,
-    packets across tiles, every base alignment mod 128."""
-    import random
-    import zlib
-    rng = random.Random(5)
-
-    def ref(b):
-        return int.from_bytes((zlib.crc32(b) & 0xFFFFFFFF).to_bytes(4, "little"), "big")
-
-    for trial in range(25):
-        n = rng.randint(1, 14)
-        lens = [rng.choice([0, 1, 2, 3, 4, 5, 31, 32, 33, 64, 127, 128, 129, 255, 256, 1200, rng.randint(1, 9000)])
-                for _ in range(n)]
-        gaps = [rng.choice([0, 0, 0, rng.randint(0, 300)]) for _ in range(n)]
-        off, p = [], rng.randint(0, 200)
-        for L, g in zip(lens, gaps):
-            p += g
-            off.append(p)
-            p += L
-        arena = bytes(rng.getrandbits(8) for _ in range(p + 300))
-        got = km.lin_unit(arena, off, lens, rng.randint(0, 127))
-        assert got == [ref(arena[o:o + L]) for o, L in zip(off, lens)], trial
-

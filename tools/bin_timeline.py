@@ -1,0 +1,123 @@
+#!/usr/bin/env python3
+"""Measurement only: where the cfg3 length-binned checksum spends its time.
+One call = bin kernel + records kernel (crc32_vring_kernel BIN = 1, 4 lanes, one workgroup
+per CU).  The diagnostics library's trace instance of the records kernel writes per-wave
+timestamps [start, metadata, table, barrier B, loop entry, end, HW_ID, groups]
+(enet_hip_diag_trace); the records themselves (the workspace after the call) give each
+group's stage count.  Splits the records kernel's span into
+  start  -- the kernel's first wave start to the waves' loop entry (metadata, table image);
+  steady -- the waves' loop time, per group and per stage (a CU runs 16 waves at once);
+  drain  -- the last wave's end against the median wave's end (imbalance).
+HIP events time the whole call and the records kernel's product instance alone beside it.
+    python tools/bin_timeline.py [reps=3]"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "enet-csharp_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import enethip  # noqa: E402
+from enethip import workloads  # noqa: E402
+
+
+def stages_of_groups(rec: np.ndarray, base_addr: int, lanes: int = 4, kpk: int = 16) -> np.ndarray:
+    """Per group of kpk records (length-binned order): its stage count, the wave maximum of
+    ceil(nb / lanes), nb = ceil((lz + L) / 32), as the records instance cuts windows: an
+    end on a 16-byte boundary gets an end-aligned window (lz = 32 ceil(L / 32) - L),
+    others start at the 64-byte boundary at or before the first byte."""
+    L = rec[:, 0].astype(np.int64)
+    off = rec[:, 1].astype(np.int64) | (rec[:, 2].astype(np.int64) << 32)
+    a = base_addr + off
+    ea = ((a + L) & 15) == 0
+    eb = (L + 31) // 32 * 32
+    lz = np.where(ea, eb - L, a & 63)
+    nb = np.where(L > 0, (lz + L + 31) // 32, 0)
+    st = np.maximum(1, (nb + lanes - 1) // lanes)
+    g = len(st) // kpk
+    return st[:g * kpk].reshape(g, kpk).max(axis=1)
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    b = workloads.cfg3()
+    dev = torch.device("cuda")
+    payload = torch.from_numpy(b.payload).to(dev)
+    off = torch.from_numpy(b.off.view(np.int64)).to(dev)
+    lens = torch.from_numpy(b.lens.view(np.int32)).to(dev)
+    out = torch.zeros(b.n, dtype=torch.int32, device=dev)
+    ctx = enethip.Context(0, 4, 1, diag=True)
+    ws = torch.zeros(ctx.binned_workspace_size(b.n), dtype=torch.uint8, device=dev)
+    h = torch.cuda.current_stream().cuda_stream
+    import oracle
+    exp = oracle.OracleLib().batch(b.payload, b.off, b.lens, threads=8)
+    nw = 256 * 16
+    tr = torch.zeros(nw * 8, dtype=torch.int64, device=dev)
+
+    def call():
+        ctx.crc32_batch_device_binned(payload, off, lens, b.n, out, ws, ws.numel(), h)
+
+    # the product instance (no trace) timed by HIP events: whole call
+    for _ in range(3):
+        call()
+    torch.cuda.synchronize()
+    assert (out.cpu().numpy().view(np.uint32) == exp).all(), "binned CRCs differ from the oracle"
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
+        call()
+    e1.record()
+    torch.cuda.synchronize()
+    call_us = e0.elapsed_time(e1) / 20 * 1e3
+    rec = ws[:16 * b.n].cpu().numpy().view(np.uint32).reshape(b.n, 4)
+    st = stages_of_groups(rec, payload.data_ptr())
+    ctx.diag_trace(tr)
+    for rep in range(reps):
+        tr.zero_()
+        call()
+        torch.cuda.synchronize()
+        assert (out.cpu().numpy().view(np.uint32) == exp).all(), "trace instance CRCs differ from the oracle"
+        t = tr.cpu().numpy().view(np.uint64).reshape(nw, 8)
+        rows = np.nonzero(t[:, 0] > 0)[0]
+        t = t[rows]
+        t0 = t[:, 0].min()
+        rel = lambda c: (t[:, c].astype(np.int64) - np.int64(t0)) / 100.0      # s_memrealtime: 100 MHz
+        start, meta, table, barrier, entry, end = (rel(c) for c in range(6))
+        groups = t[:, 7].astype(np.int64)
+        span = float(end.max())
+        loop = end - entry
+        tot_groups = int(groups.sum())
+        # per workgroup (16 waves = one CU's worth at one workgroup per CU): its loop time
+        wg = rows // 16
+        wg_loop = np.array([end[wg == g].max() - entry[wg == g].min() for g in np.unique(wg)])
+        wg_groups = np.array([groups[wg == g].sum() for g in np.unique(wg)])
+        mb = float(b.lens.astype(np.int64).sum()) / 1e6
+        print(json.dumps({
+            "rep": rep, "call_us_events": round(call_us, 2), "records_span_us": round(span, 2),
+            "waves": int(len(t)), "groups": tot_groups, "groups_expected": int(len(st)),
+            "stages_total": int(st.sum()), "stages_per_group_mean": round(float(st.mean()), 3),
+            "start_loop_entry_p50_max_us": [round(float(np.median(entry)), 2), round(float(entry.max()), 2)],
+            "start_parts_p50_us": {"metadata": round(float(np.median(meta)), 2),
+                                   "table": round(float(np.median(table)), 2),
+                                   "barrier_B": round(float(np.median(barrier)), 2)},
+            "end_p10_p50_p90_max_us": [round(float(np.percentile(end, q)), 2) for q in (10, 50, 90)] +
+                                      [round(float(end.max()), 2)],
+            "drain_us (max end - p50 end)": round(float(end.max() - np.median(end)), 2),
+            "wave_loop_us_p50": round(float(np.median(loop)), 2),
+            "wave_groups_min_p50_max": [int(groups.min()), int(np.median(groups)), int(groups.max())],
+            "cu_us_per_group (workgroup loop / its groups, p50)": round(float(np.median(wg_loop / wg_groups)), 4),
+            "cu_us_per_stage (p50 over workgroups)": round(float(np.median(wg_loop / wg_groups)) /
+                                                           float(st.mean()), 4),
+            "steady_rate_TBps (payload / (loop p50 x ...))": round(mb / float(np.median(wg_loop)) / 1e6, 3),
+            "payload_MB": round(mb, 1),
+        }), flush=True)
+    ctx.diag_trace(None)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -16,8 +16,8 @@ drains the socket for SECONDS per mode:
            (the reference's own loop, the CPU baseline);
   recv     enet_hip_udp_receive alone (the socket's own ceiling).
 UDP_BENCH_CALLS=1: instead, the cost of one receive call (gpu, callback) on a socket
-already holding k = 8, 32, 64 DGRAMs (the streaming rates above are bound by the sender
-thread: every mode but port keeps up with it).  UDP_BENCH_SEND_CALLS=1: the cost of one
+already holding k = 8, 32, 64 DGRAMs (UDP_BENCH_KS="8,...,256" for others; the streaming
+rates above are bound by the sender thread: every mode but port keeps up with it).  UDP_BENCH_SEND_CALLS=1: the cost of one
 stamp + send call (gpu, callback) over k = 8 ... 65536 DGRAMs of a pinned send batch.
 Send side: stamp + send of the whole batch, GPU (enet_hip_udp_stamp_send) against the
 callback stamp (enet_hip_stamp_callback + enet_hip_udp_send), a receiver thread
@@ -234,6 +234,9 @@ def call_latency(ctx, sb, mode, k, reps=300):
             t0 = time.perf_counter()
             if mode == "gpu":
                 n, lens, ok = ctx.udp_receive_verify(rx.fileno(), arena, STRIDE, k, sb.peers, timeout_ms=100)
+            elif mode == "recv":                                 # (the socket call alone)
+                n, lens, _, _ = enethip.udp_receive(rx.fileno(), arena, STRIDE, k, timeout_ms=100)
+                ok = np.ones(n, np.uint8)
             else:
                 n, lens, _, _ = enethip.udp_receive(rx.fileno(), arena, STRIDE, k, timeout_ms=100)
                 slot, conn, verdict = enethip.parse_headers(arena, STRIDE, lens, sb.peers)
@@ -311,8 +314,9 @@ def main():
     if os.environ.get("UDP_BENCH_CALLS"):            # per-call costs only
         if os.environ.get("UDP_BENCH_PATH"):          # (a kernel path for the GPU verify: 13 = lean)
             ctx.set_kernel_path(int(os.environ["UDP_BENCH_PATH"]))
-        for k in (8, 32, 64):
-            for mode in ("gpu", "callback"):
+        ks = tuple(int(x) for x in os.environ.get("UDP_BENCH_KS", "8,32,64").split(","))
+        for k in ks:
+            for mode in os.environ.get("UDP_BENCH_CALL_MODES", "gpu,callback").split(","):
                 print(json.dumps(call_latency(ctx, sb, mode, k)), flush=True)
         ctx.close()
         return
