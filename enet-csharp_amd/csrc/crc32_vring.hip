@@ -787,10 +787,21 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     // the arena front to back (the access shape of tools/streamprobe.hip's chunk
     // and sub-stream probes) instead of a round of 16 groups every wt groups
     const uint64_t gw = WK ? (ngroups_all + gridDim.x - 1u) / gridDim.x : 0u;
+    // Length-binned records (BIN) are rank-interleaved (length_bin_tiles: group q T + t =
+    // rank q of tile t, longest first), so round r's 16 groups of workgroup k are about one
+    // rank, 16 r + k / 16 at cfg3's 256 tiles: in the plain deal workgroup 0 took the
+    // longest rank of every round and the last workgroup the shortest, 1.5 x less work,
+    // and the records kernel's span ended 9 us after its median wave (tools/bin_timeline.py,
+    // profiles/r06_cfg3/).  Odd rounds therefore deal the workgroups in reverse order
+    // (k -> G - 1 - k): still a permutation of the round's groups, and every workgroup's
+    // rounds sum to about the same bytes (boustrophedon).
+    constexpr bool kSnake = BIN != 0;
     auto slot_group = [&](uint32_t sl) __attribute__((always_inline)) -> uint64_t {
         if constexpr (WK) return sl < gw ? static_cast<uint64_t>(blockIdx.x) * gw + sl : ~0ull;
         if (kDyn && sl >= kStatic * kVrW) return static_cast<uint64_t>(vr_round_chunk(sl / kVrW)) * kVrW + (sl & (kVrW - 1u));
-        return static_cast<uint64_t>(blockIdx.x) * kVrW + (sl & (kVrW - 1u)) + static_cast<uint64_t>(sl / kVrW) * wt;
+        const uint32_t r = sl / kVrW;
+        const uint64_t k = (kSnake && (r & 1u)) ? gridDim.x - 1u - blockIdx.x : blockIdx.x;
+        return k * kVrW + (sl & (kVrW - 1u)) + static_cast<uint64_t>(r) * wt;
     };
     // `it` moved to global group gg (its batch found from it.b on: a wave's groups
     // ascend -- with dynamic rounds too); false past the launch's last group

@@ -1,0 +1,192 @@
+// rx_small.hip -- receive verify (/root/reference/enet-csharp/ENet/c/protocol.cs:1052-1068)
+// of a small batch of DGRAMs read in place from a pinned receive arena over PCIe: the
+// kernel behind enet_hip_udp_receive_verify for the batch sizes ENet's receive loop
+// produces (at most 256 DGRAMs per enet_host_service pass, protocol.cs:1213).
+//
+// Why a separate kernel.  The vring verify kernel keeps one stage of a
+// packet in flight while it folds the previous one.  Over PCIe each of a 1200-byte
+// DGRAM's five stages then costs a dependent host-memory round trip, and its workgroup
+// first builds the 64 KiB table image from a DMA'd basis: 9.5 us of kernel for 8 DGRAMs
+// (profiles/r06_udp/).  Here every byte of the batch is requested at once:
+//   * one wave per DGRAM; its metadata (length, slot offset, connectID) rides in the
+//     kernel arguments, so the first host-memory request is the data itself;
+//   * lane e holds the 64-byte chunk that ENDS 64 e bytes before the DGRAM's end,
+//     [L - 64 e - 64, L - 64 e), as five aligned 16-byte loads issued together (bytes
+//     before the DGRAM read as zero), realigned in registers (the misalignment is the
+//     same in every lane);
+//   * the P = 1 table image is copied from HBM into LDS beside the data loads;
+//   * each lane folds its chunk from a zero register, two 32-byte slicing-by-32 blocks
+//     (fold_block, crc32_device.hpp: conflict-free XOR Latin square);
+//   * the 64 chunk CRCs are joined in six tree levels, lane e taking lane e + 2^j's value
+//     advanced over 64 * 2^j zero bytes (four byte-indexed lookups in the image's free
+//     columns 4 j + b, tables built on the host): reg(0, M) = sum_e c_e x^(512 e);
+//   * leading zero bytes do not change reg(0, .), and packet.cs:144's initial register
+//     0xFFFFFFFF equals XORing 0xFF into the message's first four bytes (applied after
+//     the slot substitution, as the reference checksums the substituted DGRAM).
+// Tested through the socket pipeline against the oracle (tests/test_gpu_harness.py:
+// every length 6..4096 and both slot offsets, corrupted DGRAMs, the arena's last byte).
+#include <hip/hip_runtime.h>
+
+#include "crc32_device.hpp"
+#include "crc32_math.hpp"
+#include "rx_small.hpp"
+
+namespace enethip {
+
+constexpr int kRxWaves = 8;                      // DGRAMs (waves) per workgroup
+
+struct RxSmallArgs {
+    const uint8_t* arena;
+    uint64_t stride;
+    uint8_t* ok;
+    uint32_t* computed;
+    const uint32_t* image;
+    uint32_t n;
+    uint32_t pad;
+    uint32_t meta[kRxSmallMax][2];               // {len | slotOff << 16, connectID}
+};
+static_assert(sizeof(RxSmallArgs) <= 4096, "kernel arguments");
+
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4_rw;
+
+__global__ void __launch_bounds__(64 * kRxWaves) rx_small_verify_kernel(RxSmallArgs a) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t i = blockIdx.x * kRxWaves + (threadIdx.x >> 6);        // this wave's DGRAM
+    const bool live = i < a.n;
+    const uint32_t m0 = live ? a.meta[i][0] : 0u, conn = live ? a.meta[i][1] : 0u;
+    const int32_t L = static_cast<int32_t>(m0 & 0xFFFFu), so = static_cast<int32_t>(m0 >> 16);
+    const bool has_slot = L >= 4 && so <= L - 4;                          // (L = 0: dropped, no slot)
+    // 1. the chunk's granules, all requested before anything waits
+    const uint64_t base = reinterpret_cast<uint64_t>(a.arena) + static_cast<uint64_t>(i) * a.stride;
+    const int32_t s = L - 64 * static_cast<int32_t>(lane) - 64;          // chunk start, message bytes
+    const uint64_t A = base + static_cast<uint64_t>(static_cast<int64_t>(s));
+    const uint32_t o = static_cast<uint32_t>(A) & 15u;                    // (the same in every lane)
+    const int32_t gm = s - static_cast<int32_t>(o);                       // first granule, message bytes
+    // (a chunk off a 16-byte boundary spans five granules; the fifth is the next lane's
+    // first, taken from it below instead of being requested twice -- except lane 0's,
+    // which holds the DGRAM's last bytes)
+    u32x4 G[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const int32_t g = gm + 16 * k;
+        const bool want = g + 16 > 0 && g < L && (k < 4 || (lane == 0u && o != 0u));
+        G[k] = want ? ldg16_addr(A - o + 16u * k) : u32x4{0u, 0u, 0u, 0u};
+    }
+    // 2. the P = 1 image into LDS (beside the loads above)
+    const u32x4* img = reinterpret_cast<const u32x4*>(a.image);
+#pragma unroll
+    for (uint32_t r = 0; r < static_cast<uint32_t>(kLdsTableBytes / 16 / (64 * kRxWaves)); ++r) {
+        const uint32_t q = r * 64u * kRxWaves + threadIdx.x;
+        *reinterpret_cast<lds_u32x4_rw*>(static_cast<uintptr_t>(16u * q)) = img[q];
+    }
+    __syncthreads();
+    if (!live) return;                                                    // (after the barrier)
+    if (o != 0u) {                                                        // (wave-uniform)
+        const uint32_t u0 = static_cast<uint32_t>(__shfl_up(static_cast<int>(G[0].x), 1u, 64));
+        const uint32_t u1 = static_cast<uint32_t>(__shfl_up(static_cast<int>(G[0].y), 1u, 64));
+        const uint32_t u2 = static_cast<uint32_t>(__shfl_up(static_cast<int>(G[0].z), 1u, 64));
+        const uint32_t u3 = static_cast<uint32_t>(__shfl_up(static_cast<int>(G[0].w), 1u, 64));
+        if (lane != 0u) G[4] = u32x4{u0, u1, u2, u3};
+    }
+    // 3. realign: chunk dword q = bytes [o + 4 q, o + 4 q + 4) of the 80 loaded bytes
+    const uint32_t w[20] = {G[0].x, G[0].y, G[0].z, G[0].w, G[1].x, G[1].y, G[1].z, G[1].w,
+                            G[2].x, G[2].y, G[2].z, G[2].w, G[3].x, G[3].y, G[3].z, G[3].w,
+                            G[4].x, G[4].y, G[4].z, G[4].w};
+    uint32_t c[16];
+    const uint32_t sh = o & 3u;
+    switch (o >> 2) {                                                     // (wave-uniform)
+#define RX_ALIGN(D)                                                                      \
+    case D:                                                                              \
+        _Pragma("unroll") for (int q = 0; q < 16; ++q) c[q] = __builtin_amdgcn_alignbyte(w[q + D + 1], w[q + D], sh); \
+        break;
+        RX_ALIGN(0)
+        RX_ALIGN(1)
+        RX_ALIGN(2)
+        RX_ALIGN(3)
+#undef RX_ALIGN
+    }
+    // 4. the bytes before the DGRAM (zero), the slot (connectID in, its bytes out into
+    //    `desired`, protocol.cs:1058-1066) and packet.cs:144's initial register (the
+    //    first four bytes inverted): only the lane(s) whose chunk starts before byte
+    //    max(4, so + 4)
+    uint32_t desired = 0;
+    if (s < (has_slot ? so + 4 : 4)) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int32_t b0 = s + 4 * q;                                 // message index of the dword's byte 0
+            uint32_t v = c[q];
+            if (b0 < 0) v = b0 <= -4 ? 0u : v & (0xFFFFFFFFu << (8 * -b0));
+            const int32_t d = so - b0;                                    // the slot's start, relative
+            if (has_slot && d > -4 && d < 4) {
+                uint32_t M, C;
+                if (d >= 0) {
+                    M = 0xFFFFFFFFu << (8 * d);
+                    C = conn << (8 * d);
+                    desired |= v >> (8 * d);
+                } else {
+                    M = 0xFFFFFFFFu >> (-8 * d);
+                    C = conn >> (-8 * d);
+                    desired |= (v & M) << (-8 * d);
+                }
+                v = (v & ~M) | (C & M);
+            }
+            if (b0 > -4 && b0 < 4) v ^= b0 >= 0 ? 0xFFFFFFFFu >> (8 * b0) : 0xFFFFFFFFu << (8 * -b0);
+            c[q] = v;
+        }
+    }
+    desired = wave_or_u(desired);
+    // 5. the chunk's register from zero: two 32-byte blocks
+    const LaneSched sc = make_sched(lane);
+    uint32_t reg = fold_block(0u, u32x4{c[0], c[1], c[2], c[3]}, u32x4{c[4], c[5], c[6], c[7]}, sc);
+    reg = fold_block(reg, u32x4{c[8], c[9], c[10], c[11]}, u32x4{c[12], c[13], c[14], c[15]}, sc);
+    // 6. the tree: lane e += advance over 64 * 2^j zero bytes of lane e + 2^j
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const uint32_t dl = 1u << j;
+        uint32_t p = static_cast<uint32_t>(__shfl_down(static_cast<int>(reg), dl, 64));
+        p = lane + dl < 64u ? p : 0u;
+        uint32_t x = 0;
+#pragma unroll
+        for (uint32_t b = 0; b < 4; ++b)
+            x ^= *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(256u * ((p >> (8 * b)) & 0xFFu) +
+                                                                    free_col(kRxAdvCol + 4u * j + b)));
+        reg ^= x;
+    }
+    if (lane == 0) {
+        const uint32_t comp = has_slot ? finalize(reg) : 0u;              // packet.cs:159
+        a.ok[i] = (has_slot && comp == desired) ? 1 : 0;                  // protocol.cs:1066-1068
+        if (a.computed) a.computed[i] = comp;
+    }
+}
+
+int rx_small_setup() {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(rx_small_verify_kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTableBytes);
+    return e == hipSuccess ? 0 : -static_cast<int>(e);
+}
+
+int rx_small_verify(hipStream_t st, const uint8_t* arena, uint64_t stride, const uint32_t* len,
+                    const uint32_t* slotOff, const uint32_t* connectId, size_t count, uint8_t* ok, uint32_t* computed,
+                    const uint32_t* image1) {
+    if (count == 0) return 0;
+    if (count > static_cast<size_t>(kRxSmallMax) || (stride & 15u) || !arena || !ok || !image1) return 1;
+    RxSmallArgs a{};
+    a.arena = arena;
+    a.stride = stride;
+    a.ok = ok;
+    a.computed = computed;
+    a.image = image1;
+    a.n = static_cast<uint32_t>(count);
+    const uint64_t lmax = stride < kRxSmallMaxLen ? stride : kRxSmallMaxLen;
+    for (size_t k = 0; k < count; ++k) {
+        if (len[k] > lmax || slotOff[k] > 0xFFFFu) return 1;
+        a.meta[k][0] = len[k] | (slotOff[k] << 16);
+        a.meta[k][1] = connectId[k];
+    }
+    const unsigned grid = static_cast<unsigned>((count + kRxWaves - 1) / kRxWaves);
+    hipLaunchKernelGGL(rx_small_verify_kernel, dim3(grid), dim3(64 * kRxWaves), kLdsTableBytes, st, a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : -static_cast<int>(e);
+}
+
+}  // namespace enethip

@@ -658,13 +658,16 @@ def vring_packet(arena: bytes, addr: int, L: int, P: int, lane_base: int = 0, ro
 
 
 # ---------------------------------------------------------------- vring slots
-def vring_slot_group(blk: int, sl: int, wt: int, W: int = 16) -> int:
+def vring_slot_group(blk: int, sl: int, wt: int, W: int = 16, grid: int = 0, snake: bool = False) -> int:
     """crc32_vring.hip slot_group: workgroup blk's slot sl is global group
-    16 blk + sl % 16 + (sl / 16) wt (wt = the launch's waves)."""
-    return W * blk + (sl % W) + (sl // W) * wt
+    16 blk + sl % 16 + (sl / 16) wt (wt = the launch's waves); snake (the records
+    instance, round 6): odd rounds deal the workgroups in reverse, blk -> grid - 1 - blk."""
+    r = sl // W
+    k = grid - 1 - blk if (snake and r & 1) else blk
+    return W * k + (sl % W) + r * wt
 
 
-def vring_dynamic_deal(batch_groups, grid: int, rng, W: int = 16):
+def vring_dynamic_deal(batch_groups, grid: int, rng, W: int = 16, snake: bool = False):
     """Simulate one launch of the vring kernel's dynamic slots: every wave takes
     slots wave and 16 + wave, then slots from its workgroup's counter (starting at
     32) in a random interleaving of the workgroup's waves, until a slot maps past
@@ -696,7 +699,7 @@ def vring_dynamic_deal(batch_groups, grid: int, rng, W: int = 16):
                 sl = ctr
                 ctr += 1
             c[1] += 1
-            gg = vring_slot_group(blk, sl, wt, W)
+            gg = vring_slot_group(blk, sl, wt, W, grid, snake)
             if gg >= total:
                 c[2] = False
                 continue

@@ -562,3 +562,63 @@ def test_receive_verify_dgram_ending_on_the_arena(ctx, oracle_lib):  # noqa: F81
         free_pinned(p)
         rx.close()
         tx.close()
+
+
+def _enet_dgram(oracle_lib, rng, L, peer, sent_time, conn):
+    """An ENet DGRAM of L bytes as a host sends it: big-endian peer word (SENT_TIME flag:
+    a 4-byte header), checksum slot after the header holding the CRC taken with the slot
+    set to the peer's connectID (protocol.cs:1690-1698)."""
+    hs = 4 if sent_time else 2
+    b = bytearray(rng.integers(0, 256, size=L, dtype=np.uint8).tobytes())
+    b[0:2] = ((peer & 0x0FFF) | (0x8000 if sent_time else 0)).to_bytes(2, "big")
+    b[hs:hs + 4] = int(conn).to_bytes(4, "little")
+    b[hs:hs + 4] = int(oracle_lib.crc32(bytes(b))).to_bytes(4, "little")
+    return bytes(b)
+
+
+def test_receive_verify_every_length(ctx, oracle_lib):  # noqa: F811
+    """The receive verify of ENet-sized calls (at most 256 DGRAMs, which csrc/rx_small.hip
+    serves on a pinned arena) over every DGRAM length 6..4096, both header sizes (SENT_TIME
+    or not), peers with connectIDs and peer 0xFFF, one DGRAM in nine corrupted in one byte:
+    keep mask equal to the oracle's (expected_keep restates the header stage) in every call,
+    and every intact DGRAM kept."""
+    rng = np.random.default_rng(102)
+    peers = rng.integers(1, 1 << 32, size=5, dtype=np.uint64).astype(np.uint32)
+    dgrams, intact = [], []
+    for L in range(6, STRIDE + 1):
+        for sent_time in ((False, True) if L >= 8 else (False,)):
+            if (L + sent_time) % 3:                              # (two thirds of the pairs: ~5400 DGRAMs)
+                continue
+            p = int(rng.integers(0, 6))
+            peer = 0x0FFF if p == 5 else p
+            dg = bytearray(_enet_dgram(oracle_lib, rng, L, peer, sent_time, 0 if peer == 0x0FFF else peers[peer]))
+            bad = rng.random() < 1 / 9
+            if bad:
+                k = int(rng.integers(2, L))
+                dg[k] ^= 1 << int(rng.integers(0, 8))
+            dgrams.append(bytes(dg))
+            intact.append(not bad)
+    rx, tx, port = sockets()
+    arena, p = pinned(STRIDE * 256)
+    try:
+        got, keep_all = 0, []
+        for a in range(0, len(dgrams), 256):
+            part = dgrams[a:a + 256]
+            for dg in part:
+                tx.sendto(dg, ("127.0.0.1", port))
+            k = 0
+            while k < len(part):
+                n, lens, ok = ctx.udp_receive_verify(rx.fileno(), arena, STRIDE, 256, peers, timeout_ms=2000)
+                assert n > 0
+                exp = expected_keep(oracle_lib, arena, STRIDE, lens, peers)
+                assert (ok == exp).all(), (a, k, np.nonzero(ok != exp)[0][:10], lens[np.nonzero(ok != exp)[0][:10]])
+                keep_all.append(ok.copy())
+                k += n
+            got += k
+        keep = np.concatenate(keep_all)
+        assert got == len(dgrams)
+        assert keep.sum() == sum(intact)                        # (corrupting a peer word may drop it too)
+    finally:
+        free_pinned(p)
+        rx.close()
+        tx.close()

@@ -291,18 +291,21 @@ def test_vring_tail_first_model_matches_oracle(P):
         assert got == exp, (a, L, P, gs, hex(got), hex(exp))
 
 
+@pytest.mark.parametrize("snake", [False, True])
 @pytest.mark.parametrize("batch_groups,grid", [([4096] * 5, 512), ([1], 1), ([0, 3, 0, 17], 2),
-                                               ([5000, 1, 70, 2, 800], 300), ([33] * 48, 7)])
-def test_vring_dynamic_slots_cover_every_group_once(batch_groups, grid):
+                                               ([5000, 1, 70, 2, 800], 300), ([33] * 48, 7), ([16384], 256),
+                                               ([16383], 256), ([1000], 17)])
+def test_vring_dynamic_slots_cover_every_group_once(batch_groups, grid, snake):
     """The vring kernel's dynamic slots (crc32_vring.hip slot_group / take / locate):
     whatever order a workgroup's waves take slots in, every group of every batch is
-    processed exactly once, in its own batch, and each wave's groups ascend."""
+    processed exactly once, in its own batch, and each wave's groups ascend -- with the
+    records instance's reversed odd rounds (snake) too, partial last rounds included."""
     import random
     from kernel_model import vring_dynamic_deal
     rng = random.Random(sum(batch_groups) + grid)
     nonempty = [n for n in batch_groups if n]                 # (the host drops empty batches)
     grid = max(1, min(grid, (sum(nonempty) + 15) // 16))      # (the host's grid rule)
-    seen, per_wave, total = vring_dynamic_deal(nonempty, grid, rng)
+    seen, per_wave, total = vring_dynamic_deal(nonempty, grid, rng, snake=snake)
     assert sorted(seen) == list(range(total))
     g0 = [sum(nonempty[:b]) for b in range(len(nonempty))]
     for gg, (b, local) in seen.items():
@@ -454,3 +457,25 @@ def test_gather_join_fold_small_matches_oracle(oracle_lib):
         for a, L in segs:
             reg = km.fold_small(reg, arena, a, L)
         assert km.finalize(reg) == oracle_lib.crc32(b"".join(arena[a:a + L] for a, L in segs))
+
+
+def test_snake_deal_balances_binned_ranks():
+    """Why the records instance reverses odd rounds: cfg3's rank-interleaved records (256
+    tiles, 16-record groups, rank q of 64 ~ longest first) give workgroup k about rank
+    16 r + k / 16 in round r.  The plain deal hands workgroup 0 the longest rank of every
+    round (1.5 x the last workgroup's bytes); reversed odd rounds even the sums out."""
+    from kernel_model import vring_slot_group
+    G, W, T, ranks = 256, 16, 256, 64
+    wt = G * W
+    length = lambda q: 1400 - q * (1336 / (ranks - 1))           # rank q's typical length
+    def work(snake):
+        per = []
+        for k in range(G):
+            tot = 0.0
+            for sl in range(ranks * T // G):                      # every slot of the workgroup
+                g = vring_slot_group(k, sl, wt, W, G, snake)
+                tot += length(g // T)
+            per.append(tot)
+        return max(per) / min(per)
+    assert work(False) > 1.4
+    assert work(True) < 1.02
