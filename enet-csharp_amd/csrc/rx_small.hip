@@ -51,8 +51,17 @@ typedef __attribute__((address_space(3))) u32x4 lds_u32x4_rw;
 
 __global__ void __launch_bounds__(64 * kRxWaves) rx_small_verify_kernel(RxSmallArgs a) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t i = blockIdx.x * kRxWaves + (threadIdx.x >> 6);        // this wave's DGRAM
+    // this wave's DGRAM (readfirstlane: wave-uniform, so its metadata comes by scalar loads
+    // from the kernel arguments, not by a vector load the data loads would wait behind)
+    const uint32_t i = blockIdx.x * kRxWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const bool live = i < a.n;
+    // the P = 1 image first: its loads hit L2 and are older than the data loads below, so
+    // its LDS stores wait only for them while the host-memory loads are still in flight
+    const u32x4* img = reinterpret_cast<const u32x4*>(a.image);
+    constexpr uint32_t kImgRounds = kLdsTableBytes / 16 / (64 * kRxWaves);
+    u32x4 T[kImgRounds];
+#pragma unroll
+    for (uint32_t r = 0; r < kImgRounds; ++r) T[r] = img[r * 64u * kRxWaves + threadIdx.x];
     const uint32_t m0 = live ? a.meta[i][0] : 0u, conn = live ? a.meta[i][1] : 0u;
     const int32_t L = static_cast<int32_t>(m0 & 0xFFFFu), so = static_cast<int32_t>(m0 >> 16);
     const bool has_slot = L >= 4 && so <= L - 4;                          // (L = 0: dropped, no slot)
@@ -65,22 +74,26 @@ __global__ void __launch_bounds__(64 * kRxWaves) rx_small_verify_kernel(RxSmallA
     // (a chunk off a 16-byte boundary spans five granules; the fifth is the next lane's
     // first, taken from it below instead of being requested twice -- except lane 0's,
     // which holds the DGRAM's last bytes)
+    // (every lane issues all five loads -- a granule it does not need reads the image instead,
+    // an L2 hit -- so the count of loads behind the image's is fixed and its LDS stores need
+    // not wait for host memory)
     u32x4 G[5];
+    bool want[5];
+    const uint64_t spare = reinterpret_cast<uint64_t>(a.image) + 16u * lane;
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
         const int32_t g = gm + 16 * k;
-        const bool want = g + 16 > 0 && g < L && (k < 4 || (lane == 0u && o != 0u));
-        G[k] = want ? ldg16_addr(A - o + 16u * k) : u32x4{0u, 0u, 0u, 0u};
+        want[k] = live && g + 16 > 0 && g < L && (k < 4 || (lane == 0u && o != 0u));
+        G[k] = ldg16_addr(want[k] ? A - o + 16u * k : spare);
     }
-    // 2. the P = 1 image into LDS (beside the loads above)
-    const u32x4* img = reinterpret_cast<const u32x4*>(a.image);
+    // 2. the P = 1 image into LDS (beside the data loads above)
 #pragma unroll
-    for (uint32_t r = 0; r < static_cast<uint32_t>(kLdsTableBytes / 16 / (64 * kRxWaves)); ++r) {
-        const uint32_t q = r * 64u * kRxWaves + threadIdx.x;
-        *reinterpret_cast<lds_u32x4_rw*>(static_cast<uintptr_t>(16u * q)) = img[q];
-    }
+    for (uint32_t r = 0; r < kImgRounds; ++r)
+        *reinterpret_cast<lds_u32x4_rw*>(static_cast<uintptr_t>(16u * (r * 64u * kRxWaves + threadIdx.x))) = T[r];
     __syncthreads();
     if (!live) return;                                                    // (after the barrier)
+#pragma unroll
+    for (int k = 0; k < 5; ++k) G[k] = want[k] ? G[k] : u32x4{0u, 0u, 0u, 0u};
     if (o != 0u) {                                                        // (wave-uniform)
         const uint32_t u0 = static_cast<uint32_t>(__shfl_up(static_cast<int>(G[0].x), 1u, 64));
         const uint32_t u1 = static_cast<uint32_t>(__shfl_up(static_cast<int>(G[0].y), 1u, 64));
