@@ -32,7 +32,6 @@
 #include "crc32_math.hpp"
 #include "crc32_lean.hpp"
 #include "crc32_vring.hpp"
-#include "rx_small.hpp"
 #include "crc32_stream_common.hpp"
 #include "context.hpp"
 #include "enet_hip.h"
@@ -1022,13 +1021,6 @@ struct HostTables {
                 for (uint32_t j = 0; j < 256; ++j) img[(j * 256 + col_byte(t)) / 4] = row[j];
                 for (uint32_t j = 0; j < 256; ++j) row[j] = sarwate_step(row[j], 0);
             }
-            if (kImageP[im] == 1)                               // rx_small.hip's chunk-advance tables
-                for (int j = 0; j < kRxAdvLevels; ++j) {
-                    const uint32_t xa = x8n_modp(64ull << j);
-                    for (uint32_t b = 0; b < 4; ++b)
-                        for (uint32_t v = 0; v < 256; ++v)
-                            img[(256u * v + free_col(kRxAdvCol + 4u * j + b)) / 4] = gf2_mulmod(v << (8 * b), xa);
-                }
             for (uint32_t k = 1; k < std::min<uint32_t>(kImageP[im], kCorrLanes); ++k)
                 for (uint32_t b = 0; b < 4; ++b)
                     for (uint32_t v = 0; v < 256; ++v)
@@ -1507,7 +1499,6 @@ int enet_hip_context_create(int device, enet_hip_context** out) {
         if ((rc = herr(hipMemset(ctx->d_pairs, 0, pair_bytes)))) break;
 #endif
         if ((rc = vring_setup())) break;
-        if ((rc = rx_small_setup())) break;
 #ifdef ENET_HIP_DIAG
         if ((rc = setup_stream())) break;
         if ((rc = setup_vstream())) break;

@@ -30,7 +30,6 @@
 
 #include "context.hpp"
 #include "enet_hip.h"
-#include "rx_small.hpp"
 
 namespace enethip {
 
@@ -426,18 +425,6 @@ static int rx_stage(enet_hip_context* ctx, int slot, uint8_t* arena, size_t stri
         for (size_t i = 0; i < n; ++i) {
             h_off[i] = i * stride;
             h_len[i] = h_verdict[i] == ENET_HIP_DGRAM_CHECKSUM ? lengths[i] : 0u;   // header-stage drops: no slot
-        }
-        // ENet-sized batches (at most 256 DGRAMs of at most 4096 B, the default path):
-        // rx_small.hip requests every byte at once, metadata in its kernel arguments
-        // (kernel path 17 keeps the vring verify below: A/B in tools/udp_bench.py)
-        if (ctx->path == 0) {
-            rc = rx_small_verify(st, zc, stride, h_len, h_slot, h_conn, n, zs + ho + 3 * hl + hv, nullptr,
-                                 ctx->d_image);
-            if (rc < 0) return rc;
-            if (rc == 0) {
-                ctx->rx_pending[slot] = true;
-                return 0;
-            }
         }
         if ((rc = enet_hip_verify_batch_device(ctx, zc, reinterpret_cast<uint64_t*>(zs), reinterpret_cast<uint32_t*>(zs + ho),
                                                reinterpret_cast<uint32_t*>(zs + ho + hl),

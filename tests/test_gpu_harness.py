@@ -577,11 +577,11 @@ def _enet_dgram(oracle_lib, rng, L, peer, sent_time, conn):
 
 
 def test_receive_verify_every_length(ctx, oracle_lib):  # noqa: F811
-    """The receive verify of ENet-sized calls (at most 256 DGRAMs, which csrc/rx_small.hip
-    serves on a pinned arena) over every DGRAM length 6..4096, both header sizes (SENT_TIME
-    or not), peers with connectIDs and peer 0xFFF, one DGRAM in nine corrupted in one byte:
-    keep mask equal to the oracle's (expected_keep restates the header stage) in every call,
-    and every intact DGRAM kept."""
+    """The receive verify of ENet-sized calls (at most 256 DGRAMs, read in place from a
+    pinned arena) over every DGRAM length 6..4096, both header sizes (SENT_TIME or not),
+    peers with connectIDs and peer 0xFFF, one DGRAM in nine corrupted in one byte: keep mask
+    equal to the oracle's (expected_keep restates the header stage) in every call, and every
+    intact DGRAM kept."""
     rng = np.random.default_rng(102)
     peers = rng.integers(1, 1 << 32, size=5, dtype=np.uint64).astype(np.uint32)
     dgrams, intact = [], []
