@@ -147,6 +147,7 @@ class GpuEngine:
         torch.cuda.set_device(device)
         self.torch = torch
         self.ctx = enethip.Context(device, lanes, wgs, diag=diag)
+        self.num_cus = torch.cuda.get_device_properties(device).multi_processor_count
         self.stream = torch.cuda.Stream()          # dedicated stream: handle != 0
         self.h = self.stream.cuda_stream
         self.streams = [self.stream]
@@ -403,10 +404,12 @@ PRODUCT_PATHS = (0, 13, 17)                # built in libenethip.so (the rest: l
 PRODUCT_LANES = (0, 4, 8)                  # lanes per packet libenethip.so takes (the rest: diagnostics)
 
 
-def kernel_name(args, list_launch: bool = False) -> str:
+def kernel_name(args, list_launch: bool = False, local_tiles: bool = False) -> str:
     """The dominant kernel of the measured entry point (as rocprofv3 names it:
     crc32_vring_kernel<LG, TR, NT, ABL, BIN, WK, ROT, VF, DYN>; DYN = 1 / 2, the chip-wide
-    / pair rounds, when the diagnostics ablation 524288 / 8388608 selects them)."""
+    / pair rounds, when the diagnostics ablation 524288 / 8388608 selects them).
+    local_tiles: the binned batch fits one tile per workgroup, so the default path runs
+    the one-launch local-tile records instance (BIN = 3)."""
     path = getattr(args, "path", 0)
     if list_launch and path == 13 and args.lanes in (0, 4, 8) and not args.binned:
         # batch lists: the lean kernel's list instance, 8 lanes per packet unless set
@@ -416,6 +419,8 @@ def kernel_name(args, list_launch: bool = False) -> str:
     if path and path not in (17, 18, 21):
         return f"kernel path {path}"
     dyn = 2 if (args.ablate & 8388608) else 1 if (args.ablate & 524288) else 0   # (pair / chip-wide rounds)
+    if args.binned and local_tiles and path == 0 and args.ablate == 0 and lg is not None:
+        return f"crc32_vring_kernel<{lg}, 0, 0, 0, 3, 0, 0, 0, 0>"
     if args.binned:
         dyn = 0 if dyn == 2 else dyn                          # (no pair rounds for the records instance)
         abl = (args.ablate >> 11) & 255
@@ -603,6 +608,11 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:    # (the CPU baseline: rank 0 at N = 1 only)
         cpu = (cpu_factory or cpu_baseline)(batches[0], args.cpu_seconds, args.cpu_threads)
 
+    # the binned entry's one-launch form: the batch fits one tile of <= 1024 packets per
+    # workgroup (crc32_kernels.hip enet_hip_crc32_batch_device_binned)
+    wgs_eff = min(args.wgs, 2) if args.wgs >= 1 else 2       # (the local tiles' default: two per CU)
+    local_tiles = (args.binned and args.path == 0 and args.ablate == 0 and
+                   batches[0].n <= 1024 * getattr(eng, "num_cus", 0) * wgs_eff)
     if rank == 0:
         import enethip
         traffic = load_traffic(args.config, args.binned, enethip.library_sha256(diag))
@@ -637,7 +647,7 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
                 "entry": ("enet_hip_crc32_batch_device_binned" if args.binned else
                           "enet_hip_crc32_batch_list_device" if per_launch_steps > 1 else
                           "enet_hip_crc32_batch_device"),
-                "workgroups_per_cu": args.wgs or f"default ({2 if per_launch_steps > 1 else 1})",
+                "workgroups_per_cu": args.wgs or f"default ({2 if per_launch_steps > 1 or local_tiles else 1})",
                 "launch": args.launch,
                 "kernel_path": args.path,
                 **({"ablation": args.ablate, "note": "ABLATION: wrong CRCs by design"} if args.ablate else {}),
@@ -655,7 +665,7 @@ def main(argv=None, engine_factory=None, cpu_factory=None):
                                    f"profiles/traffic_{args.config}{'_binned' if args.binned else ''}.json "
                                    f"(FETCH_SIZE pass of library sha256 {traffic['library_sha256'][:12]}, "
                                    f"the build this run loaded)"),
-                "kernel": kernel_name(args, per_launch_steps > 1),
+                "kernel": kernel_name(args, per_launch_steps > 1, local_tiles),
                 "kernel_ms": round(r_ms, 5),
                 "kernel_ms_timing": f"HIP events around {nk} serial launches on the launch stream",
                 "kernel_ms_bracketed_median": round(k_ms, 5),

@@ -1685,6 +1685,19 @@ int enet_hip_crc32_batch_device_binned(enet_hip_context* ctx, const uint8_t* byt
     // (cfg3: 3160-3217 GiB/s at 4 lanes against 2495 at 8, profiles/r01e_*, r01f_*)
     pa.lg = static_cast<uint32_t>(log2i(ctx->lanes_per_packet > 0 ? ctx->lanes_per_packet : 4));
     pa.out = out;
+    // default path: one launch -- each workgroup orders its own tile of at most 1024
+    // packets in its prologue (vring_launch_local) -- when the batch fits one tile per
+    // workgroup (cfg3: 262144 packets); larger batches, path 17 and the diagnostics
+    // ablations: the bin kernel, then the records instance
+    // (two workgroups per CU unless set: cfg3 49.5-49.9 us against 50.7-51.0 at one, and
+    // against 51.3-51.5 for the two-launch form at two, one box, profiles/r06_local/)
+    const int wgs = ctx->wgs_per_cu >= 1 ? std::min(ctx->wgs_per_cu, 2) : 2;
+    if (ctx->path == 0 && (pa.lg == 2 || pa.lg == 3) && ctx->ablation == 0 && ctx->vr_abl == 0 &&
+        !ctx->bin_identity && !ctx->vr_dynamic &&
+        count <= static_cast<uint64_t>(kVrLocalTile) * static_cast<uint64_t>(ctx->num_cus * wgs)) {
+        pa.trace = ctx->trace;
+        return vring_launch_local(pa.lg, ctx->num_cus * wgs, st, pa, workspace, tables_of(ctx), ctx->d_basis2);
+    }
     // the ordered records pay on the vring (path 0) and lean kernels; every other path
     // reads len/off itself
     const bool lean = ctx->path != 1 && (pa.lg == 2 || pa.lg == 3) && ctx->ablation == 0 &&
@@ -1870,7 +1883,22 @@ int enet_hip_crc32_gather_binned_device(enet_hip_context* ctx, const uint8_t* by
         return herr(hipGetLastError());
     }
 #endif
-    if (segCount && split) {
+    // default path, up to 2048 segments per workgroup (cfg5: 602112 at two per CU): one
+    // launch -- each workgroup sorts its own tile's segments longer than the short bound
+    // and checksums them (vring_launch_local) -- then the join
+    const int lgw = ctx->wgs_per_cu >= 1 ? std::min(ctx->wgs_per_cu, 2) : 2;
+    if (segCount && split && ctx->path == 0 && ctx->vr_abl == 0 && !ctx->vr_dynamic &&
+        segCount <= static_cast<uint64_t>(kVrLocalTile) * static_cast<uint64_t>(ctx->num_cus * lgw)) {
+        PacketArgs pa{};
+        pa.bytes = bytes;
+        pa.off = segOffsets;
+        pa.len = segLengths;
+        pa.n = segCount;
+        pa.out = seg_crc;
+        const int rc = vring_launch_local(lanes == 4 ? 2 : 3, ctx->num_cus * lgw, st, pa, workspace, tables_of(ctx),
+                                          ctx->d_basis2, gather_small(ctx) + 1u);
+        if (rc) return rc;
+    } else if (segCount && split) {
         const KernelTables tb = tables_of(ctx);
         const uint32_t kpk = lanes == 4 ? 16u : 8u;
         int rc;

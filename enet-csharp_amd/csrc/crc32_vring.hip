@@ -78,7 +78,23 @@ constexpr uint32_t kVrTileMaxC = kVrLds;
 constexpr int kVrLdsBinC = kVrTileMaxC + kVrW * 4;
 static_assert(2 * kVrLdsBinC <= 160 * 1024, "compact records instance: two workgroups per CU");
 template <int BIN>
-constexpr uint32_t vr_tile_max() { return BIN == 2 ? kVrTileMaxC : kVrTileMax; }
+constexpr uint32_t vr_tile_max() { return BIN >= 2 ? kVrTileMaxC : kVrTileMax; }
+// the local-tile records instance (BIN = 3): its prologue's counting sort -- 256 bins and
+// the 4 scan waves' totals -- in the image area, which is free until barrier A
+constexpr uint32_t kVrLocalBins = 256;
+constexpr uint32_t kVrLocalHist = 0;
+// ... and the staging of the metadata of each wave's second group (round 1), 256 B a wave
+constexpr uint32_t kVrLocalNext = 2048;
+static_assert(4u * (kVrLocalBins + kVrLocalBins / 64u) <= kVrLocalNext, "local sort's bins");
+static_assert(kVrLocalNext + 256u * kVrW <= kLdsTableBytes, "local sort in the image area");
+constexpr uint32_t kVrLocalItems = kVrLocalTile / (64u * kVrW);           // packets per thread
+static_assert(kVrLocalItems * 64u * kVrW == kVrLocalTile, "whole packets per thread");
+// an LDS add returning the old value (inline asm: no vmcnt wait put in front of it)
+__device__ __forceinline__ uint32_t lds_add_rtn(uint32_t addr, uint32_t v) {
+    uint32_t r;
+    asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(addr), "v"(v) : "memory");
+    return r;
+}
 // BIN's index stash (two slots of kPk dwords per wave) fits the basis staging area
 static_assert(kVrW * 2 * 16 * 4 <= kVrBasisRows * 256, "index stash over the basis staging area");
 
@@ -145,10 +161,9 @@ __device__ __forceinline__ void vr_issue_meta(uint64_t addr, uint32_t base) {
 }
 // the metadata of the lane's packet p (of kPk) once at most N younger loads are in
 // flight (BIN: and the record's caller index; VF: the slot offset and connectID)
-template <int N, int BIN, int VF, uint32_t kPk>
-__device__ __forceinline__ void vr_wait_meta(uint32_t base, uint32_t p, uint32_t& L, uint64_t& off, uint32_t& idx,
+template <int BIN, int VF, uint32_t kPk>
+__device__ __forceinline__ void vr_read_meta(uint32_t base, uint32_t p, uint32_t& L, uint64_t& off, uint32_t& idx,
                                              uint32_t& so, uint32_t& conn) {
-    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
     L = lds_load(base + 4u * p);
     off = static_cast<uint64_t>(lds_load(base + 4u * (kPk + p))) |
           (static_cast<uint64_t>(lds_load(base + 4u * (2u * kPk + p))) << 32);
@@ -157,6 +172,12 @@ __device__ __forceinline__ void vr_wait_meta(uint32_t base, uint32_t p, uint32_t
         so = lds_load(base + 4u * (3u * kPk + p));
         conn = lds_load(base + 4u * (4u * kPk + p));
     }
+}
+template <int N, int BIN, int VF, uint32_t kPk>
+__device__ __forceinline__ void vr_wait_meta(uint32_t base, uint32_t p, uint32_t& L, uint64_t& off, uint32_t& idx,
+                                             uint32_t& so, uint32_t& conn) {
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
+    vr_read_meta<BIN, VF, kPk>(base, p, L, off, idx, so, conn);
 }
 
 // Receive verify (protocol.cs:1052-1068) in the lane folding the slot: the slot's
@@ -687,6 +708,9 @@ struct VrIt {
 // out[record r's index] (enet_hip_crc32_batch_device_binned).  One workgroup per CU;
 // BIN = 2, the compact records instance: the same without the x^(-8 c) tables (tz mod 8
 // by unsteps), two workgroups per CU.
+// BIN = 3, the local-tile records instance (vring_launch_local): as BIN = 2, but each
+// workgroup orders its own tile of packets in its prologue (no bin kernel, no second
+// launch) and checksums that tile's groups, longest first.
 // ROT = 1: the tail-first stage order (below; diagnostics library); 0 = stages in
 // window order (the product).
 // VF = 1: receive verify (protocol.cs:1052-1068) over a VrVBatches list, 8 lanes per
@@ -736,7 +760,7 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t wv = static_cast<uint64_t>(blockIdx.x) * kVrW + wave;
     const uint64_t wt = static_cast<uint64_t>(gridDim.x) * kVrW;
-    constexpr bool kDyn = DYN != 0 && !WK;
+    constexpr bool kDyn = DYN != 0 && !WK && BIN != 3;
     // slots taken statically per wave: rounds 0 .. kStatic - 1 are chunks k + r G
     constexpr uint32_t kStatic = kDyn ? 3u : 2u;
     if constexpr (kDyn) {                                    // wave 0, before its takes: no round published
@@ -760,8 +784,104 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     // its maximum goes to LDS, one raw barrier, every wave reads the 16 maxima (no
     // global atomic; a launch over tens of millions of segments reads each count
     // once per workgroup, not once per wave).
-    uint64_t n0 = bl.b[0].n, ngroups_all = bl.groups;
-    if constexpr (BIN) {
+    // BIN = 3 (the local-tile records instance, vring_launch_local): workgroup k orders
+    // its own packets [k T, (k + 1) T) here, two per thread, those of at least
+    // local_keep_min bytes (lcnt of them) -- a counting sort by window length (bin_of's
+    // 32-byte bins, longest first) in LDS: each packet's place in its bin (an LDS add), an
+    // exclusive scan of the bins (wave scans by DPP shifts, then the four waves'
+    // totals), then its record {len, off_lo, off_hi, index} to local_rec[k T + rank].  The first two rounds' metadata also go straight to LDS
+    // (vr_read_meta's layout: field f of packet p at +4 (f kPk + p)): round 0's group g to
+    // wave g's metadata area, round 1's to a staging area of the wave whose slot 16 + w
+    // takes it, copied over once the wave has read round 0's.  So the first two groups
+    // need no metadata DMA, and the record stores -- read by the DMAs from the third
+    // group on, by this CU's waves -- are waited for only before barrier A, with the
+    // first stage's loads in flight.  One
+    // tile per workgroup streams as fast as the bin kernel's rank-interleaved order
+    // (tools/dealprobe.hip: 42.2 against 41.9 us for cfg3, profiles/r06_local/).
+    // basis row `wave` (waves < 10) and, waves 0..7, one KiB each of the zero-byte
+    // multiplier tables: LDS-DMAs, outside the image area
+    auto issue_tables = [&]() __attribute__((always_inline)) {
+        if (wave < static_cast<uint32_t>(kVrBasisRows))
+            dma4(basis + static_cast<size_t>(LG == 2 ? 1 : 2) * kVrBasisDwords + 64u * wave + lane,
+                 kVrStaging + 256u * wave);
+        if (wave < static_cast<uint32_t>(kTzTableDwords / 256)) dma16(tb.tz + 256u * wave + 4u * lane, kVrTz + 1024u * wave);
+    };
+    uint64_t lrec = 0, lcnt = 0;                             // BIN 3: records, and the tile's kept packets
+    if constexpr (BIN == 3) {
+        if (TR == 1 && (threadIdx.x & 63u) == 0u) trace[8u * wv] = __builtin_amdgcn_s_memrealtime();   // (start)
+        issue_tables();                                      // (they land while the tile is sorted)
+        const uint64_t first = static_cast<uint64_t>(blockIdx.x) * bl.tile_local, nb = bl.b[0].n;
+        const uint64_t tn = first < nb ? umin64(nb - first, bl.tile_local) : 0u;   // the tile's packets
+        lrec = reinterpret_cast<uint64_t>(bl.local_rec) + 16u * first;
+        const uint32_t t = threadIdx.x;
+        // item i of thread t = the tile's packet t + 1024 i; kept: live and at least
+        // local_keep_min bytes (the binned gather leaves its short segments to the join)
+        uint32_t L[kVrLocalItems], bin[kVrLocalItems], slot[kVrLocalItems];
+        uint64_t o[kVrLocalItems];
+        bool kept[kVrLocalItems];
+#pragma unroll
+        for (uint32_t i = 0; i < kVrLocalItems; ++i) {
+            const uint32_t j = t + 64u * kVrW * i;
+            L[i] = j < tn ? bl.b[0].len[first + j] : 0u;
+            o[i] = j < tn ? bl.b[0].off[first + j] : 0u;
+        }
+        if (t < kVrLocalBins) lds_store(kVrLocalHist + 4u * t, 0u);
+        static_assert(kVrMetaWaveBin * kVrW == 4u * 64u * kVrW, "one metadata dword per thread");
+        lds_store(kVrMeta + 4u * t, 0u);                     // (a partial group's missing packets: zeros)
+        lds_store(kVrLocalNext + 4u * t, 0u);
+        __syncthreads();
+#pragma unroll
+        for (uint32_t i = 0; i < kVrLocalItems; ++i) {
+            kept[i] = t + 64u * kVrW * i < tn && L[i] >= bl.local_keep_min;
+            bin[i] = kVrLocalBins - 1u - min((L[i] + (static_cast<uint32_t>(o[i]) & 63u)) >> 5, kVrLocalBins - 1u);
+            slot[i] = kept[i] ? lds_add_rtn(kVrLocalHist + 4u * bin[i], 1u) : 0u;
+        }
+        __syncthreads();
+        uint32_t mine = 0, incl = 0;
+        if (t < kVrLocalBins) {
+            mine = lds_load(kVrLocalHist + 4u * t);
+            incl = mine;
+#pragma unroll
+            for (uint32_t sh = 1; sh < 64u; sh <<= 1) {
+                const uint32_t u = static_cast<uint32_t>(__shfl_up(static_cast<int>(incl), sh));
+                incl += (t & 63u) >= sh ? u : 0u;
+            }
+            if ((t & 63u) == 63u) lds_store(kVrLocalHist + 4u * (kVrLocalBins + (t >> 6)), incl);
+        }
+        __syncthreads();
+        uint32_t pre = 0, total = 0;                         // (total: the tile's kept packets)
+#pragma unroll
+        for (uint32_t w = 0; w < kVrLocalBins / 64u; ++w) {
+            const uint32_t ws = lds_load(kVrLocalHist + 4u * (kVrLocalBins + w));
+            pre += w < (t >> 6) ? ws : 0u;
+            total += ws;
+        }
+        if (t < kVrLocalBins) lds_store(kVrLocalHist + 4u * t, pre + incl - mine);   // the bin's first rank
+        lcnt = total;
+        const uint32_t ng = (total + kPk - 1u) / kPk;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t i = 0; i < kVrLocalItems; ++i) {
+            if (!kept[i]) continue;
+            const uint32_t rank = lds_load(kVrLocalHist + 4u * bin[i]) + slot[i];
+            const uint32_t olo = static_cast<uint32_t>(o[i]), ohi = static_cast<uint32_t>(o[i] >> 32);
+            const uint32_t idx = static_cast<uint32_t>(first + t + 64u * kVrW * i);
+            reinterpret_cast<uint4*>(lrec)[rank] = make_uint4(L[i], olo, ohi, idx);
+            const uint32_t g = rank / kPk, p = rank % kPk;
+            const uint32_t dst = g < kVrW ? kVrMeta + kVrMetaWaveBin * g
+                               : g < 2u * kVrW ? kVrLocalNext + 256u * (ng >= 2u * kVrW ? 2u * kVrW - 1u - g : g - kVrW)
+                                               : ~0u;
+            if (dst != ~0u) {
+                lds_store(dst + 4u * p, L[i]);
+                lds_store(dst + 4u * (kPk + p), olo);
+                lds_store(dst + 4u * (2u * kPk + p), ohi);
+                lds_store(dst + 4u * (3u * kPk + p), idx);
+            }
+        }
+        __syncthreads();                                     // (LDS only: the record stores stay in flight)
+    }
+    uint64_t n0 = BIN == 3 ? lcnt : bl.b[0].n, ngroups_all = BIN == 3 ? (lcnt + kPk - 1u) / kPk : bl.groups;
+    if constexpr (BIN == 1 || BIN == 2) {
         if (bl.tile_counts) {
             uint32_t m = 0;
             for (uint32_t t = wave * 64u + (threadIdx.x & 63u); t < bl.tiles; t += 64u * kVrW)
@@ -795,9 +915,15 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     // profiles/r06_cfg3/).  Odd rounds therefore deal the workgroups in reverse order
     // (k -> G - 1 - k): still a permutation of the round's groups, and every workgroup's
     // rounds sum to about the same bytes (boustrophedon).
-    constexpr bool kSnake = BIN != 0;
+    constexpr bool kSnake = BIN == 1 || BIN == 2;
     auto slot_group = [&](uint32_t sl) __attribute__((always_inline)) -> uint64_t {
         if constexpr (WK) return sl < gw ? static_cast<uint64_t>(blockIdx.x) * gw + sl : ~0ull;
+        // BIN = 3: the workgroup's own groups in slot order, round 1 reversed when it is
+        // full, so each wave's two static groups (w and 31 - w) sum to about the same
+        // bytes; later rounds are taken as the waves free up (a partial round stays in
+        // order: live slots a prefix)
+        if constexpr (BIN == 3)
+            return (sl / kVrW == 1u && ngroups_all >= 2u * kVrW) ? 3u * kVrW - 1u - sl : sl;
         if (kDyn && sl >= kStatic * kVrW) return static_cast<uint64_t>(vr_round_chunk(sl / kVrW)) * kVrW + (sl & (kVrW - 1u));
         const uint32_t r = sl / kVrW;
         const uint64_t k = (kSnake && (r & 1u)) ? gridDim.x - 1u - blockIdx.x : blockIdx.x;
@@ -883,14 +1009,10 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
             tr[7] = ngroups;
         }
     };
-    mark(0);
+    if constexpr (BIN != 3) mark(0);                         // (BIN 3: before its sort)
 
     // ---- prologue: basis row `wave` (waves < 10) and metadata of the first group
-    if (wave < static_cast<uint32_t>(kVrBasisRows))
-        dma4(basis + static_cast<size_t>(LG == 2 ? 1 : 2) * kVrBasisDwords + 64u * wave + lane,
-             kVrStaging + 256u * wave);
-    // waves 0..7: one KiB each of the zero-byte multiplier tables
-    if (wave < static_cast<uint32_t>(kTzTableDwords / 256)) dma16(tb.tz + 256u * wave + 4u * lane, kVrTz + 1024u * wave);
+    if constexpr (BIN != 3) issue_tables();                  // (BIN 3: before its sort)
     if constexpr (BIN == 1) {                                // the small x^(-8 c) tables: 28 one-KiB chunks
 #pragma unroll
         for (uint32_t c = wave; c < static_cast<uint32_t>(kTzSmallDwords / 256); c += kVrW)
@@ -914,7 +1036,7 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
         const uint32_t q = min(l & (kPk - 1u), left < 63u ? static_cast<uint32_t>(left) : 63u);
         if constexpr (BIN) {
             f = f < 4u ? f : 0u;
-            vr_issue_meta(reinterpret_cast<uint64_t>(B.off) + 16u * (base + q) + 4u * f, mbase);
+            vr_issue_meta((BIN == 3 ? lrec : reinterpret_cast<uint64_t>(B.off)) + 16u * (base + q) + 4u * f, mbase);
         } else if constexpr (VF) {
             f = f < 5u ? f : 0u;
             const uint64_t la = reinterpret_cast<uint64_t>(B.len + base) + 4u * q;
@@ -928,8 +1050,14 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
             vr_issue_meta(f ? oa : la, mbase);
         }
     };
-    load_meta(any ? pit : VrIt{0u, 0u});                     // (batch 0 exists: count >= 1)
-    vr_wait_meta<0, BIN, VF, kPk>(mbase, lane_p(), mL, moff, midx, mso, mconn);   // basis row and metadata landed
+    if constexpr (BIN == 3) {
+        // round 0's metadata, put here by the sort; then round 1's over it (its DMA skipped)
+        vr_read_meta<BIN, VF, kPk>(mbase, lane_p(), mL, moff, midx, mso, mconn);
+        lds_store(mbase + 4u * lane, lds_load(kVrLocalNext + 256u * wave + 4u * lane));
+    } else {
+        load_meta(any ? pit : VrIt{0u, 0u});                 // (batch 0 exists: count >= 1)
+        vr_wait_meta<0, BIN, VF, kPk>(mbase, lane_p(), mL, moff, midx, mso, mconn);   // basis row and metadata landed
+    }
     mark(1);
 
     // ---- producer: window of the group it loads, one stage ahead of the consumer
@@ -1047,7 +1175,8 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
             s0 = (a0 < pe && a0 + 16u > lz) ? ws + a0 : zero;
             s1 = (a1 < pe && a1 + 16u > lz) ? ws + a1 : zero;
         }
-        const bool meta = (pst == 0u) & qlive & !pdone;     // (one branch, no short-circuit flow blocks)
+        // (BIN 3's first produce: the second group's metadata is in LDS already)
+        const bool meta = (BIN == 3 && WS < 0) ? false : ((pst == 0u) & qlive & !pdone);
         if (meta) {
             load_meta(qit);
             vr_issue_stage<slot, NT>(s0, s1);
@@ -1061,6 +1190,12 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     if (any) {
         producer_enter(std::false_type{});
         produce(std::integral_constant<uint32_t, 0>{}, std::integral_constant<int, -1>{});
+    }
+    if constexpr (BIN == 3) {
+        // the wave's record stores (and the table DMAs) have completed before barrier A;
+        // only the first stage's two loads stay in flight
+        if (any) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
 
     // ---- the table image, rebuilt in LDS while stage 0 is in flight.  Wave w
@@ -1371,6 +1506,18 @@ const void* vring_pick_bin(int lg, int dyn, int abl = 0, bool compact = false, b
     return nullptr;
 }
 
+// the local-tile records instance (BIN = 3); trace = its per-wave timeline twin
+// (diagnostics library)
+const void* vring_pick_local(int lg, bool trace) {
+    if (lg != 2 && lg != 3) return nullptr;
+#ifdef ENET_HIP_DIAG
+    if (trace) return lg == 2 ? vring_fn<2, 1, 0, 0, 3>() : vring_fn<3, 1, 0, 0, 3>();
+#else
+    if (trace) return nullptr;
+#endif
+    return lg == 2 ? vring_fn<2, 0, 0, 0, 3>() : vring_fn<3, 0, 0, 0, 3>();
+}
+
 // The product instances: 64 VGPRs (WPE 8), one or two workgroups per CU, stages in
 // window order.  The diagnostics library (ENET_HIP_DIAG) adds the sweep variants: a
 // trace buffer (per-wave timestamps), nt stage loads, workgroup walks, the tail-first
@@ -1449,6 +1596,8 @@ int vring_setup() {
             }
             if ((rc = set(vring_pick_bin(lg, d, 0, false, true), kVrLdsBin))) return rc;
             if ((rc = set(vring_pick_bin(lg, d, 0, true, true), kVrLdsBinC))) return rc;
+            for (bool tr : {false, true})
+                if ((rc = set(vring_pick_local(lg, tr), kVrLdsBinC))) return rc;
             for (int t = 0; t < 2; ++t)
                 for (int nt = 0; nt < 2; ++nt)
                     for (int abl : kAbl)
@@ -1534,6 +1683,34 @@ int vring_launch_vlist(int max_wgs, const VrVariant& v, hipStream_t st, const Vr
         return -static_cast<int>(hipErrorInvalidValue);
     void* args[] = {&a, const_cast<KernelTables*>(&tb), const_cast<const uint32_t**>(&basis2), &trace};
     const hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(64 * kVrW), args, kVrLds, st);
+    return e == hipSuccess ? 0 : -static_cast<int>(e);
+}
+
+int vring_launch_local(int lg, int max_wgs, hipStream_t st, const PacketArgs& pa, void* records,
+                       const KernelTables& tb, const uint32_t* basis2, uint32_t keep_min) {
+    if (pa.n == 0) return 0;
+    if ((lg != 2 && lg != 3) || max_wgs < 1 || !records || (reinterpret_cast<uintptr_t>(records) & 15u))
+        return -static_cast<int>(hipErrorInvalidValue);
+    // T: the packets of a workgroup -- the batch over max_wgs workgroups, in whole groups,
+    // at least a group per wave, at most kVrLocalTile (two per thread)
+    const uint64_t kpk = 64u >> lg;
+    uint64_t T = (pa.n + static_cast<uint64_t>(max_wgs) - 1u) / static_cast<uint64_t>(max_wgs);
+    T = std::max<uint64_t>((T + kpk - 1u) / kpk * kpk, kpk * kVrW);
+    T = std::min<uint64_t>(T, kVrLocalTile);
+    const uint64_t grid = (pa.n + T - 1u) / T;               // (every workgroup has a packet)
+    if (grid > static_cast<uint64_t>(max_wgs)) return -static_cast<int>(hipErrorInvalidValue);
+    VrBatches a{};
+    a.count = 1;
+    a.b[0] = VrBatch{pa.bytes, pa.off, pa.len, pa.out, pa.n, 0u};
+    a.groups = (pa.n + kpk - 1u) / kpk;
+    a.tile_local = static_cast<uint32_t>(T);
+    a.local_rec = records;
+    a.local_keep_min = keep_min;
+    const void* fn = vring_pick_local(lg, pa.trace != nullptr);
+    if (!fn) return -static_cast<int>(hipErrorInvalidValue);
+    uint64_t* trace = pa.trace;
+    void* args[] = {&a, const_cast<KernelTables*>(&tb), const_cast<const uint32_t**>(&basis2), &trace};
+    const hipError_t e = hipLaunchKernel(fn, dim3(static_cast<unsigned>(grid)), dim3(64 * kVrW), args, kVrLdsBinC, st);
     return e == hipSuccess ? 0 : -static_cast<int>(e);
 }
 

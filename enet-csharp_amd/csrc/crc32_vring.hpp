@@ -42,7 +42,14 @@ struct VrBatches {
     // static deal, and the launch's generation of it
     uint64_t* claim;
     uint32_t claim_gen;
-    uint32_t pad;
+    // the local-tile records instance (vring_launch_local): packets per workgroup, and
+    // the records it writes (16 B per packet, workgroup k's at [k tile_local, ...))
+    uint32_t tile_local;
+    void* local_rec;
+    // ... and the shortest packet it keeps (shorter ones get no record and no CRC: the
+    // binned gather's short segments, folded by its join); 0 = every packet
+    uint32_t local_keep_min;
+    uint32_t local_pad;
     VrBatch b[kVrMaxBatches];
 };
 static_assert(sizeof(VrBatches) <= 3072, "kernel arguments");
@@ -115,6 +122,19 @@ int vring_launch_list(int lg, int max_wgs, const VrVariant& v, hipStream_t st, c
 // workgroups, LDS and variants as vring_launch_list (trace: end records only).
 int vring_launch_vlist(int max_wgs, const VrVariant& v, hipStream_t st, const VrVBatches& bl, const KernelTables& tb,
                        const uint32_t* basis2, uint64_t* trace);
+
+// The length-binned checksum in ONE launch (enet_hip_crc32_batch_device_binned and
+// the binned gather's segment pass when n <= kVrLocalTile x max_wgs): workgroup k
+// takes the packets [k T, (k + 1) T) of the batch (T <= kVrLocalTile, a multiple of
+// the packets per group), orders the records of those of at least keep_min bytes by
+// window length in its own prologue -- a counting sort in LDS, the records written to
+// `records` from 16 k T on (16 B per packet) -- and checksums them longest first,
+// CRCs to out[index] (shorter packets: none).  No bin kernel, no dependent launch.
+// Returns 0 or -hipError_t (-hipErrorInvalidValue when the batch is too large for one
+// tile per workgroup).
+constexpr uint32_t kVrLocalTile = 2048;
+int vring_launch_local(int lg, int max_wgs, hipStream_t st, const PacketArgs& pa, void* records,
+                       const KernelTables& tb, const uint32_t* basis2, uint32_t keep_min = 0);
 
 // Launch the vring kernel over one batch: checksum mode, lanes per packet 2^lg
 // (lg = 2 or 3), at most max_wgs workgroups; pa.meta4 set = binned records.

@@ -89,8 +89,8 @@ ENET_HIP_API int enet_hip_set_tuning(enet_hip_context* ctx, int lanes_per_packet
  * verify.  (Diagnostics library: 16 lanes run the LDS-ring stream kernel, other
  * lane counts the direct kernel.)
  * Every path gives the same (correct) checksums.  Built in every library: 13 = the
- * lean kernel, 17 = the vring kernel (for the length-binned entries: its records
- * instance).  Tuning sweeps, libenethip_diag.so only (-1 elsewhere): 1 = direct
+ * lean kernel, 17 = the vring kernel (for the length-binned entries: the bin
+ * kernel and its records instance, the two-launch form at every batch size).  Tuning sweeps, libenethip_diag.so only (-1 elsewhere): 1 = direct
  * loads only, 2 + k = stream kernel geometry k (k < 11), 13 + g = lean kernel geometry g (g < 4), 18 = vring with nontemporal
  * stage loads, 19 / 20 = vring with each workgroup walking a contiguous range of
  * groups (plain / nontemporal loads), 21 = vring with the tail-first stage order
@@ -132,9 +132,15 @@ ENET_HIP_API int enet_hip_crc32_batch_list_device(enet_hip_context* ctx, const E
 
 /* Same results as enet_hip_crc32_batch_device (enet_crc32, c/packet.cs:142-160,
  * per packet), for batches of mixed lengths (SURVEY cfg3): inside each tile of
- * 1024 packets the packet records are first ordered by window length (offset mod
+ * packets the packet records are first ordered by window length (offset mod
  * 64 + length, 32-byte bins, longest first) on the GPU, so the packets the kernel
- * runs together need about the same number of stages; out[] stays in caller order.  `workspace` is caller-owned
+ * runs together need about the same number of stages; out[] stays in caller order.
+ * Default path, count <= 1024 x CUs x workgroups per CU (two per CU unless
+ * enet_hip_set_tuning sets one; cfg3 fits either): one
+ * launch, workgroup k ordering its own tile of T <= 1024 packets in its prologue
+ * (records [k T, (k + 1) T) of the workspace).  Larger batches, and kernel path 17:
+ * a bin kernel over 1024-packet tiles, rank-interleaved, then the records instance
+ * of the vring kernel.  `workspace` is caller-owned
  * device memory of at least enet_hip_binned_workspace_size(count) bytes (16 per
  * packet: the ordered {len, off_lo, off_hi, index} records), 16-byte aligned, not
  * shared with a call in flight on another stream; count < 2^32.  No state is

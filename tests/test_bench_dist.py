@@ -222,10 +222,10 @@ def test_kernel_name_follows_the_entry_and_knobs():
     import argparse
     import bench
 
-    def name(**kw):
+    def name(local_tiles=False, **kw):
         a = dict(path=0, lanes=0, binned=False, ablate=0, wgs=0)
         a.update(kw)
-        return bench.kernel_name(argparse.Namespace(**a))
+        return bench.kernel_name(argparse.Namespace(**a), local_tiles=local_tiles)
 
     assert name() == "crc32_vring_kernel<3, 0, 0, 0, 0, 0, 0, 0, 0>"
     assert name(binned=True) == "crc32_vring_kernel<2, 0, 0, 0, 1, 0, 0, 0, 0>"
@@ -235,6 +235,12 @@ def test_kernel_name_follows_the_entry_and_knobs():
     assert name(binned=True, ablate=8388608) == "crc32_vring_kernel<2, 0, 0, 0, 1, 0, 0, 0, 0>"
     assert name(ablate=524288) == "crc32_vring_kernel<3, 0, 0, 0, 0, 0, 0, 0, 1>"
     assert name(ablate=8388608) == "crc32_vring_kernel<3, 0, 0, 0, 0, 0, 0, 0, 2>"
+    # the one-launch local-tile records instance (batches of one tile per workgroup)
+    assert name(binned=True, local_tiles=True) == "crc32_vring_kernel<2, 0, 0, 0, 3, 0, 0, 0, 0>"
+    assert name(binned=True, local_tiles=True, wgs=2) == "crc32_vring_kernel<2, 0, 0, 0, 3, 0, 0, 0, 0>"
+    assert name(binned=True, local_tiles=True, lanes=8) == "crc32_vring_kernel<3, 0, 0, 0, 3, 0, 0, 0, 0>"
+    assert name(binned=True, local_tiles=True, path=17) == "crc32_vring_kernel<2, 0, 0, 0, 1, 0, 0, 0, 0>"
+    assert name(binned=True, local_tiles=True, ablate=38912) == "crc32_vring_kernel<2, 0, 0, 19, 1, 0, 0, 0, 0>"
 
 
 def test_shard_option_measures_one_cfg4_shard(monkeypatch):

@@ -207,10 +207,11 @@ def test_binned_records_instance_per_workgroup_count(ctx, golden, oracle_lib, wg
 
 
 def test_binned_records_are_a_length_ordered_permutation(ctx, oracle_lib):
-    """The workspace's records (documented layout: n x {len, off_lo, off_hi, index}
-    first) are a permutation of the batch: each 1024-packet tile ordered by non-increasing
-    32-byte bin of the window length (offset mod 64 + length), full tiles interleaved
-    group by group; 600 K packets, ragged last tile."""
+    """The two-launch form's records (kernel path 17, and the default past the local
+    tiles' limit; documented layout: n x {len, off_lo, off_hi, index} first) are a
+    permutation of the batch: each 1024-packet tile ordered by non-increasing 32-byte bin
+    of the window length (offset mod 64 + length), full tiles interleaved group by group;
+    600 K packets, ragged last tile."""
     rng = np.random.default_rng(11)
     n = 600_000
     lens = rng.integers(0, 1500, size=n).astype(np.uint32)
@@ -218,12 +219,17 @@ def test_binned_records_are_a_length_ordered_permutation(ctx, oracle_lib):
     off = rng.integers(0, 1 << 22, size=n).astype(np.uint64)
     payload = rng.integers(0, 256, size=(1 << 22) + 20000, dtype=np.uint8)
     ctx.set_tuning(8, 0)
-    d_p, d_o, d_l = dev(payload), dev(off), dev(lens)
-    out = torch.zeros(n, dtype=torch.int32, device="cuda")
-    ws_bytes = ctx.binned_workspace_size(n)
-    ws = torch.zeros(ws_bytes, dtype=torch.uint8, device="cuda")
-    ctx.crc32_batch_device_binned(d_p, d_o, d_l, n, out, ws, ws_bytes, stream=torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
+    ctx.set_kernel_path(17)
+    try:
+        d_p, d_o, d_l = dev(payload), dev(off), dev(lens)
+        out = torch.zeros(n, dtype=torch.int32, device="cuda")
+        ws_bytes = ctx.binned_workspace_size(n)
+        ws = torch.zeros(ws_bytes, dtype=torch.uint8, device="cuda")
+        ctx.crc32_batch_device_binned(d_p, d_o, d_l, n, out, ws, ws_bytes, stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+    finally:
+        ctx.set_kernel_path(0)
+        ctx.set_tuning(0, 0)
     rec = ws[:16 * n].cpu().numpy().view(np.uint32).reshape(n, 4)
     idx = rec[:, 3].astype(np.int64)
     assert (np.sort(idx) == np.arange(n)).all()
@@ -244,6 +250,56 @@ def test_binned_records_are_a_length_ordered_permutation(ctx, oracle_lib):
     assert (np.diff(bins[order])[same] <= 0).all()            # longest bin first inside a tile
     exp = oracle_lib.batch(payload, off, lens, threads=16)
     assert (out.cpu().numpy().view(np.uint32) == exp).all()
+
+
+@pytest.mark.parametrize("wgs", [1, 2])
+@pytest.mark.parametrize("lanes", [4, 8])
+def test_binned_local_tiles_layout_and_limit(ctx, oracle_lib, wgs, lanes):
+    """The one-launch binned checksum (default path, vring_launch_local): workgroup k
+    orders its own tile of T packets, so the workspace's records [k T, (k + 1) T) are a
+    permutation of packets [k T, (k + 1) T) in non-increasing 32-byte bins of the window
+    length (offset mod 64 + length).  T = the batch over the grid (CUs x workgroups per
+    CU) in whole groups, at least one group per wave, at most 2048 (two per thread).
+    Checked at several sizes, up to the one-tile-per-workgroup limit, and one packet past
+    it (the bin kernel and the records instance)."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    G = cus * wgs
+    limit = 2048 * G
+    kpk = 64 // lanes
+    rng = np.random.default_rng(97 + wgs + lanes)
+    payload = rng.integers(0, 256, size=(1 << 21) + 4096, dtype=np.uint8)
+    for n in (1, 17, 255, 16 * kpk + 3, 5000, G * 16 * kpk + 1, 1024 * G + 1, limit - 7, limit, limit + 1):
+        lens = rng.integers(0, 300, size=n).astype(np.uint32)
+        lens[rng.integers(0, n, size=max(1, n // 500))] = rng.integers(4000, 4096, size=max(1, n // 500)).astype(np.uint32)
+        lens[: min(n, 5)] = 0
+        off = rng.integers(0, 1 << 21, size=n).astype(np.uint64)
+        ctx.set_tuning(lanes, wgs)
+        try:
+            d_p, d_o, d_l = dev(payload), dev(off), dev(lens)
+            out = torch.zeros(n, dtype=torch.int32, device="cuda")
+            ws_bytes = ctx.binned_workspace_size(n)
+            ws = torch.zeros(ws_bytes, dtype=torch.uint8, device="cuda")
+            ctx.crc32_batch_device_binned(d_p, d_o, d_l, n, out, ws, ws_bytes,
+                                          stream=torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+        finally:
+            ctx.set_tuning(0, 0)
+        exp = oracle_lib.batch(payload, off, lens, threads=16)
+        assert (out.cpu().numpy().view(np.uint32) == exp).all(), n
+        if n > limit:
+            continue
+        per_wg = -(-n // G)                                     # ceil(n / G), then whole groups
+        T = min(max(-(-per_wg // kpk) * kpk, kpk * 16), 2048)
+        rec = ws[:16 * n].cpu().numpy().view(np.uint32).reshape(n, 4)
+        idx = rec[:, 3].astype(np.int64)
+        pos = np.arange(n)
+        assert (idx // T == pos // T).all(), n                  # each record stays in its workgroup's tile
+        assert (np.sort(idx) == pos).all(), n
+        assert (rec[:, 0] == lens[idx]).all(), n
+        assert ((rec[:, 1].astype(np.uint64) | (rec[:, 2].astype(np.uint64) << np.uint64(32))) == off[idx]).all(), n
+        bins = np.minimum((rec[:, 0] + (rec[:, 1] & 63)) >> 5, 255).astype(np.int64)
+        same = np.diff(pos // T) == 0
+        assert (np.diff(bins)[same] <= 0).all(), n              # longest bin first inside a tile
 
 
 def test_binned_rejects_small_workspace(ctx):

@@ -9,7 +9,11 @@ group's stage count.  Splits the records kernel's span into
   steady -- the waves' loop time, per group and per stage (a CU runs 16 waves at once);
   drain  -- the last wave's end against the median wave's end (imbalance).
 HIP events time the whole call and the records kernel's product instance alone beside it.
-    python tools/bin_timeline.py [reps=3]"""
+Round 6: the default path of a batch that fits one tile per workgroup is ONE launch, the
+local-tile records instance (BIN = 3): its trace's start is the kernel's entry, before the
+workgroup's own sort, so "metadata" = sort + the first group's metadata.  wgs = workgroups
+per CU (1 or 2), path 17 = the two-launch form (bin kernel + records instance).
+    python tools/bin_timeline.py [reps=3] [wgs=1] [path=0]"""
 import json
 import os
 import sys
@@ -44,6 +48,8 @@ def stages_of_groups(rec: np.ndarray, base_addr: int, lanes: int = 4, kpk: int =
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    wgs = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    path = int(sys.argv[3]) if len(sys.argv) > 3 else 0
     b = workloads.cfg3()
     dev = torch.device("cuda")
     # five copies of the batch in turn (960 MB, more than the 256 MB MALL), as the bench
@@ -53,12 +59,13 @@ def main():
     off = torch.from_numpy(b.off.view(np.int64)).to(dev)
     lens = torch.from_numpy(b.lens.view(np.int32)).to(dev)
     out = torch.zeros(b.n, dtype=torch.int32, device=dev)
-    ctx = enethip.Context(0, 4, 1, diag=True)
+    ctx = enethip.Context(0, 4, wgs, diag=True)
+    ctx.set_kernel_path(path)
     ws = torch.zeros(ctx.binned_workspace_size(b.n), dtype=torch.uint8, device=dev)
     h = torch.cuda.current_stream().cuda_stream
     import oracle
     exp = oracle.OracleLib().batch(b.payload, b.off, b.lens, threads=8)
-    nw = 256 * 16
+    nw = torch.cuda.get_device_properties(0).multi_processor_count * wgs * 16
     tr = torch.zeros(nw * 8, dtype=torch.int64, device=dev)
 
     turn = [0]
@@ -108,7 +115,7 @@ def main():
         xcc = (t[:, 6] >> np.uint64(32)).astype(np.int64)
         mb = float(b.lens.astype(np.int64).sum()) / 1e6
         print(json.dumps({
-            "rep": rep, "call_us_events": round(call_us, 2), "records_span_us": round(span, 2),
+            "rep": rep, "wgs": wgs, "path": path, "call_us_events": round(call_us, 2), "records_span_us": round(span, 2),
             "waves": int(len(t)), "groups": tot_groups, "groups_expected": int(len(st)),
             "stages_total": int(st.sum()), "stages_per_group_mean": round(float(st.mean()), 3),
             "start_loop_entry_p50_max_us": [round(float(np.median(entry)), 2), round(float(entry.max()), 2)],
