@@ -667,6 +667,60 @@ def vring_slot_group(blk: int, sl: int, wt: int, W: int = 16, grid: int = 0, sna
     return W * k + (sl % W) + r * wt
 
 
+def vring_local_tile(n: int, max_wgs: int, kpk: int, W: int = 16, cap: int = 2048):
+    """crc32_vring.hip vring_launch_local: packets per workgroup T (the batch over max_wgs
+    workgroups, in whole groups, at least a group per wave, at most cap) and the grid
+    ceil(n / T); None when the batch does not fit one tile per workgroup."""
+    T = -(-n // max_wgs)
+    T = max(-(-T // kpk) * kpk, kpk * W)
+    T = min(T, cap)
+    grid = -(-n // T)
+    return (T, grid) if grid <= max_wgs else None
+
+
+def vring_local_slot_group(sl: int, ng: int, W: int = 16) -> int:
+    """The local-tile instance's slot_group: the workgroup's own groups in slot order,
+    round 1 reversed when it is full (ng >= 2 W)."""
+    return 3 * W - 1 - sl if (sl // W == 1 and ng >= 2 * W) else sl
+
+
+def vring_local_meta_area(g: int, ng: int, W: int = 16):
+    """Where the local sort puts group g's metadata: ("M", w) = wave w's metadata area
+    (round 0), ("X", w) = wave w's staging of its second group (round 1), None = read
+    later by a metadata DMA."""
+    if g < W:
+        return ("M", g)
+    if g < 2 * W:
+        return ("X", 2 * W - 1 - g if ng >= 2 * W else g - W)
+    return None
+
+
+def vring_local_deal(ng: int, rng, W: int = 16):
+    """Simulate one workgroup of the local-tile instance: every wave takes slots wave
+    and 16 + wave, then slots from the workgroup's counter (from 32), in a random
+    interleaving, until a slot maps past the tile's last group.  Returns the groups in
+    the order taken and each wave's groups."""
+    ctr = 2 * W
+    taken = {w: 0 for w in range(W)}
+    alive = set(range(W))
+    groups, per_wave = [], {w: [] for w in range(W)}
+    while alive:
+        w = rng.choice(sorted(alive))
+        if taken[w] < 2:
+            sl = w + W * taken[w]
+        else:
+            sl = ctr
+            ctr += 1
+        taken[w] += 1
+        g = vring_local_slot_group(sl, ng, W)
+        if g >= ng:
+            alive.discard(w)
+            continue
+        groups.append(g)
+        per_wave[w].append(g)
+    return groups, per_wave
+
+
 def vring_dynamic_deal(batch_groups, grid: int, rng, W: int = 16, snake: bool = False):
     """Simulate one launch of the vring kernel's dynamic slots: every wave takes
     slots wave and 16 + wave, then slots from its workgroup's counter (starting at

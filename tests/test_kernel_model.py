@@ -479,3 +479,71 @@ def test_snake_deal_balances_binned_ranks():
         return max(per) / min(per)
     assert work(False) > 1.4
     assert work(True) < 1.02
+
+
+@pytest.mark.parametrize("ng", list(range(0, 70)) + [128, 129, 200])
+def test_local_tile_slots_cover_every_group_once(ng):
+    """The local-tile records instance (crc32_vring.hip BIN 3): whatever order its waves
+    take slots in, each of the tile's groups is taken exactly once, a wave's groups
+    ascend (so its stop at the first dead slot loses nothing), and the round-1 reversal
+    (full rounds only) keeps the live slots a prefix of every round."""
+    import random
+    from kernel_model import vring_local_deal
+    for seed in range(3):
+        groups, per_wave = vring_local_deal(ng, random.Random(seed * 1000 + ng))
+        assert sorted(groups) == list(range(ng))
+        for w, gs in per_wave.items():
+            assert gs == sorted(gs), (w, gs)
+
+
+@pytest.mark.parametrize("ng", list(range(0, 70)))
+def test_local_sort_places_each_waves_first_two_groups(ng):
+    """The sort's LDS placement agrees with the deal: wave w's metadata area holds its
+    first group (slot w) and its staging area its second (slot 16 + w), reversed round 1
+    included; no area receives two groups."""
+    from kernel_model import vring_local_meta_area, vring_local_slot_group
+    W = 16
+    placed = {}
+    for g in range(ng):
+        a = vring_local_meta_area(g, ng, W)
+        if a is not None:
+            assert a not in placed, (a, g, placed[a])
+            placed[a] = g
+    for w in range(W):
+        for area, sl in (("M", w), ("X", W + w)):
+            g = vring_local_slot_group(sl, ng, W)
+            if g < ng:
+                assert placed.get((area, w)) == g, (area, w, g)
+            else:
+                assert (area, w) not in placed
+
+
+def test_local_round_one_reversal_balances_the_static_groups():
+    """Why round 1 is reversed: in a length-sorted tile, group g's packets get shorter
+    with g, so wave w's two static groups w and 16 + w are both long for w = 0; w and
+    31 - w sum to about the same for every wave."""
+    from kernel_model import vring_local_slot_group
+    W, ng = 16, 32
+    length = lambda g: 1400 - g * (1336 / (ng - 1))
+    plain = [length(w) + length(W + w) for w in range(W)]
+    rev = [length(vring_local_slot_group(w, ng)) + length(vring_local_slot_group(W + w, ng)) for w in range(W)]
+    assert max(plain) / min(plain) > 1.3
+    assert max(rev) / min(rev) < 1.001
+
+
+@pytest.mark.parametrize("kpk", [8, 16])
+@pytest.mark.parametrize("max_wgs", [256, 512])
+def test_local_tile_rule(kpk, max_wgs):
+    """vring_launch_local's tile: whole groups, at least a group per wave, at most 2048
+    packets (two per thread), a grid within max_wgs whose tiles cover the batch; the
+    default path falls back to the two-launch form exactly past 2048 x max_wgs."""
+    from kernel_model import vring_local_tile
+    for n in [1, 15, 16, 255, 256, 257, 5000, 65536, 262144, 602112, 2048 * max_wgs - 1, 2048 * max_wgs,
+              2048 * max_wgs + 1]:
+        r = vring_local_tile(n, max_wgs, kpk)
+        if n > 2048 * max_wgs:
+            assert r is None
+            continue
+        T, grid = r
+        assert T % kpk == 0 and kpk * 16 <= T <= 2048
+        assert grid <= max_wgs and (grid - 1) * T < n <= grid * T
