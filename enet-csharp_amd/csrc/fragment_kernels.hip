@@ -29,7 +29,8 @@
 //      descriptor.  Winners whose byte ranges may overlap another winner of the
 //      same slot are DEFERRED (status 2): the slot kernel checks, per slot, that
 //      the winners' ranges are disjoint and ascending in fragment-number order;
-//      the atomic kernel defers every slot with two or more winners;
+//      on the atomic path frag_clash_kernel runs the same check after the decide
+//      kernel, for the slots with two or more winners (round 6);
 //   3. the copy, 4 descriptors per wave as one flat space of 16-byte chunks:
 //      frag_copy_claims_kernel on the slots path (descriptors slot-major in claim
 //      space, written coalesced by the decide kernel: on a shuffled batch the
@@ -108,7 +109,8 @@ __global__ void __launch_bounds__(256) frag_claim_kernel(FragArgs a) {
 }
 
 // Thread per command: the claim winner tests-and-sets the bitmap bit (a bit set
-// by an earlier batch = duplicate) and decrements remaining; every command gets a
+// by an earlier batch = duplicate) and counts itself into its slot's winners
+// (frag_clash_kernel decrements remaining by that count); every command gets a
 // copy descriptor (len 0 = nothing to copy) for the copy kernel.
 // Reads the command as the claim kernel parsed it (no second parse of the arena).
 __global__ void __launch_bounds__(256) frag_decide_kernel(FragArgs a) {
@@ -125,8 +127,10 @@ __global__ void __launch_bounds__(256) frag_decide_kernel(FragArgs a) {
             const uint32_t old =
                 atomicOr(a.fragments + static_cast<uint64_t>(slot) * a.words + (number >> 5), bit);   // 619, 623
             if (!(old & bit)) {
-                atomicSub(a.remaining + slot, 1u);                       // --fragmentsRemaining (621)
-                atomicAdd(a.wcount + slot, 1u);                          // 2+ winners: the slot is deferred
+                // winners per slot: frag_clash_kernel takes them off fragmentsRemaining (621)
+                // with one subtraction per slot (a second contended atomic per winner cost
+                // more than the whole overlap check)
+                atomicAdd(a.wcount + slot, 1u);
                 a.status[i] = 1;
                 len = min(static_cast<uint32_t>(a.copy_src[i]), a.msg_len[slot] - offset);   // clamp (625-626)
                 src = a.cmd_off[i] + kCmdBytes;
@@ -211,6 +215,76 @@ __global__ void __launch_bounds__(256) frag_decide_slots_kernel(FragArgs a) {
     }
 }
 
+// The atomic decide path's overlap check (round 6).  Before, the atomic path deferred
+// every slot with two or more winners to the one-wave serial pass: a batch of ordinary
+// multi-fragment messages against a large claim space (a host that sizes its bitmaps
+// for its largest message) was copied one command at a time -- cfg5 with 64 bitmap
+// words per slot took 282 ms per call, against 0.15 ms on the slots path
+// (profiles/r06_frag/).  Now one wave per slot with two or more winners walks the
+// slot's claim words in fragment-number order, as frag_decide_slots_kernel does, but
+// only up to min(bits, fragmentCount) -- no command of a slot carries a number past its
+// fragmentCount (parse) -- and defers the slot's winners (status 2) only when their
+// byte ranges are not disjoint and ascending in number order.  The walk reads one
+// claim word per number, so a slot of more than 1024 numbers and over 64 per winner
+// (a few fragments of a huge message) is not walked: its winner count becomes
+// kDeferSlot and frag_copy_kernel defers its winners as before (the serial pass puts
+// the count back to 0).  Every other slot's winner count goes back to 0 here.
+constexpr uint32_t kClashWalkPerWinner = 64u;    // numbers walked per winner before deferring instead
+constexpr uint32_t kClashWalkFree = 1024u;       // numbers always walked
+constexpr uint32_t kDeferSlot = ~0u;             // winner count of a slot whose winners all go serial
+__global__ void __launch_bounds__(256) frag_clash_kernel(FragArgs a) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t waves = static_cast<uint64_t>(gridDim.x) * (blockDim.x >> 6);
+    const uint32_t bits = a.words << 5;
+    for (uint64_t sl = static_cast<uint64_t>(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6); sl < a.slot_count;
+         sl += waves) {
+        const uint32_t wc = a.wcount[sl];
+        if (wc == 0u) continue;
+        if (lane == 0u) a.remaining[sl] -= wc;             // --fragmentsRemaining per winner (621)
+        if (wc >= 2u) {
+            const uint32_t nb = min(bits, a.msg_count[sl]);
+            const uint64_t mo = a.msg_off[sl];
+            if (nb > max(kClashWalkFree, kClashWalkPerWinner * wc)) {   // too sparse to walk: defer them all
+                if (lane == 0u) a.wcount[sl] = kDeferSlot;
+                continue;
+            }
+            bool clash = false;
+            uint32_t mx = 0;                               // largest end of the slot's winners so far
+            for (uint32_t f0 = 0; f0 < nb && !clash; f0 += 64u) {
+                const uint32_t f = f0 + lane;
+                const uint32_t w = f < nb ? a.claim[sl * bits + f] : ~0u;
+                const bool take = w != ~0u && a.status[w] == 1;
+                if (!__ballot(take)) continue;
+                uint32_t offset = 0, end = 0;
+                if (take) {
+                    offset = static_cast<uint32_t>(a.copy_dst[w] - mo);
+                    end = offset + a.copy_len[w];
+                }
+                // exclusive prefix max of the winners' ends in fragment-number (lane) order
+                uint32_t pm = end;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t o = static_cast<uint32_t>(__shfl_up(static_cast<int>(pm), d));
+                    if (lane >= static_cast<uint32_t>(d)) pm = max(pm, o);
+                }
+                uint32_t before = static_cast<uint32_t>(__shfl_up(static_cast<int>(pm), 1));
+                before = lane ? max(before, mx) : mx;
+                if (__ballot(take && offset < before)) clash = true;
+                mx = max(mx, static_cast<uint32_t>(__shfl(static_cast<int>(pm), 63)));
+            }
+            if (clash) {                                   // the slot's winners to the serial pass, in batch order
+                for (uint32_t f0 = 0; f0 < nb; f0 += 64u) {
+                    const uint32_t f = f0 + lane;
+                    const uint32_t w = f < nb ? a.claim[sl * bits + f] : ~0u;
+                    if (w != ~0u && a.status[w] == 1) a.status[w] = 2;
+                }
+                if (lane == 0u) *a.deferred = 1u;
+            }
+        }
+        if (lane == 0u) a.wcount[sl] = 0u;                 // for the next batch
+    }
+}
+
 // Unaligned 16-byte access (gfx950 unaligned mode), both ways with the nontemporal
 // policy: every fragment byte is read once and written once, so neither side is worth
 // keeping in L2 (cfg5 151.1 against 159.7 us with the default policy,
@@ -255,10 +329,9 @@ __global__ void __launch_bounds__(256) frag_copy_kernel(FragArgs a) {
             if (L[c]) {
                 const int8_t st = a.status[i];
                 const uint64_t slot = ci / (static_cast<uint64_t>(a.words) << 5);
-                const uint32_t wc = a.wcount[slot];      // winners of the slot (atomic decide path)
-                defer = st == 2 || wc >= 2u;
+                // deferred by frag_clash_kernel: its own status, or its whole slot
+                defer = st == 2 || a.wcount[slot] == kDeferSlot;
                 if (lane == c) {
-                    if (wc == 1u) a.wcount[slot] = 0u;     // its only winner: reset for the next batch
                     if (defer && st != 2) {
                         a.status[i] = 2;
                         *a.deferred = 1u;
@@ -401,6 +474,8 @@ int fragment_reassemble_launch(const FragArgs& a, int num_cus, hipStream_t st) {
         hipLaunchKernelGGL(frag_copy_claims_kernel, dim3(g_q), dim3(256), 0, st, a, claim_space);
     } else {
         hipLaunchKernelGGL(frag_decide_kernel, dim3(g_thr), dim3(256), 0, st, a);
+        const unsigned g_clash = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>((a.slot_count + 3) / 4, cap)));
+        hipLaunchKernelGGL(frag_clash_kernel, dim3(g_clash), dim3(256), 0, st, a);
         hipLaunchKernelGGL(frag_copy_kernel, dim3(g_wave), dim3(256), 0, st, a);
     }
     hipLaunchKernelGGL(frag_serial_kernel, dim3(1), dim3(64), 0, st, a);

@@ -175,3 +175,33 @@ def test_fragments_scratch_layout_changes(ctx, oracle_lib):  # noqa: F811
         assert (run_gpu(ctx, fb, sg, sel) == run_oracle(oracle_lib, fb, so, sel)).all(), (slots, words)
         for k in ("msg_bytes", "fragments", "remaining"):
             assert (so[k] == sg[k]).all(), (slots, words, k)
+
+
+def test_fragments_atomic_path_many_fragment_messages(ctx, oracle_lib):  # noqa: F811
+    """Round 6: the atomic decide path checks each slot's winners for overlap
+    (frag_clash_kernel) instead of deferring every slot with two or more winners to the
+    serial pass.  Messages of 1563 fragments (mtu 96) against 64 bitmap words per slot
+    (60 slots x 2048 claim words > 8 n + 65536): a slot with a few of its fragments in a
+    batch is not walked (its winners stay serial), one with hundreds is walked, small
+    messages beside them, duplicates across batches -- every batch against the oracle."""
+    rng = np.random.default_rng(71)
+    lens = [100_000] * 4 + [int(x) for x in rng.integers(1, 5000, 56)]
+    fb = workloads.fragments(lens, mtu=96, seed=72, duplicates=0.1)
+    assert int(fb.msg_count.max()) == 1563
+    words = 64
+    so, sg = state(fb, words), state(fb, words)
+    slot = fb.slots
+    big = [np.flatnonzero(slot == m) for m in range(4)]
+    small = np.flatnonzero(slot >= 4)
+    batches = [
+        np.concatenate([big[0][:4], big[1][:800], small[:700]]),     # sparse slot 0, walked slot 1
+        np.concatenate([big[0][4:10], big[2][:3], small[700:]]),     # sparse slots 0 and 2
+        np.concatenate([big[1][800:], big[3], big[2][3:1500]]),      # walked 1, 2 and 3
+        np.concatenate([big[0][10:], big[2][1500:]]),
+    ]
+    for sel in batches:
+        sel = np.sort(sel)
+        assert not slots_path(len(lens) * 32 * words, len(sel)), len(sel)
+        assert (run_gpu(ctx, fb, sg, sel) == run_oracle(oracle_lib, fb, so, sel)).all()
+    for k in ("msg_bytes", "fragments", "remaining"):
+        assert (so[k] == sg[k]).all(), k

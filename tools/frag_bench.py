@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--in-order", action="store_true",
                     help="fragments in send order instead of shuffled (prices the scattered descriptor stores)")
     ap.add_argument("--words", type=int, default=2, help="bitmap words per message slot")
+    ap.add_argument("--copy-ref", action="store_true",
+                    help="also time a plain device-to-device copy of the same data bytes (torch copy_)")
     ap.add_argument("--first", type=int, default=0,
                     help="pass only the first N fragments (tiny batch against the whole slot table)")
     a = ap.parse_args()
@@ -77,6 +79,22 @@ def main():
                       "slots_path": claims <= 8 * nf + 65536, "data_bytes": fb.data_bytes,
                       "us_per_call": round(dt * 1e6, 2), "GBps_moved": round(moved / dt / 1e9, 1),
                       "hbm_frac": round(moved / dt / 8e12, 4), "ok": ok}), flush=True)
+    if a.copy_ref:                                # the chip's rate for a plain copy of the same bytes
+        src = torch.empty_like(d_msg).random_(0, 255)
+        rt = []
+        for r in range(a.reps + 2):
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(s):
+                e0.record(s)
+                d_msg.copy_(src)
+                e1.record(s)
+            torch.cuda.synchronize()
+            if r >= 2:
+                rt.append(e0.elapsed_time(e1) * 1e-3)
+        rd = float(np.median(rt))
+        print(json.dumps({"plain_copy_bytes": int(d_msg.numel()), "us": round(rd * 1e6, 2),
+                          "GBps_moved": round(2.0 * d_msg.numel() / rd / 1e9, 1)}), flush=True)
     ctx.close()
 
 
