@@ -106,7 +106,11 @@ ENET_HIP_API int enet_hip_is_diagnostics_build(void);
  * for that packet as a single ENetBuffer.  Inputs are read-only; `out` is
  * caller-allocated.  `stream` is a hipStream_t (NULL = ctx's stream, a blocking
  * stream: ordered after work on the legacy null stream, not after other non-blocking
- * streams).  Async: returns after the launch. */
+ * streams).  Async: returns after the launch.  Throughput comes from many packets
+ * at once: each packet is folded by the 8 (or 4) lanes of one wave, so a packet far
+ * longer than ENet's DGRAMs (ENET_PROTOCOL_MAXIMUM_MTU = 4096, include/protocol.cs:12)
+ * streams at one wave's rate -- checksum a lone multi-megabyte buffer with
+ * enet_hip_crc32 on the CPU instead. */
 ENET_HIP_API int enet_hip_crc32_batch_device(enet_hip_context* ctx, const uint8_t* bytes,
                                              const uint64_t* offsets, const uint32_t* lengths,
                                              size_t count, uint32_t* out, void* stream);
