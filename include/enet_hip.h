@@ -217,7 +217,10 @@ ENET_HIP_API int enet_hip_verify_batch_device_binned(enet_hip_context* ctx, cons
 /* ---- batched gather-list checksum (send path, c/protocol.cs:1690-1698) ----
  * DGRAM d is the concatenation of segments segFirst[d] .. segFirst[d+1]-1;
  * segment s is bytes[segOffsets[s] .. +segLengths[s]).  segFirst has
- * dgramCount+1 entries.  Device pointers, async. */
+ * dgramCount+1 entries.  Device pointers, async.  One lane per DGRAM: when the
+ * host knows the segment count, enet_hip_crc32_gather_binned_device below gives
+ * the same results 2.5x faster on cfg5 (60 against 152 us for 200 704 DGRAMs,
+ * profiles/r06_close/gather_both.log). */
 ENET_HIP_API int enet_hip_crc32_gather_device(enet_hip_context* ctx, const uint8_t* bytes,
                                               const uint64_t* segOffsets, const uint32_t* segLengths,
                                               const uint32_t* segFirst, size_t dgramCount, uint32_t* out,
