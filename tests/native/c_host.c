@@ -53,8 +53,12 @@ static uint32_t rnd(void) { /* xorshift64* */
 
 static void* dev_copy(enet_hip_context* ctx, const void* src, size_t bytes) {
     void* d = NULL;
-    CHECK(enet_hip_device_alloc(ctx, bytes ? bytes : 16, &d) == 0 && d, "device_alloc %zu", bytes);
-    if (bytes) CHECK(enet_hip_memcpy_h2d(ctx, d, src, bytes) == 0, "memcpy_h2d");
+    int rc = enet_hip_device_alloc(ctx, bytes ? bytes : 16, &d);
+    CHECK(rc == 0 && d, "device_alloc %zu: %d %s", bytes, rc, enet_hip_error_string(rc));
+    if (src && bytes) {                                 /* (src NULL: allocate only) */
+        rc = enet_hip_memcpy_h2d(ctx, d, src, bytes);
+        CHECK(rc == 0, "memcpy_h2d %zu: %d %s", bytes, rc, enet_hip_error_string(rc));
+    }
     return d;
 }
 
@@ -94,40 +98,47 @@ int main(void) {
     uint8_t* arena = (uint8_t*)malloc(arena_bytes);
     CHECK(arena != NULL, "malloc");
     for (size_t i = 0; i < arena_bytes; ++i) arena[i] = (uint8_t)rnd();
-    uint64_t off[N];
-    uint32_t len[N], want[N], out[N];
+    /* host arrays on the heap, as a host's packet tables would be */
+    uint64_t* off = (uint64_t*)calloc(N, sizeof *off);
+    uint32_t* len = (uint32_t*)calloc(N, sizeof *len);
+    uint32_t* want = (uint32_t*)calloc(N, sizeof *want);
+    uint32_t* out = (uint32_t*)calloc(2 * N, sizeof *out);
+    CHECK(off && len && want && out, "calloc");
     for (int i = 0; i < N; ++i) {
         len[i] = (uint32_t)i;
         off[i] = rnd() % (arena_bytes - 1600);
         want[i] = wire(bitwise_reg(0xFFFFFFFFu, arena + off[i], len[i]));
     }
     uint8_t* d_arena = (uint8_t*)dev_copy(ctx, arena, arena_bytes);
-    uint64_t* d_off = (uint64_t*)dev_copy(ctx, off, sizeof off);
-    uint32_t* d_len = (uint32_t*)dev_copy(ctx, len, sizeof len);
-    uint32_t* d_out = (uint32_t*)dev_copy(ctx, NULL, 2 * sizeof out);
+    uint64_t* d_off = (uint64_t*)dev_copy(ctx, off, N * sizeof *off);
+    uint32_t* d_len = (uint32_t*)dev_copy(ctx, len, N * sizeof *len);
+    uint32_t* d_out = (uint32_t*)dev_copy(ctx, NULL, 2 * N * sizeof *out);
 
     /* enet_hip_crc32_batch_device on the context's stream */
     CHECK(enet_hip_crc32_batch_device(ctx, d_arena, d_off, d_len, N, d_out, NULL) == 0, "batch_device");
     CHECK(enet_hip_synchronize(ctx) == 0, "synchronize");
-    CHECK(enet_hip_memcpy_d2h(ctx, out, d_out, sizeof out) == 0, "memcpy_d2h");
+    CHECK(enet_hip_memcpy_d2h(ctx, out, d_out, N * sizeof *out) == 0, "memcpy_d2h");
     for (int i = 0; i < N; ++i) CHECK(out[i] == want[i], "batch_device packet %d: %08x against %08x", i, out[i], want[i]);
 
     /* two batches in one launch: the second is the first half again, written after it */
     ENetHipBatch list[2] = {{d_arena, d_off, d_len, N, d_out}, {d_arena, d_off, d_len, N / 2, d_out + N}};
     CHECK(enet_hip_crc32_batch_list_device(ctx, list, 2, NULL) == 0, "batch_list_device");
     CHECK(enet_hip_synchronize(ctx) == 0, "synchronize");
-    uint32_t both[2 * N];
-    CHECK(enet_hip_memcpy_d2h(ctx, both, d_out, sizeof both) == 0, "memcpy_d2h");
-    for (int i = 0; i < N; ++i) CHECK(both[i] == want[i], "list batch 0 packet %d", i);
-    for (int i = 0; i < N / 2; ++i) CHECK(both[N + i] == want[i], "list batch 1 packet %d", i);
+    CHECK(enet_hip_memcpy_d2h(ctx, out, d_out, 2 * N * sizeof *out) == 0, "memcpy_d2h");
+    for (int i = 0; i < N; ++i) CHECK(out[i] == want[i], "list batch 0 packet %d", i);
+    for (int i = 0; i < N / 2; ++i) CHECK(out[N + i] == want[i], "list batch 1 packet %d", i);
 
     /* receive verify (c/protocol.cs:1052-1068): DGRAMs of >= 8 bytes carrying their CRC,
      * computed with connectID in the slot, in the slot; one in seven corrupted */
     enum { M = 1200 };
     uint8_t* dg = (uint8_t*)malloc((size_t)M * 1600);
-    uint64_t voff[M];
-    uint32_t vlen[M], slot[M], conn[M];
-    uint8_t expect_ok[M], ok[M];
+    uint64_t* voff = (uint64_t*)calloc(M, sizeof *voff);
+    uint32_t* vlen = (uint32_t*)calloc(M, sizeof *vlen);
+    uint32_t* slot = (uint32_t*)calloc(M, sizeof *slot);
+    uint32_t* conn = (uint32_t*)calloc(M, sizeof *conn);
+    uint8_t* expect_ok = (uint8_t*)calloc(M, 1);
+    uint8_t* ok = (uint8_t*)calloc(M, 1);
+    CHECK(dg && voff && vlen && slot && conn && expect_ok && ok, "calloc");
     for (int i = 0; i < M; ++i) {
         vlen[i] = 8u + (uint32_t)(rnd() % 1400u);
         voff[i] = (uint64_t)i * 1600u + (rnd() % 64u);
@@ -145,10 +156,10 @@ int main(void) {
         }
     }
     uint8_t* d_dg = (uint8_t*)dev_copy(ctx, dg, (size_t)M * 1600);
-    uint64_t* d_voff = (uint64_t*)dev_copy(ctx, voff, sizeof voff);
-    uint32_t* d_vlen = (uint32_t*)dev_copy(ctx, vlen, sizeof vlen);
-    uint32_t* d_slot = (uint32_t*)dev_copy(ctx, slot, sizeof slot);
-    uint32_t* d_conn = (uint32_t*)dev_copy(ctx, conn, sizeof conn);
+    uint64_t* d_voff = (uint64_t*)dev_copy(ctx, voff, M * sizeof *voff);
+    uint32_t* d_vlen = (uint32_t*)dev_copy(ctx, vlen, M * sizeof *vlen);
+    uint32_t* d_slot = (uint32_t*)dev_copy(ctx, slot, M * sizeof *slot);
+    uint32_t* d_conn = (uint32_t*)dev_copy(ctx, conn, M * sizeof *conn);
     uint8_t* d_ok = (uint8_t*)dev_copy(ctx, NULL, M);
     CHECK(enet_hip_verify_batch_device(ctx, d_dg, d_voff, d_vlen, d_slot, d_conn, M, d_ok, NULL, NULL) == 0,
           "verify_batch_device");
@@ -160,7 +171,7 @@ int main(void) {
     uint8_t* pinned = NULL;
     CHECK(enet_hip_host_alloc(arena_bytes, (void**)&pinned) == 0 && pinned, "host_alloc");
     memcpy(pinned, arena, arena_bytes);
-    memset(out, 0, sizeof out);
+    memset(out, 0, N * sizeof *out);
     CHECK(enet_hip_crc32_batch_host(ctx, pinned, arena_bytes, off, len, N, out) == 0, "batch_host");
     for (int i = 0; i < N; ++i) CHECK(out[i] == want[i], "batch_host packet %d", i);
 
@@ -175,6 +186,16 @@ int main(void) {
     CHECK(enet_hip_context_destroy(ctx) == 0, "context_destroy");
     free(arena);
     free(dg);
+    free(off);
+    free(len);
+    free(want);
+    free(out);
+    free(voff);
+    free(vlen);
+    free(slot);
+    free(conn);
+    free(expect_ok);
+    free(ok);
     printf("c_host: ok (device)\n");
     return 0;
 }

@@ -3,5 +3,6 @@ set -o pipefail
 out=gpurun_out/r6x
 mkdir -p $out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+ulimit -s > $out/stack_limit.txt
 tools/gpu_step.sh 300 $out/pytest_c_host.log python -u -m pytest tests/test_c_host.py -v --timeout 120 --timeout-method thread || exit 1
 touch $out/done
