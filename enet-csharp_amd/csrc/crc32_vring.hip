@@ -702,7 +702,8 @@ struct VrIt {
 // XORs the prepared dwords) -- both wrong CRCs by design; bit 2 = each stage's
 // wait also retires the stage just issued (no load in flight during a fold); bit 3
 // = 128-byte window starts and line-shaped stage loads (wrong CRCs by design);
-// bit 4 = no end-of-packet corrections (wrong CRCs by design)
+// bit 4 = no end-of-packet corrections (wrong CRCs by design); bit 5 (8 lanes) = each
+// produce runs at s_setprio 3, the rest of the turn at 0 (correct CRCs; round 6 probe)
 // BIN = 1: the batch's metadata are length-binned records (VrBatch::off points at
 // them, 4 dwords per packet), read in record order; packet r's CRC goes to
 // out[record r's index] (enet_hip_crc32_batch_device_binned).  One workgroup per CU;
@@ -1138,6 +1139,7 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
     auto produce = [&](auto slot_c, auto ws_c) __attribute__((always_inline)) {
         constexpr uint32_t slot = decltype(slot_c)::value;
         constexpr int WS = decltype(ws_c)::value;
+        if constexpr ((ABL & 32) != 0) __builtin_amdgcn_s_setprio(3);
         if (!pdone && pst == pstages) {
             if (qlive) {
                 // group qit's metadata was issued before the last produce's two stage
@@ -1185,6 +1187,7 @@ crc32_vring_kernel(std::conditional_t<VF != 0, VrVBatches, VrBatches> bl, Kernel
             vr_issue_stage<slot, NT>(s0, s1);
             if constexpr (WS >= 0) vr_wait_stage<(ABL & 4) ? 0 : 2>();
         }
+        if constexpr ((ABL & 32) != 0) __builtin_amdgcn_s_setprio(0);
         ++pst;
     };
     if (any) {
@@ -1554,6 +1557,7 @@ const void* vring_pick(int lg, bool trace, const VrVariant& v) {
     if (abl == 19 && !nt) return lg == 2 ? vring_fn<2, 0, 0, 19>() : vring_fn<3, 0, 0, 19>();
     if (abl == 2 && lg == 3 && !nt) return vring_fn<3, 0, 0, 2>();
     if (abl == 32 && lg == 2) return nt ? vring_fn<2, 0, 3>() : vring_fn<2, 0, 2>();   // sc1 / sc0 sc1
+    if (abl == 32 && lg == 3 && !nt) return vring_fn<3, 0, 0, 32>();                     // produce at s_setprio 3
     if (lg == 2 && !nt) {
         switch (abl) {
             case 1: return vring_fn<2, 0, 0, 1>();

@@ -467,7 +467,8 @@ ENET_HIP_API int enet_hip_read_probe_device(enet_hip_context* ctx, const uint8_t
  * 2048 + 4096 + 32768 (4 lanes): no masks, lookups or end-of-packet
  * corrections (WRONG checksums: the kernel's memory and control skeleton);
  * 65536 (4 lanes, correct checksums): the stage loads with the sc1 (path 17)
- * or sc0 sc1 (path 18) cache policy; 262144: the vring's end-record trace
+ * or sc0 sc1 (path 18) cache policy; at 8 lanes on path 17 (correct checksums): each
+ * stage's loads issued at s_setprio 3; 262144: the vring's end-record trace
  * instance (with enet_hip_diag_trace).  Also on the linear-stream paths 22 / 23:
  * 2048 = no boundary passes, 2048 + 4096 = no fold lookups either (WRONG
  * checksums).  524288 (correct checksums): the vring's dynamic rounds (rounds
