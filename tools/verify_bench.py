@@ -12,6 +12,7 @@ timed beside it.  ok[] and computed[] are checked against the oracle on batch 0.
 
     python tools/verify_bench.py [--reps 100] [--lanes 0] [--list 5]
 
+verify_noslot times the same call with every slot offset past its DGRAM (no slot work).
 --list L also times enet_hip_verify_batch_list_device over L consecutive rotating
 batches per call (per-batch time = call time / L), each batch's ok[] / computed[]
 in its own slice, checked against batch 0's single call.
@@ -81,6 +82,13 @@ def main():
                                        lok[t * N:(t + 1) * N], lcomp[t * N:(t + 1) * N]) for t in range(a.list)],
                                      st.cuda_stream)
 
+    # the same call with every slot offset past its DGRAM: no slot to substitute or collect
+    # (ok = 0 everywhere) -- what the slot handling costs
+    d_noslot = torch.full((N,), 0x7FFFFF00, dtype=torch.int32, device="cuda")
+
+    def verify_noslot(i):
+        ctx.verify_batch_device(batches[i % a.rotate], d_off, d_len, d_noslot, d_conn, N, ok, comp, st.cuda_stream)
+
     def checksum(i):
         ctx.crc32_batch_device(batches[i % a.rotate], d_off, d_len, N, crc, st.cuda_stream)
 
@@ -116,7 +124,8 @@ def main():
 
     res = {"kind": "verify-bench", "path": a.path, "list": a.list, "dgrams": N, "bytes_per_batch": N * L, "lanes": a.lanes or "default",
            "bit_exact_vs_oracle": exact, "ok_count": int(exp_ok.sum())}
-    fns = [("verify", verify, 1), ("checksum", checksum, 1)] + ([("verify_list", vlist, a.list)] if a.list else [])
+    fns = [("verify", verify, 1), ("verify_noslot", verify_noslot, 1), ("checksum", checksum, 1)] + \
+        ([("verify_list", vlist, a.list)] if a.list else [])
     for name, fn, per in fns:
         us = region_us(fn) / per
         res[name + "_us"] = round(us, 2)
